@@ -1,0 +1,204 @@
+"""Deterministic synthetic inputs for the BASELINE.json workloads.
+
+* ``xorshift32`` / ``random_bytes`` / ``ramp``: the reference's own fuzz generators
+  (test/brotli.test.ts:247-260), bit-for-bit.
+* ``fox``: the reference's encode bench input (bench/encode.bench.ts:7-8,14).
+* ``enwik_text``: MediaWiki-XML-like text ("enwik-style"): <page> records with titles, ids,
+  timestamps and a word-salad body drawn from the English word frequencies of the
+  canonical corpus texts (data/words.txt), with [[links]], {{templates}}, '''bold''',
+  &quot; entities and ~1/16 newlines.  Vectorised numpy; deterministic for a given
+  (seed, length) on a given numpy version.
+* ``glyf_stream``: WOFF2-transformed-glyf-like byte streams (see its docstring).
+"""
+import os
+
+import numpy as np
+
+_DATA = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), 'data')
+
+
+def xorshift32(seed):
+    """makeXorshift32 (test/brotli.test.ts:247-255)."""
+    x = seed & 0xFFFFFFFF
+
+    def nxt():
+        nonlocal x
+        x ^= (x << 13) & 0xFFFFFFFF
+        x ^= x >> 17
+        x ^= (x << 5) & 0xFFFFFFFF
+        return x
+    return nxt
+
+
+def random_bytes(length, nxt):
+    """randomBytes (test/brotli.test.ts:257-261)."""
+    return bytes(nxt() & 0xFF for _ in range(length))
+
+
+def ramp(length):
+    return bytes(i & 0xFF for i in range(length))
+
+
+def fox(repeats=1000):
+    return b'The quick brown fox jumps over the lazy dog. ' * repeats
+
+
+_WORDS = None
+
+
+def _words():
+    global _WORDS
+    if _WORDS is None:
+        words, counts = [], []
+        with open(os.path.join(_DATA, 'words.txt'), encoding='utf-8') as f:
+            for line in f:
+                if line.startswith('#'):
+                    continue
+                w, c = line.rstrip('\n').split('\t')
+                words.append(w)
+                counts.append(int(c))
+        p = np.asarray(counts, dtype=np.float64)
+        _WORDS = (words, np.cumsum(p) / p.sum())
+    return _WORDS
+
+
+def _pieces_table(pieces):
+    blob = b''.join(pieces)
+    lens = np.fromiter((len(p) for p in pieces), dtype=np.int64, count=len(pieces))
+    starts = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    return np.frombuffer(blob, dtype=np.uint8), starts, lens
+
+
+def _gather(flat, starts, lens, ids):
+    ln = lens[ids]
+    total = int(ln.sum())
+    out_off = np.cumsum(ln) - ln
+    idx = np.repeat(starts[ids] - out_off, ln) + np.arange(total, dtype=np.int64)
+    return flat[idx]
+
+
+def enwik_text(length, seed=1):
+    """``length`` bytes of enwik-style MediaWiki XML."""
+    words, cdf = _words()
+    rng = np.random.default_rng(0x5EED0000 + seed)
+    nw = len(words)
+    caps = [w[:1].upper() + w[1:] for w in words]
+    seps = [b' ', b', ', b'. ', b'.\n', b'\n', b'; ', b' (', b') ', b': ', b'\n\n']
+    sep_p = np.array([0.80, 0.06, 0.05, 0.015, 0.035, 0.01, 0.008, 0.008, 0.007, 0.007])
+    sep_p /= sep_p.sum()
+    marks = [(b'', b''), (b'[[', b']]'), (b'{{', b'}}'), (b"'''", b"'''"), (b'&quot;', b'&quot;'), (b'[[Category:', b']]')]
+    mark_p = np.array([0.925, 0.045, 0.006, 0.012, 0.008, 0.004])
+    mark_p /= mark_p.sum()
+    # pre-rendered page headers (titles / ids / timestamps vary per header)
+    headers = []
+    for h in range(512):
+        t = rng.integers(0, min(nw, 3000), size=3)
+        title = ' '.join(caps[i] for i in t[: 1 + h % 3])
+        pid = int(rng.integers(1, 10 ** 7))
+        rid = int(rng.integers(10 ** 7, 10 ** 9))
+        user = caps[int(rng.integers(0, min(nw, 5000)))]
+        ts = '20%02d-%02d-%02dT%02d:%02d:%02dZ' % tuple(int(v) for v in rng.integers([1, 1, 1, 0, 0, 0], [9, 13, 29, 24, 60, 60]))
+        headers.append(('</text>\n    </revision>\n  </page>\n  <page>\n    <title>%s</title>\n    <ns>0</ns>\n'
+                        '    <id>%d</id>\n    <revision>\n      <id>%d</id>\n      <timestamp>%s</timestamp>\n'
+                        '      <contributor>\n        <username>%s</username>\n        <id>%d</id>\n'
+                        '      </contributor>\n      <text xml:space="preserve">' % (
+                            title, pid, rid, ts, user, pid % 99991)).encode())
+    # piece ids: [0] empty, words, capitalised words, separators, mark prefixes, mark suffixes, headers
+    pieces = [b''] + [w.encode() for w in words] + [c.encode() for c in caps] + seps
+    pieces += [m[0] for m in marks] + [m[1] for m in marks] + headers
+    W0, C0 = 1, 1 + nw
+    S0 = C0 + nw
+    MP0 = S0 + len(seps)
+    MS0 = MP0 + len(marks)
+    H0 = MS0 + len(marks)
+    flat, starts, lens = _pieces_table(pieces)
+    out = [b'<mediawiki xml:lang="en">\n  <page>\n    <title>Start</title>\n    <text xml:space="preserve">']
+    have = len(out[0])
+    while have < length:
+        n = max(4096, (length - have) // 5)
+        wid = np.searchsorted(cdf, rng.random(n))
+        sep = rng.choice(len(seps), size=n, p=sep_p)
+        # capitalise after a sentence end
+        cap = np.zeros(n, dtype=bool)
+        cap[1:] = (sep[:-1] == 2) | (sep[:-1] == 3) | (sep[:-1] == 9)
+        word_piece = np.where(cap, C0 + wid, W0 + wid)
+        mk = rng.choice(len(marks), size=n, p=mark_p)
+        pre = np.where(mk > 0, MP0 + mk, 0)
+        suf = np.where(mk > 0, MS0 + mk, 0)
+        sep_piece = S0 + sep
+        page_break = rng.random(n) < 1.0 / 900
+        sep_piece = np.where(page_break, H0 + rng.integers(0, len(headers), size=n), sep_piece)
+        ids = np.stack([pre, word_piece, suf, sep_piece], axis=1).reshape(-1)
+        chunk = _gather(flat, starts, lens, ids).tobytes()
+        out.append(chunk)
+        have += len(chunk)
+    return b''.join(out)[:length]
+
+
+def enwik_batch(count, length, seed0):
+    """``count`` independent buffers (seeds seed0 .. seed0+count-1)."""
+    return [enwik_text(length, seed0 + i) for i in range(count)]
+
+
+def glyf_stream(length, seed=1000):
+    """WOFF2 §5.1 transformed-glyf-like stream: nContour (int16 BE per glyph), nPoints
+    (255UInt16 per contour), flags (1 byte / point), triplet-coded glyph coordinates,
+    composite records, bbox bitmap + bbox stream and instructions, concatenated in the
+    WOFF2 stream order.  Glyph shapes follow a typical text face: 1-4 contours, 4-40
+    points per contour, mostly on-curve short deltas."""
+    rng = np.random.default_rng(0x61F0000 + seed)
+    # estimate glyph count from the target length (about 95 bytes per glyph on average)
+    g = max(16, length // 95)
+    ncont = rng.choice([0, 1, 2, 3, 4], size=g, p=[0.04, 0.46, 0.32, 0.13, 0.05])
+    ncont_stream = ncont.astype('>i2').tobytes()
+    npts = rng.integers(4, 40, size=int(ncont.sum()))
+    npts_stream = bytearray()
+    for v in npts:
+        v = int(v)
+        if v < 253:
+            npts_stream.append(v)
+        else:
+            npts_stream += bytes([253, v >> 8, v & 0xFF])
+    tot = int(npts.sum())
+    on_curve = rng.random(tot) < 0.6
+    dx = np.rint(rng.normal(0, 40, tot)).astype(np.int64)
+    dy = np.rint(rng.normal(0, 40, tot)).astype(np.int64)
+    flags = bytearray(tot)
+    glyph = bytearray()
+    for i in range(tot):
+        x, y = int(dx[i]), int(dy[i])
+        ax, ay = abs(x), abs(y)
+        if x == 0 and ay < 1280:
+            f = 0 + ((ay >> 8) << 1) + (1 if y >= 0 else 0)
+            glyph.append(ay & 0xFF)
+        elif y == 0 and ax < 1280:
+            f = 10 + ((ax >> 8) << 1) + (1 if x >= 0 else 0)
+            glyph.append(ax & 0xFF)
+        elif ax <= 64 and ay <= 64:
+            f = 20 + ((ax - 1) & 0x30) + (((ay - 1) & 0x30) >> 2) + (2 if x >= 0 else 0) + (1 if y >= 0 else 0)
+            glyph.append((((ax - 1) & 0xF) << 4) | ((ay - 1) & 0xF))
+        elif ax <= 768 and ay <= 768:
+            f = 84 + 12 * (((ax - 1) >> 8) & 3) + ((((ay - 1) >> 8) & 3) << 2) + (2 if x >= 0 else 0) + (1 if y >= 0 else 0)
+            glyph += bytes([(ax - 1) & 0xFF, (ay - 1) & 0xFF])
+        else:
+            f = 120 + (2 if x >= 0 else 0) + (1 if y >= 0 else 0)
+            glyph += bytes([(ax >> 4) & 0xFF, ((ax & 0xF) << 4) | ((ay >> 8) & 0xF), ay & 0xFF])
+        flags[i] = (f & 0x7F) | (0 if on_curve[i] else 0x80)
+    # instruction lengths (255UInt16 per simple glyph) go to the glyph stream, bodies to instructions
+    simple = int((ncont > 0).sum())
+    ilen = rng.integers(0, 60, size=simple)
+    for v in ilen:
+        glyph.append(int(v))
+    instr = rng.integers(0, 256, size=int(ilen.sum()), dtype=np.uint8)
+    instr[::3] = rng.choice([0x40, 0x41, 0x1D, 0x1E, 0x2B, 0x5D, 0xB0, 0xB8], size=instr[::3].shape)
+    comp = int((ncont == 0).sum())
+    composite = bytearray()
+    for _ in range(comp):
+        composite += bytes([0x00, 0x23, 0, int(rng.integers(0, 255)), int(rng.integers(0, 64)), int(rng.integers(0, 64)),
+                            0x00, 0x22, 0, int(rng.integers(0, 255)), 0, 0])
+    bbox_bitmap = bytes(((g + 31) >> 5) << 2)
+    bbox = rng.integers(-200, 1800, size=4 * max(1, g // 20)).astype('>i2').tobytes()
+    out = ncont_stream + bytes(npts_stream) + bytes(flags) + bytes(glyph) + bytes(composite) + bbox_bitmap + bbox + instr.tobytes()
+    if len(out) < length:
+        out = (out * (length // max(1, len(out)) + 1))
+    return out[:length]

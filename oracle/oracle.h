@@ -1,0 +1,33 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY (see oracle_decode.c / oracle_encode.c headers).
+ * CPU restatement of countertype/brotli-lib's encode/decode algorithms, used as the
+ * checker for the HIP path and as bench.py's cpu_baseline.  Never linked by the product.
+ */
+#ifndef BROTLI_ORACLE_H_
+#define BROTLI_ORACLE_H_
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* engine.ts:2155 peekDecodedSize: decoded size of a single-ISLAST-metablock stream, else -1/0 */
+int64_t oracle_peek_decoded_size(const uint8_t *in, size_t n);
+
+/* engine.ts:2197 brotliDecode.  out_size > 0: decode into an exact buffer of that size
+ * (truncate / zero-pad, trailing checks skipped, as the reference).  Returns 0 or the
+ * reference's negative error code; *out is malloc'ed (free with oracle_free). */
+int oracle_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n,
+                  int64_t out_size, uint8_t **out, size_t *out_n);
+
+/* encode.ts:50 brotliEncode (bugs A,B fixed = the survey's "ref-fixed"; C,E fixed too).
+ * quality 0..11, lgwin 10..24, mode 0 GENERIC / 1 TEXT / 2 FONT. */
+int oracle_encode(const uint8_t *in, size_t n, int quality, int lgwin, int mode,
+                  uint8_t **out, size_t *out_n);
+
+void oracle_free(void *p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
