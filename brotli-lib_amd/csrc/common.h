@@ -1,0 +1,27 @@
+// Shared host/device definitions of the brotli_amd engine (job descriptors, status codes).
+#pragma once
+#include <stdint.h>
+
+#include "../../include/brotli_amd.h"
+
+namespace mib {
+
+// One stream to decode.  Filled by the host, read/written by decode kernels.
+struct DecJob {
+  const uint8_t *in;      // compressed stream (device)
+  uint64_t in_len;
+  uint8_t *out;           // output window (device), capacity out_cap (+64 B slack owned by us)
+  uint64_t out_cap;
+  int64_t out_size;       // > 0: known-size mode (brotliDecode pre-sizing / legacy outputSize)
+  const uint8_t *dict;    // compound dictionary (device) or null
+  uint64_t dict_len;
+  int64_t result_len;     // out: bytes produced
+  int32_t status;         // out: 0, reference error code, or MIB_E_*
+  int32_t max_ring_log;   // window bits from the stream header (host peek), sizes scratch
+};
+
+constexpr int kDecodeBlock = 64;                    // one wave per stream
+constexpr uint64_t kDecodeTableInts = 256u * (1 + 630) + 256u * (1 + 1080) + 256u * (1 + 1080) + 64;
+constexpr uint64_t kDecodeCtxBytes = 256u * 64 + 256u * 4 + 256;
+
+}  // namespace mib

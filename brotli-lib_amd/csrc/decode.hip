@@ -1,0 +1,1267 @@
+// brotli_amd: RFC 7932 stream decoder for gfx950, one wave (64 lanes) per stream.
+//
+// Semantics are those of the reference decoder (countertype/brotli-lib
+// src/decode/engine.ts, a port of Google's Java decoder) so that output bytes AND error
+// codes are identical, including on corrupted input:
+//   * the 4,160-byte input window refilled when halfOffset > 2030 (engine.ts:1764-1790),
+//     kept here in LDS and refilled cooperatively by the wave; its stale bytes after the
+//     end of input decide which error a truncated stream raises;
+//   * the ring buffer sized by maybeReallocateRingBuffer (:608-630), flushed at the fence
+//     (:1477-1497) into the output, kept in a per-block HBM scratch slice;
+//   * the command / literal / distance / copy state machine of decompress (:1012-1517),
+//     including its literal batching (:1166, :1221) -- with Bug J fixed (a zero
+//     batch after end of input spins forever in the reference);
+//   * brotliDecode's output modes (:2197-2257): a known size (one pass, truncate/zero-pad,
+//     trailing checks skipped) or chunks of 16 KiB doubling to 4 MiB.
+//
+// GPU mapping: the bit-serial part (Huffman symbol reads) runs wave-uniform -- every lane
+// computes the same state, reads broadcast from LDS/L1 -- and the byte-parallel parts
+// (window refill, Huffman table replication, LZ77 copies, uncompressed copies, ring
+// flushes) are spread over the 64 lanes.  Parallelism across streams comes from the grid:
+// a persistent grid of one-wave workgroups walks the job list.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#define RFC_CONST static __device__ const
+#include "rfc_tables.h"
+
+namespace mib {
+
+__device__ const uint8_t kDictionary[RFC_DICT_SIZE] = {
+#include "rfc_dictionary.inc"
+};
+
+__constant__ int16_t kCmdLut[704 * 4];   // engine.ts:65-90, filled by the host at init
+
+static __device__ const int kMaxHuffTable[23] = {256, 402, 436, 468, 500, 534, 566, 598, 630, 662, 694, 726,
+                                                 758, 790, 822, 854, 886, 920, 952, 984, 1016, 1048, 1080};
+static __device__ const uint8_t kCodeLenOrder[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+static __device__ const int8_t kDistIdxOff[16] = {0, 3, 2, 1, 0, 0, 0, 0, 0, 0, 3, 3, 3, 3, 3, 3};
+static __device__ const int8_t kDistValOff[16] = {0, 0, 0, 0, -1, 1, -2, 2, -3, 3, -1, 1, -2, 2, -3, 3};
+static __device__ const int kFixedCL[16] = {0x020000, 0x020004, 0x020003, 0x030002, 0x020000, 0x020004,
+                                            0x020003, 0x040001, 0x020000, 0x020004, 0x020003, 0x030002,
+                                            0x020000, 0x020004, 0x020003, 0x040005};
+static __device__ const int kBlockLenOff[26] = {1, 5, 9, 13, 17, 25, 33, 41, 49, 65, 81, 97, 113,
+                                                145, 177, 209, 241, 305, 369, 497, 753, 1265, 2289, 4337, 8433, 16625};
+static __device__ const int8_t kBlockLenBits[26] = {2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 7, 8, 9, 10, 11, 12, 13, 24};
+
+enum : int {
+  ST_INITED = 1, ST_BLOCK_START = 2, ST_COMPRESSED_BLOCK_START = 3, ST_MAIN_LOOP = 4, ST_READ_METADATA = 5,
+  ST_COPY_UNCOMPRESSED = 6, ST_INSERT_LOOP = 7, ST_COPY_LOOP = 8, ST_USE_DICTIONARY = 9, ST_FINISHED = 10,
+  ST_INIT_WRITE = 12, ST_WRITE = 13, ST_COPY_FROM_COMPOUND = 14
+};
+
+constexpr int kBlockTreesCap = 3091;   // engine.ts:163 Int32Array(3091)
+
+// LDS working set of one stream (one wave).
+struct Lds {
+  uint8_t win[4160 + 64];    // byteBuffer (4160) + read slack
+  int lens[1080];            // code lengths scratch
+  uint16_t sorted[1080];
+  int32_t cl_table[33];
+  int32_t ctx_tree_base[64];
+  uint8_t mtf[256];
+  int32_t block_trees[kBlockTreesCap + 1];
+};
+
+struct Dec {
+  // input
+  const uint8_t *in;
+  uint64_t in_len, in_off;
+  uint32_t acc;
+  int bo, ho, tail, eos;
+  // state
+  int running, next_running;
+  uint8_t *ring;
+  int ring_cap, ring_size, max_ring, max_back, max_dist, expected_total, pos;
+  int mbl, input_end, is_uncompressed, is_metadata;
+  int lit_blen, n_lit_types, cmd_blen, n_cmd_types, dist_blen, n_dist_types;
+  int rings[10], dist_rb_idx;
+  int32_t *lit_group, *cmd_group, *dist_group;   // HBM scratch
+  uint8_t *ctx_modes, *ctx_map, *dist_ctx_map;   // HBM scratch
+  int trivial_lit_ctx, lit_tree_idx, cmd_tree_idx;
+  int j, insert_len, copy_len, dist_code, distance;
+  int ctx_map_slice, dist_ctx_map_slice, clo1, clo2;
+  int npostfix, ndirect;
+  // output (virtual 16 KiB..4 MiB chunks of the reference's unknown-size mode)
+  uint8_t *out;
+  int64_t out_cap, out_flushed, chunk_start, chunk_size;
+  int known_size;
+  int rb_written, rb_ready;
+  // compound dictionary
+  const uint8_t *cd;
+  int cd_total, cd_br_offset, cd_br_length, cd_br_copied, cd_br_index;
+  int lane;
+  Lds *l;
+  uint64_t guard, guard_limit;
+};
+
+#define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
+
+__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+
+// ---------------------------------------------------------------- bit reader
+__device__ __forceinline__ uint32_t half_at(const Dec &s, int h) {
+  if (h < 0 || h >= 2080) return 0;   // Int16Array(2080): undefined -> 0
+  return (uint32_t)s.l->win[2 * h] | ((uint32_t)s.l->win[2 * h + 1] << 8);
+}
+__device__ __forceinline__ void fill16(Dec &s) {
+  if (s.bo >= 16) {
+    s.acc = (half_at(s, s.ho++) << 16) | (s.acc >> 16);
+    s.bo -= 16;
+  }
+}
+__device__ __forceinline__ void force16(Dec &s) {
+  s.acc = (half_at(s, s.ho++) << 16) | (s.acc >> 16);
+  s.bo -= 16;
+}
+__device__ __forceinline__ uint32_t peek(const Dec &s) { return s.acc >> (s.bo & 31); }
+__device__ __forceinline__ int bits(Dec &s, int n) {
+  int v = (int)(peek(s) & ((1u << n) - 1u));
+  s.bo += n;
+  return v;
+}
+__device__ __forceinline__ int many_bits(Dec &s, int n) {
+  int lo = bits(s, 16);
+  force16(s);
+  return lo | (bits(s, n - 16) << 16);
+}
+__device__ int half_available(const Dec &s) {
+  int limit = s.eos ? (s.tail + 1) >> 1 : 2048;
+  return limit - s.ho;
+}
+
+// readMoreInput (engine.ts:1764-1790): LDS memmove + HBM -> LDS fill, by the whole wave.
+__device__ int read_more_input(Dec &s) {
+  if (s.eos) return half_available(s) >= -2 ? 0 : ERR(s, -16);
+  int ro = s.ho << 1;
+  int have = 4096 - ro;
+  if (have < 0) return MIB_E_JS_RANGE_ERROR;
+  uint16_t tmp[32];
+  const uint16_t *w16 = reinterpret_cast<const uint16_t *>(s.l->win);
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    int idx = s.lane + 64 * k;
+    tmp[k] = (2 * idx < have) ? w16[(ro >> 1) + idx] : 0;
+  }
+  wave_sync();
+  uint16_t *wo = reinterpret_cast<uint16_t *>(s.l->win);
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    int idx = s.lane + 64 * k;
+    if (2 * idx < have) wo[idx] = tmp[k];
+  }
+  wave_sync();
+  s.ho = 0;
+  uint64_t avail = s.in_len - s.in_off;
+  int n = (uint64_t)(4096 - have) < avail ? 4096 - have : (int)avail;
+  for (int i = s.lane; i < n; i += 64) s.l->win[have + i] = s.in[s.in_off + i];
+  wave_sync();
+  s.in_off += (uint64_t)n;
+  have += n;
+  if (have < 4096) {
+    s.eos = 1;
+    s.tail = have;
+  }
+  return 0;
+}
+#define MAYBE_REFILL(s)                       \
+  do {                                        \
+    if ((s).ho > 2030) {                      \
+      int r_ = read_more_input(s);            \
+      if (r_ < 0) return r_;                  \
+    }                                         \
+  } while (0)
+
+__device__ int check_health(Dec &s, int end_of_stream) {
+  if (!s.eos) return 0;
+  int byte_off = (s.ho << 1) + ((s.bo + 7) >> 3) - 4;
+  if (byte_off > s.tail) return ERR(s, -13);
+  if (end_of_stream && byte_off != s.tail) return ERR(s, -17);
+  return 0;
+}
+__device__ int prepare(Dec &s) {
+  MAYBE_REFILL(s);
+  int h = check_health(s, 0);
+  if (h) return h;
+  force16(s);
+  force16(s);
+  return 0;
+}
+__device__ int jump_to_byte_boundary(Dec &s) {
+  int pad = (32 - s.bo) & 7;
+  if (pad && bits(s, pad) != 0) return ERR(s, -5);
+  return 0;
+}
+
+// ---------------------------------------------------------------- Huffman tables (engine.ts:1677-1762)
+__device__ int next_key(int key, int len) {
+  int step = 1 << (len - 1);
+  while (key & step) step >>= 1;
+  return (key & (step - 1)) + step;
+}
+// group[off + p] = item for p = end - step, end - 2 step, ..., 0 ; lanes split the writes
+__device__ __forceinline__ void replicate(const Dec &s, int32_t *g, int cap, int off, int step, int end, int item) {
+  int n = end / step;
+  for (int k = s.lane; k < n; k += 64) {
+    int i = off + k * step;
+    if (i < cap) g[i] = item;
+  }
+}
+__device__ int build_table(Dec &s, int32_t *group, int cap, int idx, int root, const int *lens, int nsym) {
+  int toff = group[idx];
+  int count[16], offset[16];
+  for (int i = 0; i < 16; i++) count[i] = offset[i] = 0;
+  for (int i = 0; i < nsym; i++) count[lens[i]]++;
+  offset[1] = 0;
+  for (int l = 1; l < 15; l++) offset[l + 1] = offset[l] + count[l];
+  uint16_t *sorted = s.l->sorted;
+  wave_sync();
+  if (s.lane == 0)
+    for (int i = 0; i < nsym; i++)
+      if (lens[i]) sorted[offset[lens[i]]++] = (uint16_t)i;
+  for (int i = 0; i < nsym; i++)   // uniform copy of the per-length running offsets
+    if (lens[i]) offset[lens[i]]++;
+  wave_sync();
+  int tbits = root, tsize = 1 << tbits, total = tsize;
+  if (offset[15] == 1) {
+    replicate(s, group, cap, toff, 1, total, sorted[0]);
+    wave_sync();
+    return total;
+  }
+  int key = 0, sym = 0, step = 1;
+  for (int l = 1; l <= root; l++) {
+    step <<= 1;
+    for (; count[l] > 0; count[l]--) {
+      replicate(s, group, cap, toff + key, step, tsize, (l << 16) | sorted[sym++]);
+      key = next_key(key, l);
+    }
+  }
+  wave_sync();
+  int mask = total - 1, low = -1, cur = toff;
+  step = 1;
+  for (int l = root + 1; l <= 15; l++) {
+    step <<= 1;
+    for (; count[l] > 0; count[l]--) {
+      if ((key & mask) != low) {
+        cur += tsize;
+        // nextTableBitSize
+        int b = l, left = 1 << (b - root);
+        while (b < 15) {
+          left -= count[b];
+          if (left <= 0) break;
+          b++;
+          left <<= 1;
+        }
+        tbits = b - root;
+        tsize = 1 << tbits;
+        total += tsize;
+        low = key & mask;
+        if (s.lane == 0 && toff + low < cap) group[toff + low] = ((tbits + root) << 16) | (cur - toff - low);
+      }
+      replicate(s, group, cap, cur + (key >> root), step, tsize, ((l - root) << 16) | sorted[sym++]);
+      key = next_key(key, l);
+    }
+  }
+  wave_sync();
+  return total;
+}
+__device__ __forceinline__ int read_symbol(Dec &s, const int32_t *g, int cap, int idx) {
+  int off = g[idx];
+  uint32_t v = peek(s);
+  off += (int)(v & 0xFF);
+  int e0 = off < cap ? g[off] : 0;
+  int nb = e0 >> 16, sym = e0 & 0xFFFF;
+  if (nb <= 8) {
+    s.bo += nb;
+    return sym;
+  }
+  off += sym;
+  off += (int)((v & ((1u << nb) - 1u)) >> 8);
+  int e1 = off < cap ? g[off] : 0;
+  s.bo += (e1 >> 16) + 8;
+  return e1 & 0xFFFF;
+}
+constexpr int kNoCap = 1 << 30;
+
+__device__ int read_code_lengths(Dec &s, const int *cl_lens, int nsym, int *lens) {   // engine.ts:305-369
+  int sym = 0, prev = 8, repeat = 0, repeat_len = 0, space = 32768;
+  int32_t *table = s.l->cl_table;
+  if (s.lane == 0) table[32] = 0;
+  wave_sync();
+  build_table(s, table, kNoCap, 32, 5, cl_lens, 18);
+  while (sym < nsym && space > 0) {
+    MAYBE_REFILL(s);
+    fill16(s);
+    int p = (int)(peek(s) & 31);
+    s.bo += table[p] >> 16;
+    int len = table[p] & 0xFFFF;
+    if (len < 16) {
+      repeat = 0;
+      if (s.lane == 0) lens[sym] = len;
+      sym++;
+      if (len) {
+        prev = len;
+        space -= 32768 >> len;
+      }
+    } else {
+      int eb = len - 14, new_len = len == 16 ? prev : 0;
+      if (repeat_len != new_len) {
+        repeat = 0;
+        repeat_len = new_len;
+      }
+      int old = repeat;
+      if (repeat > 0) {
+        repeat -= 2;
+        repeat <<= eb;
+      }
+      fill16(s);
+      repeat += bits(s, eb) + 3;
+      int delta = repeat - old;
+      if (sym + delta > nsym) return ERR(s, -2);
+      for (int k = s.lane; k < delta; k += 64) lens[sym + k] = repeat_len;
+      sym += delta;
+      if (repeat_len) space -= delta << (15 - repeat_len);
+    }
+    wave_sync();
+  }
+  if (space != 0) return ERR(s, -18);
+  for (int k = sym + s.lane; k < nsym; k += 64) lens[k] = 0;
+  wave_sync();
+  return 0;
+}
+
+__device__ int read_huffman_code(Dec &s, int amax, int alimit, int32_t *group, int cap, int idx) {   // :370-470
+  int *lens = s.l->lens;
+  MAYBE_REFILL(s);
+  fill16(s);
+  int kind = bits(s, 2);
+  for (int k = s.lane; k < alimit; k += 64) lens[k] = 0;
+  wave_sync();
+  if (kind == 1) {
+    int syms[4];
+    int maxbits = 0;
+    for (int v = amax - 1; v; v >>= 1) maxbits++;
+    int n = bits(s, 2) + 1;
+    for (int i = 0; i < n; i++) {
+      fill16(s);
+      int sy = bits(s, maxbits);
+      if (sy >= alimit) return ERR(s, -15);
+      syms[i] = sy;
+    }
+    for (int i = 0; i < n - 1; i++)
+      for (int k = i + 1; k < n; k++)
+        if (syms[i] == syms[k]) return ERR(s, -7);
+    int hid = n;
+    if (n == 4) hid += bits(s, 1);
+    if (s.lane == 0) {
+      switch (hid) {
+        case 1: lens[syms[0]] = 1; break;
+        case 2: lens[syms[0]] = 1; lens[syms[1]] = 1; break;
+        case 3: lens[syms[0]] = 1; lens[syms[1]] = 2; lens[syms[2]] = 2; break;
+        case 4: for (int i = 0; i < 4; i++) lens[syms[i]] = 2; break;
+        case 5: lens[syms[0]] = 1; lens[syms[1]] = 2; lens[syms[2]] = 3; lens[syms[3]] = 3; break;
+      }
+    }
+    wave_sync();
+    return build_table(s, group, cap, idx, 8, lens, alimit);
+  }
+  int cl[18];
+  for (int i = 0; i < 18; i++) cl[i] = 0;
+  int space = 32, ncodes = 0;
+  for (int i = kind; i < 18; i++) {
+    int ci = kCodeLenOrder[i];
+    fill16(s);
+    int p = (int)(peek(s) & 15);
+    s.bo += kFixedCL[p] >> 16;
+    int v = kFixedCL[p] & 0xFFFF;
+    cl[ci] = v;
+    if (v) {
+      space -= 32 >> v;
+      ncodes++;
+      if (space <= 0) break;
+    }
+  }
+  if (space != 0 && ncodes != 1) return ERR(s, -4);
+  int r = read_code_lengths(s, cl, alimit, lens);
+  if (r < 0) return r;
+  return build_table(s, group, cap, idx, 8, lens, alimit);
+}
+
+__device__ int decode_var_len_byte(Dec &s) {
+  fill16(s);
+  if (bits(s, 1)) {
+    int n = bits(s, 3);
+    if (n == 0) return 1;
+    return bits(s, n) + (1 << n);
+  }
+  return 0;
+}
+
+__device__ int decode_context_map(Dec &s, int size, uint8_t *map, int32_t *table_scratch) {   // :488-558
+  MAYBE_REFILL(s);
+  int ntrees = decode_var_len_byte(s) + 1;
+  if (ntrees == 1) {
+    for (int k = s.lane; k < size; k += 64) map[k] = 0;
+    wave_sync();
+    return ntrees;
+  }
+  fill16(s);
+  int rle_max = 0;
+  if (bits(s, 1)) rle_max = bits(s, 4) + 1;
+  int asize = ntrees + rle_max;
+  int tsize = kMaxHuffTable[(asize + 31) >> 5];
+  int32_t *table = table_scratch;
+  if (s.lane == 0) table[tsize] = 0;
+  wave_sync();
+  int r = read_huffman_code(s, asize, asize, table, kNoCap, tsize);
+  if (r < 0) return r;
+  int i = 0;
+  while (i < size) {
+    MAYBE_REFILL(s);
+    fill16(s);
+    int code = read_symbol(s, table, kNoCap, tsize);
+    if (code == 0) {
+      if (s.lane == 0) map[i] = 0;
+      i++;
+    } else if (code <= rle_max) {
+      fill16(s);
+      int reps = (1 << code) + bits(s, code);
+      if (i + reps > size) return ERR(s, -3);
+      for (int k = s.lane; k < reps; k += 64) map[i + k] = 0;
+      i += reps;
+    } else {
+      if (s.lane == 0) map[i] = (uint8_t)(code - rle_max);
+      i++;
+    }
+  }
+  wave_sync();
+  fill16(s);
+  if (bits(s, 1) == 1) {   // inverse move-to-front, lane 0 (rare, small)
+    if (s.lane == 0) {
+      uint8_t *mtf = s.l->mtf;
+      for (int k = 0; k < 256; k++) mtf[k] = (uint8_t)k;
+      for (int k = 0; k < size; k++) {
+        int index = map[k];
+        int v = mtf[index];
+        map[k] = (uint8_t)v;
+        for (int q = index; q > 0; q--) mtf[q] = mtf[q - 1];
+        mtf[0] = (uint8_t)v;
+      }
+    }
+    wave_sync();
+  }
+  return ntrees;
+}
+
+__device__ int read_block_length(Dec &s, const int32_t *g, int idx) {
+  fill16(s);
+  int code = read_symbol(s, g, kBlockTreesCap, idx);
+  int n = kBlockLenBits[code];
+  fill16(s);
+  return kBlockLenOff[code] + (n <= 16 ? bits(s, n) : many_bits(s, n));
+}
+__device__ int decode_block_type_and_length(Dec &s, int tree_type, int ntypes) {   // :559-580
+  int off = 4 + tree_type * 2;
+  fill16(s);
+  int bt = read_symbol(s, s.l->block_trees, kBlockTreesCap, 2 * tree_type);
+  int len = read_block_length(s, s.l->block_trees, 2 * tree_type + 1);
+  if (bt == 1) bt = s.rings[off + 1] + 1;
+  else if (bt == 0) bt = s.rings[off];
+  else bt -= 2;
+  if (bt >= ntypes) bt -= ntypes;
+  s.rings[off] = s.rings[off + 1];
+  s.rings[off + 1] = bt;
+  return len;
+}
+__device__ void build_ctx_tree_base(Dec &s) {
+  if (s.lane < 64) s.l->ctx_tree_base[s.lane] = s.lit_group[s.ctx_map[s.ctx_map_slice + s.lane]];
+  wave_sync();
+}
+__device__ void lit_block_switch(Dec &s) {
+  s.lit_blen = decode_block_type_and_length(s, 0, s.n_lit_types);
+  int t = s.rings[5];
+  s.ctx_map_slice = t << 6;
+  s.lit_tree_idx = s.ctx_map[s.ctx_map_slice];
+  int mode = s.ctx_modes[t];
+  s.clo1 = mode << 9;
+  s.clo2 = s.clo1 + 256;
+}
+
+__device__ void maybe_realloc_ring(Dec &s) {   // :608-630 (the scratch slice is max-sized; copy semantics kept)
+  int new_size = s.max_ring;
+  if (new_size > s.expected_total) {
+    int minimal = s.expected_total;
+    while ((new_size >> 1) > minimal) new_size >>= 1;
+    if (!s.input_end && new_size < 16384 && s.max_ring >= 16384) new_size = 16384;
+  }
+  if (new_size <= s.ring_size) return;
+  // a fresh Uint8Array: bytes beyond the old size are zero
+  for (int k = s.ring_size + s.lane; k < new_size + 37; k += 64) s.ring[k] = 0;
+  wave_sync();
+  s.ring_cap = new_size + 37;
+  s.ring_size = new_size;
+}
+
+__device__ int decode_mb_length(Dec &s) {   // :204-256
+  fill16(s);
+  s.input_end = bits(s, 1);
+  s.mbl = 0;
+  s.is_uncompressed = 0;
+  s.is_metadata = 0;
+  if (s.input_end && bits(s, 1)) return 0;
+  int nibbles = bits(s, 2) + 4;
+  if (nibbles == 7) {
+    s.is_metadata = 1;
+    if (bits(s, 1)) return ERR(s, -6);
+    int nbytes = bits(s, 2);
+    if (nbytes == 0) return 0;
+    for (int i = 0; i < nbytes; i++) {
+      fill16(s);
+      int b = bits(s, 8);
+      if (b == 0 && i + 1 == nbytes && nbytes > 1) return ERR(s, -8);
+      s.mbl += b << (i * 8);
+    }
+  } else {
+    for (int i = 0; i < nibbles; i++) {
+      fill16(s);
+      int b = bits(s, 4);
+      if (b == 0 && i + 1 == nibbles && nibbles > 4) return ERR(s, -8);
+      s.mbl += b << (i * 4);
+    }
+  }
+  s.mbl++;
+  if (!s.input_end) s.is_uncompressed = bits(s, 1);
+  return 0;
+}
+
+__device__ int read_next_mb_header(Dec &s) {   // :631-678
+  if (s.input_end) {
+    s.next_running = ST_FINISHED;
+    s.running = ST_INIT_WRITE;
+    return 0;
+  }
+  MAYBE_REFILL(s);
+  int r = decode_mb_length(s);
+  if (r < 0) return r;
+  if (s.mbl == 0 && !s.is_metadata) return 0;
+  if (s.is_uncompressed || s.is_metadata) {
+    r = jump_to_byte_boundary(s);
+    if (r < 0) return r;
+    s.running = s.is_metadata ? ST_READ_METADATA : ST_COPY_UNCOMPRESSED;
+  } else {
+    s.running = ST_COMPRESSED_BLOCK_START;
+  }
+  if (s.is_metadata) return 0;
+  s.expected_total += s.mbl;
+  if (s.expected_total > (1 << 30)) s.expected_total = 1 << 30;
+  if (s.ring_size < s.max_ring) maybe_realloc_ring(s);
+  return 0;
+}
+
+__device__ int read_partition(Dec &s, int tt, int ntypes) {   // :679-704
+  int32_t *bt = s.l->block_trees;
+  int off = bt[2 * tt];
+  if (ntypes <= 1) {
+    wave_sync();
+    if (s.lane == 0) {
+      bt[2 * tt + 1] = off;
+      bt[2 * tt + 2] = off;
+    }
+    wave_sync();
+    return 1 << 28;
+  }
+  int r = read_huffman_code(s, ntypes + 2, ntypes + 2, bt, kBlockTreesCap, 2 * tt);
+  if (r < 0) return r;
+  off += r;
+  if (s.lane == 0) bt[2 * tt + 1] = off;
+  wave_sync();
+  r = read_huffman_code(s, 26, 26, bt, kBlockTreesCap, 2 * tt + 1);
+  if (r < 0) return r;
+  off += r;
+  if (s.lane == 0) bt[2 * tt + 2] = off;
+  wave_sync();
+  return read_block_length(s, bt, 2 * tt + 1);
+}
+
+__device__ int decode_tree_group(Dec &s, int amax, int alimit, int n, int32_t *group) {
+  int next = n;
+  for (int i = 0; i < n; i++) {
+    if (s.lane == 0) group[i] = next;
+    wave_sync();
+    int r = read_huffman_code(s, amax, alimit, group, kNoCap, i);
+    if (r < 0) return r;
+    next += r;
+  }
+  return 0;
+}
+
+__device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
+  int r;
+  s.n_lit_types = decode_var_len_byte(s) + 1;
+  if ((r = read_partition(s, 0, s.n_lit_types)) < 0) return r;
+  s.lit_blen = r;
+  s.n_cmd_types = decode_var_len_byte(s) + 1;
+  if ((r = read_partition(s, 1, s.n_cmd_types)) < 0) return r;
+  s.cmd_blen = r;
+  s.n_dist_types = decode_var_len_byte(s) + 1;
+  if ((r = read_partition(s, 2, s.n_dist_types)) < 0) return r;
+  s.dist_blen = r;
+  MAYBE_REFILL(s);
+  fill16(s);
+  s.npostfix = bits(s, 2);
+  s.ndirect = bits(s, 4) << s.npostfix;
+  int i = 0;
+  while (i < s.n_lit_types) {
+    int lim = i + 96 < s.n_lit_types ? i + 96 : s.n_lit_types;
+    while (i < lim) {
+      fill16(s);
+      int m = bits(s, 2);
+      if (s.lane == 0) s.ctx_modes[i] = (uint8_t)m;
+      i++;
+    }
+    MAYBE_REFILL(s);
+  }
+  int cml = s.n_lit_types << 6;
+  if ((r = decode_context_map(s, cml, s.ctx_map, ctxmap_table)) < 0) return r;
+  int nlit_trees = r;
+  int nontrivial = 0;
+  for (int k = s.lane; k < cml; k += 64)
+    if (s.ctx_map[k] != (k >> 6)) nontrivial = 1;
+  s.trivial_lit_ctx = __any(nontrivial) ? 0 : 1;
+  if ((r = decode_context_map(s, s.n_dist_types << 2, s.dist_ctx_map, ctxmap_table)) < 0) return r;
+  int ndist_trees = r;
+  // groups live back to back in the table scratch: literal, command, distance
+  s.cmd_group = s.lit_group + (size_t)nlit_trees * (1 + 630);
+  if ((r = decode_tree_group(s, 256, 256, nlit_trees, s.lit_group)) < 0) return r;
+  s.dist_group = s.cmd_group + (size_t)s.n_cmd_types * (1 + 1080);
+  if ((r = decode_tree_group(s, 704, 704, s.n_cmd_types, s.cmd_group)) < 0) return r;
+  int dmax = 16 + s.ndirect + 2 * (24 << s.npostfix);
+  if ((r = decode_tree_group(s, dmax, dmax, ndist_trees, s.dist_group)) < 0) return r;
+  // calculateDistanceLut (:705-726), lane 0
+  if (s.lane == 0) {
+    int np = s.npostfix, nd = s.ndirect, postfix = 1 << np, b = 1, half = 0, k = 16;
+    for (int q = 0; q < nd; q++) {
+      dist_extra[k] = 0;
+      dist_offset[k] = q + 1;
+      k++;
+    }
+    while (k < dmax) {
+      int base = nd + ((((2 + half) << b) - 4) << np) + 1;
+      for (int q = 0; q < postfix; q++) {
+        dist_extra[k] = (int8_t)b;
+        dist_offset[k] = base + q;
+        k++;
+      }
+      b += half;
+      half ^= 1;
+    }
+  }
+  wave_sync();
+  s.ctx_map_slice = 0;
+  s.dist_ctx_map_slice = 0;
+  s.clo1 = s.ctx_modes[0] * 512;
+  s.clo2 = s.clo1 + 256;
+  build_ctx_tree_base(s);
+  s.lit_tree_idx = 0;
+  s.cmd_tree_idx = 0;
+  s.rings[4] = 1; s.rings[5] = 0; s.rings[6] = 1; s.rings[7] = 0; s.rings[8] = 1; s.rings[9] = 0;
+  return 0;
+}
+
+// copyRawBytes (:1876-1925) into the ring
+__device__ int copy_raw_bytes(Dec &s, int pos, int len) {
+  if (s.bo & 7) return ERR(s, -30);
+  while (s.bo != 32 && len) {
+    if (s.lane == 0) s.ring[pos] = (uint8_t)peek(s);
+    pos++;
+    s.bo += 8;
+    len--;
+  }
+  wave_sync();
+  if (!len) return 0;
+  int ha = half_available(s);
+  int cn = ha < (len >> 1) ? ha : (len >> 1);
+  if (cn > 0) {
+    int ro = s.ho << 1, delta = cn << 1;
+    for (int k = s.lane; k < delta; k += 64) s.ring[pos + k] = s.l->win[ro + k];
+    wave_sync();
+    pos += delta;
+    len -= delta;
+    s.ho += cn;
+  }
+  if (!len) return 0;
+  if (half_available(s) > 0) {
+    fill16(s);
+    while (len) {
+      if (s.lane == 0) s.ring[pos] = (uint8_t)peek(s);
+      pos++;
+      s.bo += 8;
+      len--;
+    }
+    wave_sync();
+    return check_health(s, 0);
+  }
+  uint64_t avail = s.in_len - s.in_off;
+  if ((uint64_t)len > avail) {   // readInput returns what is left, then 0 -> error -16
+    for (uint64_t k = s.lane; k < avail; k += 64) s.ring[pos + k] = s.in[s.in_off + k];
+    s.in_off += avail;
+    wave_sync();
+    return ERR(s, -16);
+  }
+  for (int k = s.lane; k < len; k += 64) s.ring[pos + k] = s.in[s.in_off + k];
+  s.in_off += (uint64_t)len;
+  wave_sync();
+  return 0;
+}
+
+// write_ring (:868-879) + the reference's chunked output (:2223-2256) as one linear buffer.
+// Returns 0 (space left in the current chunk), 2 (chunk / known buffer full), or NEED_SPACE.
+__device__ int write_ring(Dec &s) {
+  int64_t chunk_left = s.chunk_start + s.chunk_size - s.out_flushed;
+  int64_t b = s.rb_ready - s.rb_written;
+  int64_t n = chunk_left < b ? chunk_left : b;
+  if (n > 0) {
+    if (s.out_flushed + n > s.out_cap) return MIB_E_NEED_SPACE;
+    uint8_t *dst = s.out + s.out_flushed;
+    const uint8_t *src = s.ring + s.rb_written;
+    for (int64_t k = s.lane; k < n; k += 64) dst[k] = src[k];
+    wave_sync();
+    s.out_flushed += n;
+    s.rb_written += (int)n;
+  }
+  return s.out_flushed < s.chunk_start + s.chunk_size ? 0 : 2;
+}
+
+// static dictionary word + RFC transform, lane 0 (engine.ts:1557-1675)
+__device__ int transform_word(uint8_t *dst, int doff, int soff, int wlen, int tidx) {
+  int off = doff;
+  int pre = kRfcTransformTriplets[3 * tidx], type = kRfcTransformTriplets[3 * tidx + 1],
+      suf = kRfcTransformTriplets[3 * tidx + 2];
+  int p = kRfcPrefixSuffixHeads[pre], pe = kRfcPrefixSuffixHeads[pre + 1];
+  int q = kRfcPrefixSuffixHeads[suf], qe = kRfcPrefixSuffixHeads[suf + 1];
+  int omit_first = type - 11, omit_last = type;
+  if (omit_first < 1 || omit_first > 9) omit_first = 0;
+  if (omit_last < 1 || omit_last > 9) omit_last = 0;
+  while (p != pe) dst[off++] = kRfcPrefixSuffix[p++];
+  int len = wlen;
+  if (omit_first > len) omit_first = len;
+  int so = soff + omit_first;
+  len -= omit_first;
+  len -= omit_last;
+  for (int i = len; i > 0; i--) dst[off++] = kDictionary[so++];
+  if (type == 10 || type == 11) {
+    int u = off - len;
+    if (type == 10) len = 1;
+    while (len > 0) {
+      int c0 = dst[u];
+      if (c0 < 0xC0) {
+        if (c0 >= 97 && c0 <= 122) dst[u] ^= 32;
+        u += 1;
+        len -= 1;
+      } else if (c0 < 0xE0) {
+        dst[u + 1] ^= 32;
+        u += 2;
+        len -= 2;
+      } else {
+        dst[u + 2] ^= 5;
+        u += 3;
+        len -= 3;
+      }
+    }
+  }
+  while (q != qe) dst[off++] = kRfcPrefixSuffix[q++];
+  return off - doff;
+}
+
+__device__ int use_dictionary(Dec &s, int fence) {   // :903-983
+  if (s.distance > 0x7FFFFFFC) return ERR(s, -9);
+  int address = s.distance - s.max_dist - 1 - s.cd_total;
+  if (address < 0) {   // compound dictionary, one chunk (attachDictionaryChunk is called once)
+    int a = -address - 1, length = s.copy_len;
+    if (s.cd_total > a + length) return ERR(s, -9);
+    s.dist_rb_idx = (s.dist_rb_idx + 1) & 3;
+    s.rings[s.dist_rb_idx] = s.distance;
+    s.mbl -= length;
+    s.cd_br_index = 0;
+    s.cd_br_offset = a;
+    s.cd_br_length = length;
+    s.cd_br_copied = 0;
+    s.running = ST_COPY_FROM_COMPOUND;
+    return 0;
+  }
+  int wlen = s.copy_len;
+  if (wlen > 31) return ERR(s, -9);
+  int shift = kRfcDictSizeBits[wlen];
+  if (shift == 0) return ERR(s, -9);
+  int off = (int)kRfcDictOffsets[wlen];
+  int mask = (1 << shift) - 1;
+  int widx = address & mask, tidx = address >> shift;
+  off += widx * wlen;
+  if (tidx >= RFC_NUM_TRANSFORMS) return ERR(s, -9);
+  int len = 0;
+  if (s.lane == 0) len = transform_word(s.ring, s.pos, off, wlen, tidx);
+  len = __shfl(len, 0);
+  wave_sync();
+  s.pos += len;
+  s.mbl -= len;
+  if (s.pos >= fence) {
+    s.next_running = ST_MAIN_LOOP;
+    s.running = ST_INIT_WRITE;
+    return 0;
+  }
+  s.running = ST_MAIN_LOOP;
+  return 0;
+}
+
+__device__ int copy_from_compound(Dec &s, int fence) {
+  int pos = s.pos, orig = pos;
+  while (s.cd_br_length != s.cd_br_copied) {
+    int space = fence - pos;
+    int clen = s.cd_br_index == 0 ? s.cd_total : 0;
+    int rem = clen - s.cd_br_offset;
+    int len = s.cd_br_length - s.cd_br_copied;
+    if (len > rem) len = rem;
+    if (len > space) len = space;
+    if (s.cd_br_index >= 1) return MIB_E_JS_TYPE_ERROR;   // reads past the last chunk in JS
+    for (int k = s.lane; k < len; k += 64) s.ring[pos + k] = s.cd[s.cd_br_offset + k];
+    wave_sync();
+    pos += len;
+    s.cd_br_offset += len;
+    s.cd_br_copied += len;
+    if (len == rem) {
+      s.cd_br_index++;
+      s.cd_br_offset = 0;
+    }
+    if (pos >= fence) break;
+  }
+  return pos - orig;
+}
+
+// LZ77 copy of `cl` bytes at ring position pos from distance dist (no fence crossing).
+__device__ void ring_copy_fast(Dec &s, int src, int cl, int dist) {
+  uint8_t *r = s.ring;
+  int dst = s.pos;
+  if (dist >= cl) {
+    for (int k = s.lane; k < cl; k += 64) r[dst + k] = r[src + k];
+  } else {
+    int chunk = dist < 64 ? dist : 64;
+    for (int off = 0; off < cl; off += chunk) {
+      int k = off + s.lane;
+      if (s.lane < chunk && k < cl) r[dst + k] = r[src + k];
+      wave_sync();
+    }
+  }
+  wave_sync();
+}
+
+// one invocation of decompress(); returns 0, 1 (done), 2 (output full / compound return) or < 0
+__device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
+  int r;
+  if (s.running < 0) return ERR(s, -28);
+  if (s.running == ST_INITED) {
+    fill16(s);
+    int wb;
+    if (bits(s, 1) == 0) wb = 16;
+    else {
+      int n = bits(s, 3);
+      if (n) wb = 17 + n;
+      else {
+        n = bits(s, 3);
+        if (n == 1) wb = -1;
+        else if (n) wb = 8 + n;
+        else wb = 17;
+      }
+    }
+    if (wb == -1) return ERR(s, -11);
+    s.max_ring = 1 << wb;
+    s.max_back = s.max_ring - 16;
+    s.running = ST_BLOCK_START;
+  }
+  int fence = s.ring_size;
+  int rmask = s.ring_size - 1;
+  while (s.running != ST_FINISHED) {
+    if (++s.guard > s.guard_limit) return MIB_E_NO_PROGRESS;
+    switch (s.running) {
+      case ST_BLOCK_START:
+        if (s.mbl < 0) return ERR(s, -10);
+        if ((r = read_next_mb_header(s)) < 0) return r;
+        fence = s.ring_size;
+        if (s.pos + s.mbl <= s.ring_size) fence = 0x7FFFFFFF;
+        rmask = s.ring_size - 1;
+        continue;
+      case ST_COMPRESSED_BLOCK_START:
+        if ((r = read_codes_and_maps(s, dist_extra, dist_offset, ctxmap_table)) < 0) return r;
+        s.running = ST_MAIN_LOOP;
+        continue;
+      case ST_MAIN_LOOP:
+      case ST_INSERT_LOOP:
+      case ST_COPY_LOOP: {
+        int phase = s.running;
+        uint8_t *ring = s.ring;
+        for (;;) {
+          if (++s.guard > s.guard_limit) return MIB_E_NO_PROGRESS;
+          if (phase == ST_MAIN_LOOP) {   // command (:1080-1152)
+            if (s.mbl <= 0) {
+              s.running = ST_BLOCK_START;
+              break;
+            }
+            MAYBE_REFILL(s);
+            if (s.cmd_blen == 0) {
+              s.cmd_blen = decode_block_type_and_length(s, 1, s.n_cmd_types);
+              s.cmd_tree_idx = s.rings[7];
+            }
+            s.cmd_blen--;
+            fill16(s);
+            int sym = read_symbol(s, s.cmd_group, kNoCap, s.cmd_tree_idx);
+            int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
+            s.dist_code = kCmdLut[4 * sym + 3];
+            fill16(s);
+            int ib = cbits & 0xFF;
+            s.insert_len = ins_off + (ib <= 16 ? bits(s, ib) : many_bits(s, ib));
+            fill16(s);
+            int cb = cbits >> 8;
+            s.copy_len = copy_off + (cb <= 16 ? bits(s, cb) : many_bits(s, cb));
+            s.j = 0;
+            phase = ST_INSERT_LOOP;
+          }
+          if (phase <= ST_INSERT_LOOP) {   // literals (:1154-1276)
+            int stop = 0;
+            while (s.j < s.insert_len) {
+              MAYBE_REFILL(s);
+              if (s.lit_blen == 0) {
+                lit_block_switch(s);
+                if (!s.trivial_lit_ctx) build_ctx_tree_base(s);
+              }
+              int a = s.insert_len - s.j, b = s.lit_blen, c2 = fence - s.pos, d = 2031 - s.ho;
+              int batch = a < b ? a : b;
+              if (c2 < batch) batch = c2;
+              if (d < batch) batch = d;
+              if (d <= 0 && batch <= 0 && a > 0 && b > 0 && c2 > 0) batch = 1;   // Bug J fix
+              s.lit_blen -= batch;
+              int end = s.j + batch;
+              if (s.trivial_lit_ctx) {
+                const int32_t *g = s.lit_group;
+                int ti = s.lit_tree_idx;
+                while (s.j < end) {
+                  fill16(s);
+                  int v = read_symbol(s, g, kNoCap, ti);
+                  if (s.lane == 0 && s.pos < s.ring_cap) ring[s.pos] = (uint8_t)v;
+                  s.pos++;
+                  s.j++;
+                }
+              } else {
+                int p1 = ring[(s.pos - 1) & rmask], p2 = ring[(s.pos - 2) & rmask];
+                const int32_t *g = s.lit_group;
+                const int32_t *ctb = s.l->ctx_tree_base;
+                while (s.j < end) {
+                  int ctx = kRfcContextLut[s.clo1 + p1] | kRfcContextLut[s.clo2 + p2];
+                  p2 = p1;
+                  fill16(s);
+                  int off = ctb[ctx];
+                  uint32_t v = peek(s);
+                  off += (int)(v & 0xFF);
+                  int e0 = g[off], nb = e0 >> 16;
+                  if (nb <= 8) {
+                    s.bo += nb;
+                    p1 = e0 & 0xFFFF;
+                  } else {
+                    off += e0 & 0xFFFF;
+                    off += (int)((v & ((1u << nb) - 1u)) >> 8);
+                    int e1 = g[off];
+                    s.bo += (e1 >> 16) + 8;
+                    p1 = e1 & 0xFFFF;
+                  }
+                  if (s.lane == 0 && s.pos < s.ring_cap) ring[s.pos] = (uint8_t)p1;
+                  s.pos++;
+                  s.j++;
+                }
+              }
+              wave_sync();
+              if (s.pos >= fence) {
+                s.next_running = ST_INSERT_LOOP;
+                s.running = ST_INIT_WRITE;
+                stop = 1;
+                break;
+              }
+            }
+            if (stop) break;
+            s.mbl -= s.insert_len;   // distance (:1277-1377)
+            if (s.mbl <= 0) {
+              s.running = ST_BLOCK_START;
+              break;
+            }
+            int dc = s.dist_code;
+            if (dc < 0) {
+              s.distance = s.rings[s.dist_rb_idx];
+            } else {
+              MAYBE_REFILL(s);
+              if (s.dist_blen == 0) {
+                s.dist_blen = decode_block_type_and_length(s, 2, s.n_dist_types);
+                s.dist_ctx_map_slice = s.rings[9] << 2;
+              }
+              s.dist_blen--;
+              fill16(s);
+              int tree = s.dist_ctx_map[s.dist_ctx_map_slice + dc];
+              dc = read_symbol(s, s.dist_group, kNoCap, tree);
+              if (dc < 16) {
+                int idx = (s.dist_rb_idx + kDistIdxOff[dc]) & 3;
+                s.distance = s.rings[idx] + kDistValOff[dc];
+                if (s.distance < 0) return ERR(s, -12);
+              } else {
+                int eb = dist_extra[dc], bv;
+                if (s.bo + eb <= 32) {
+                  bv = (int)(peek(s) & ((1u << eb) - 1u));
+                  s.bo += eb;
+                } else {
+                  fill16(s);
+                  bv = eb <= 16 ? bits(s, eb) : many_bits(s, eb);
+                }
+                s.distance = dist_offset[dc] + (bv << s.npostfix);
+              }
+            }
+            if (s.max_dist != s.max_back && s.pos < s.max_back) s.max_dist = s.pos;
+            else s.max_dist = s.max_back;
+            if (s.distance > s.max_dist) {
+              s.running = ST_USE_DICTIONARY;
+              break;
+            }
+            if (dc > 0) {
+              s.dist_rb_idx = (s.dist_rb_idx + 1) & 3;
+              s.rings[s.dist_rb_idx] = s.distance;
+            }
+            if (s.copy_len > s.mbl) return ERR(s, -9);
+            s.j = 0;
+            phase = ST_COPY_LOOP;
+          }
+          {   // copy (:1379-1433)
+            int dist = s.distance, cl = s.copy_len - s.j;
+            int src = (s.pos - dist) & rmask;
+            if (src + cl < rmask && s.pos + cl < rmask) {
+              ring_copy_fast(s, src, cl, dist);
+              s.j = s.copy_len;
+              s.mbl -= cl;
+              s.pos += cl;
+            } else {
+              // ring wrap and/or fence inside the copy: chunks that never read their own writes
+              int cut = 0;
+              while (s.j < s.copy_len) {
+                int rem = s.copy_len - s.j;
+                int room = fence - s.pos;
+                int chunk = rem < 64 ? rem : 64;
+                if (dist < chunk) chunk = dist;
+                if (dist >= s.ring_size - 64) chunk = 1;
+                if (room < chunk) chunk = room;
+                if (chunk < 1) chunk = 1;
+                if (s.lane < chunk) {
+                  int p = s.pos + s.lane;
+                  uint8_t v = ring[(p - dist) & rmask];
+                  if (p < s.ring_cap) ring[p] = v;
+                }
+                wave_sync();
+                s.mbl -= chunk;
+                s.pos += chunk;
+                s.j += chunk;
+                if (s.pos >= fence) {
+                  s.next_running = ST_COPY_LOOP;
+                  s.running = ST_INIT_WRITE;
+                  break;
+                }
+              }
+              if (s.j < s.copy_len) cut = 1;
+              if (cut) break;
+            }
+            phase = ST_MAIN_LOOP;
+          }
+        }
+        continue;
+      }
+      case ST_USE_DICTIONARY:
+        if ((r = use_dictionary(s, fence)) < 0) return r;
+        continue;
+      case ST_COPY_FROM_COMPOUND: {
+        int n = copy_from_compound(s, fence);
+        if (n < 0) return n;
+        s.pos += n;
+        if (s.pos >= fence) {
+          s.next_running = ST_COPY_FROM_COMPOUND;
+          s.running = ST_INIT_WRITE;
+          return 2;
+        }
+        s.running = ST_MAIN_LOOP;
+        continue;
+      }
+      case ST_READ_METADATA:
+        while (s.mbl > 0) {
+          MAYBE_REFILL(s);
+          fill16(s);
+          bits(s, 8);
+          s.mbl--;
+        }
+        s.running = ST_BLOCK_START;
+        continue;
+      case ST_COPY_UNCOMPRESSED: {   // :838-867
+        if (s.mbl <= 0) {
+          if (s.bo == 32 && (r = prepare(s)) < 0) return r;
+          s.running = ST_BLOCK_START;
+          continue;
+        }
+        int chunk = s.ring_size - s.pos < s.mbl ? s.ring_size - s.pos : s.mbl;
+        if ((r = copy_raw_bytes(s, s.pos, chunk)) < 0) return r;
+        s.mbl -= chunk;
+        s.pos += chunk;
+        if (s.pos == s.ring_size) {
+          s.next_running = ST_COPY_UNCOMPRESSED;
+          s.running = ST_INIT_WRITE;
+          continue;
+        }
+        if (s.bo == 32 && (r = prepare(s)) < 0) return r;
+        s.running = ST_BLOCK_START;
+        continue;
+      }
+      case ST_INIT_WRITE:
+        s.rb_ready = s.pos < s.ring_size ? s.pos : s.ring_size;
+        s.running = ST_WRITE;
+        continue;
+      case ST_WRITE:
+        if ((r = write_ring(s)) != 0) return r;
+        if (s.pos >= s.max_back) s.max_dist = s.max_back;
+        if (s.pos >= s.ring_size) {
+          if (s.pos > s.ring_size) {
+            int extra = s.pos - s.ring_size;
+            uint8_t v = 0;
+            if (s.lane < extra) v = s.ring[s.ring_size + s.lane];
+            wave_sync();
+            if (s.lane < extra) s.ring[s.lane] = v;   // slack <= 37 + 64 bytes
+            if (extra > 64) {
+              for (int k = 64; k < extra; k++) {
+                if (s.lane == 0) s.ring[k] = s.ring[s.ring_size + k];
+              }
+            }
+            wave_sync();
+          }
+          s.pos &= rmask;
+          s.rb_written = 0;
+        }
+        s.running = s.next_running;
+        continue;
+      default:
+        return ERR(s, -28);
+    }
+  }
+  if (s.mbl < 0) return ERR(s, -10);
+  if ((r = jump_to_byte_boundary(s)) != 0) return r;
+  if ((r = check_health(s, 1)) != 0) return r;
+  return 1;
+}
+
+// Persistent grid: block b decodes jobs b, b + grid, ...  Scratch per block:
+//   [ring: ring_bytes][tables: kDecodeTableInts int32][ctx maps: kDecodeCtxBytes][dist luts]
+__global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int njobs, uint8_t *scratch,
+                                                            uint64_t per_block, uint64_t ring_bytes) {
+  __shared__ Lds lds;
+  uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
+  uint8_t *ring = base;
+  int32_t *tables = reinterpret_cast<int32_t *>(base + ring_bytes);
+  uint8_t *ctx = reinterpret_cast<uint8_t *>(tables + kDecodeTableInts);
+  int8_t *dist_extra = reinterpret_cast<int8_t *>(ctx + kDecodeCtxBytes);
+  int32_t *dist_offset = reinterpret_cast<int32_t *>(dist_extra + 1152);
+  int32_t *ctxmap_table = dist_offset + 1152;
+  const int lane = threadIdx.x;
+  for (int jb = blockIdx.x; jb < njobs; jb += gridDim.x) {
+    DecJob job = jobs[jb];
+    Dec s;
+    s.l = &lds;
+    s.lane = lane;
+    s.in = job.in;
+    s.in_len = job.in_len;
+    s.in_off = 0;
+    s.acc = 0;
+    s.bo = 32;
+    s.ho = 2048;
+    s.tail = 0;
+    s.eos = 0;
+    s.running = 0;
+    s.next_running = 0;
+    s.ring = ring;
+    s.ring_cap = 0;
+    s.ring_size = 0;
+    s.max_ring = 0;
+    s.max_back = 0;
+    s.max_dist = 0;
+    s.expected_total = 0;
+    s.pos = 0;
+    s.mbl = 0;
+    s.input_end = 0;
+    s.is_uncompressed = 0;
+    s.is_metadata = 0;
+    s.lit_blen = s.n_lit_types = s.cmd_blen = s.n_cmd_types = s.dist_blen = s.n_dist_types = 0;
+    for (int i = 0; i < 10; i++) s.rings[i] = 0;
+    s.rings[0] = 16; s.rings[1] = 15; s.rings[2] = 11; s.rings[3] = 4;
+    s.dist_rb_idx = 3;
+    s.lit_group = tables;
+    s.cmd_group = tables;
+    s.dist_group = tables;
+    s.ctx_modes = ctx + 256 * 64 + 256 * 4;
+    s.ctx_map = ctx;
+    s.dist_ctx_map = ctx + 256 * 64;
+    s.trivial_lit_ctx = s.lit_tree_idx = s.cmd_tree_idx = 0;
+    s.j = s.insert_len = s.copy_len = s.dist_code = s.distance = 0;
+    s.ctx_map_slice = s.dist_ctx_map_slice = s.clo1 = s.clo2 = 0;
+    s.npostfix = s.ndirect = 0;
+    s.out = job.out;
+    s.out_cap = (int64_t)job.out_cap;
+    s.out_flushed = 0;
+    s.known_size = job.out_size > 0;
+    s.chunk_start = 0;
+    s.chunk_size = s.known_size ? job.out_size : 16384;
+    s.rb_written = s.rb_ready = 0;
+    s.cd = job.dict;
+    s.cd_total = (int)job.dict_len;
+    s.cd_br_offset = s.cd_br_length = s.cd_br_copied = s.cd_br_index = 0;
+    // iteration guard: far above what any stream can need (each iteration consumes input
+    // bits or produces output), low enough that a bug cannot spin a GPU forever
+    s.guard = 0;
+    s.guard_limit = 64ull * (job.in_len + 64) * 8 + 4ull * job.out_cap + (1ull << 26);
+    // initState (:160-178)
+    for (int i = lane; i <= kBlockTreesCap; i += 64) lds.block_trees[i] = 0;
+    __syncthreads();
+    if (lane == 0) lds.block_trees[0] = 7;
+    __syncthreads();
+    int rc = prepare(s);
+    if (rc >= 0) {
+      s.running = ST_INITED;
+      for (;;) {
+        rc = decompress(s, dist_extra, dist_offset, ctxmap_table);
+        if (rc < 0) break;
+        if (s.known_size) { rc = 0; break; }
+        // unknown size: the reference loops while a chunk comes back full (decode.ts / engine.ts:2223-2256)
+        int64_t used = s.out_flushed - s.chunk_start;
+        if (used < s.chunk_size) { rc = 0; break; }
+        s.chunk_start += s.chunk_size;
+        if (s.chunk_size < 4194304) s.chunk_size *= 2;
+      }
+    }
+    if (rc >= 0 && s.known_size && s.out_flushed < job.out_size) {   // zero-padded to the known size
+      for (int64_t k = s.out_flushed + lane; k < job.out_size; k += 64) s.out[k] = 0;
+    }
+    if (lane == 0) {
+      jobs[jb].status = rc < 0 ? rc : 0;
+      jobs[jb].result_len = s.known_size ? job.out_size : s.out_flushed;
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace mib
+
+extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
+                                        uint64_t ring_bytes, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(mib::decode_streams_kernel, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block,
+                     ring_bytes);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(mib::kCmdLut), host_lut, sizeof(int16_t) * 704 * 4);
+}

@@ -1,0 +1,468 @@
+// brotli_amd host runtime: the C ABI of include/brotli_amd.h on top of the HIP kernels.
+//
+// Host work here is orchestration only -- argument handling mirroring decode.ts / encode.ts,
+// header peeks, buffer sizing, H2D/D2H copies.  Every byte of encode/decode compute runs in
+// the kernels (decode.hip, encode*.hip); with no gfx950 device the calls fail with
+// MIB_E_NO_DEVICE rather than falling back to the CPU.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
+                                        uint64_t ring_bytes, int grid, hipStream_t stream);
+extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut);
+
+
+
+
+namespace {
+
+#define HIP_OK(x)                               \
+  do {                                          \
+    hipError_t e_ = (x);                        \
+    if (e_ != hipSuccess) return MIB_E_NO_DEVICE; \
+  } while (0)
+
+std::mutex g_mu;
+int g_device = 0;
+bool g_inited = false;
+
+void build_cmd_lut(int16_t *lut) {   // engine.ts:65-90
+  static const int ins_bits[24] = {0, 0, 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 7, 8, 9, 10, 12, 14, 24};
+  static const int copy_bits[24] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 7, 8, 9, 10, 24};
+  int ins_off[24], copy_off[24];
+  ins_off[0] = 0;
+  copy_off[0] = 2;
+  for (int i = 0; i < 23; i++) {
+    ins_off[i + 1] = ins_off[i] + (1 << ins_bits[i]);
+    copy_off[i + 1] = copy_off[i] + (1 << copy_bits[i]);
+  }
+  for (int c = 0; c < 704; c++) {
+    int r = c >> 6, dco = -4;
+    if (r >= 2) {
+      r -= 2;
+      dco = 0;
+    }
+    int ic = (((0x29850 >> (r * 2)) & 3) << 3) | ((c >> 3) & 7);
+    int cc = (((0x26244 >> (r * 2)) & 3) << 3) | (c & 7);
+    int co = copy_off[cc];
+    lut[4 * c] = (int16_t)(ins_bits[ic] | (copy_bits[cc] << 8));
+    lut[4 * c + 1] = (int16_t)ins_off[ic];
+    lut[4 * c + 2] = (int16_t)co;
+    lut[4 * c + 3] = (int16_t)(dco + std::min(co, 5) - 2);
+  }
+}
+
+int ensure_init() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_inited) return 0;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MIB_E_NO_DEVICE;
+  if (g_device >= n) return MIB_E_NO_DEVICE;
+  HIP_OK(hipSetDevice(g_device));
+  hipDeviceProp_t prop;
+  HIP_OK(hipGetDeviceProperties(&prop, g_device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    fprintf(stderr, "brotli_amd: device %d is %s, this build targets gfx950\n", g_device, prop.gcnArchName);
+    return MIB_E_NO_DEVICE;
+  }
+  int16_t lut[704 * 4];
+  build_cmd_lut(lut);
+  HIP_OK(mib_decode_init_tables(lut));
+  g_inited = true;
+  return 0;
+}
+
+// decodeWindowBits (engine.ts:91-124) on the first bits of a stream: sizes the ring scratch
+int peek_window_bits(const uint8_t *b, size_t n) {
+  uint32_t v = 0;
+  for (size_t i = 0; i < 2 && i < n; i++) v |= (uint32_t)b[i] << (8 * i);
+  if ((v & 1) == 0) return 16;
+  int m = (v >> 1) & 7;
+  if (m) return 17 + m;
+  m = (v >> 4) & 7;
+  if (m == 1) return 24;   // large window: rejected by the decoder, any ring size will do
+  if (m) return 8 + m;
+  return 17;
+}
+
+}  // namespace
+
+struct mib_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // decode scratch
+  uint8_t *d_scratch = nullptr;
+  uint64_t scratch_bytes = 0;
+  mib::DecJob *d_jobs = nullptr;
+  size_t jobs_cap = 0;
+  // encode workspace (encode.hip)
+  void *enc_ws = nullptr;
+  // profiling
+  bool profiling = false;
+  std::vector<mib_kernel_time> times;
+  void add_time(const char *name, double ms) {
+    for (auto &t : times)
+      if (strncmp(t.name, name, sizeof(t.name)) == 0) {
+        t.ms += ms;
+        t.launches++;
+        return;
+      }
+    mib_kernel_time t;
+    memset(&t, 0, sizeof(t));
+    strncpy(t.name, name, sizeof(t.name) - 1);
+    t.ms = ms;
+    t.launches = 1;
+    times.push_back(t);
+  }
+};
+
+extern "C" void mib_ctx_add_time(mib_ctx *c, const char *name, double ms) { c->add_time(name, ms); }
+extern "C" int mib_ctx_profiling(mib_ctx *c) { return c->profiling ? 1 : 0; }
+extern "C" void **mib_ctx_enc_ws(mib_ctx *c) { return &c->enc_ws; }
+extern "C" void mib_encode_ws_free(void *ws);
+
+namespace {
+
+mib_ctx *g_default_ctx = nullptr;
+
+mib_ctx *default_ctx() {
+  if (ensure_init() != 0) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_default_ctx) g_default_ctx = mib_ctx_new(g_device);
+  return g_default_ctx;
+}
+
+int grow(void **p, uint64_t *cap, uint64_t need) {
+  if (*cap >= need) return 0;
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  *cap = 0;
+  uint64_t n = std::max<uint64_t>(need, 1 << 20);
+  if (hipMalloc(p, n) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  *cap = n;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void mib_enc_opts_default(mib_enc_opts *o) {
+  o->quality = 11;
+  o->lgwin = 22;
+  o->mode = MIB_MODE_GENERIC;
+  o->size_hint = 0;
+}
+
+int mib_init(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_inited && device != g_device) return MIB_E_INVALID_ARG;
+    g_device = device;
+  }
+  return ensure_init();
+}
+
+const char *mib_strerror(int code) {
+  static thread_local char buf[96];
+  if (code <= -1 && code >= -30) {
+    snprintf(buf, sizeof(buf), "Brotli error code: %d", code);
+    return buf;
+  }
+  switch (code) {
+    case 0: return "ok";
+    case MIB_E_NO_DEVICE: return "brotli_amd: no usable gfx950 (MI355X) device";
+    case MIB_E_INVALID_ARG: return "brotli_amd: invalid argument";
+    case MIB_E_OUT_OF_MEMORY: return "brotli_amd: out of device memory";
+    case MIB_E_OUTPUT_LIMIT: return "Decompressed size exceeds limit";
+    case MIB_E_NEED_SPACE: return "brotli_amd: output buffer too small";
+    case MIB_E_JS_RANGE_ERROR: return "RangeError: offset is out of bounds";
+    case MIB_E_JS_TYPE_ERROR: return "TypeError: Cannot read property 'subarray' of undefined";
+    case MIB_E_NO_PROGRESS: return "brotli_amd: decoder made no progress";
+  }
+  snprintf(buf, sizeof(buf), "brotli_amd: error %d", code);
+  return buf;
+}
+
+void mib_buf_free(mib_buf *b) {
+  if (b && b->data) free(b->data);
+  if (b) {
+    b->data = nullptr;
+    b->size = 0;
+  }
+}
+
+int64_t mib_decoded_size(const uint8_t *b, size_t n) {   // engine.ts:2155-2192 (header parse only)
+  size_t bp = 0;
+  auto rb = [&](int k) {
+    int v = 0;
+    for (int i = 0; i < k; i++, bp++) {
+      int byte = (bp >> 3) < n ? b[bp >> 3] : 0;
+      v |= ((byte >> (bp & 7)) & 1) << i;
+    }
+    return v;
+  };
+  if (rb(1)) {
+    int m = rb(3);
+    if (m == 0) {
+      int k = rb(3);
+      if (k == 1) {
+        if (rb(1)) return -1;
+        rb(6);
+      }
+    }
+  }
+  int last = rb(1);
+  if (last && rb(1)) return 0;
+  int nib = rb(2) + 4;
+  if (nib == 7) return -1;
+  int64_t mlen = 0;
+  for (int i = 0; i < nib; i++) mlen |= (int64_t)rb(4) << (i * 4);
+  mlen++;
+  return last ? mlen : -1;
+}
+
+mib_ctx *mib_ctx_new(int device) {
+  mib_ctx *c = new mib_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return nullptr;
+  }
+  return c;
+}
+
+void mib_ctx_free(mib_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->d_scratch) hipFree(c->d_scratch);
+  if (c->d_jobs) hipFree(c->d_jobs);
+  if (c->enc_ws) mib_encode_ws_free(c->enc_ws);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void mib_ctx_set_profiling(mib_ctx *c, int on) { c->profiling = on != 0; }
+
+int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max) {
+  int n = std::min<int>(max, (int)c->times.size());
+  for (int i = 0; i < n; i++) out[i] = c->times[i];
+  return (int)c->times.size();
+}
+
+// decode k streams whose bytes are on the device; jobs[] describes them (host copy)
+static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t stream) {
+  size_t k = jobs.size();
+  if (k == 0) return 0;
+  int max_log = 10;
+  for (auto &j : jobs) max_log = std::max(max_log, j.max_ring_log);
+  uint64_t ring_bytes = ((uint64_t)1 << max_log) + 37 + 256;
+  ring_bytes = (ring_bytes + 255) & ~(uint64_t)255;
+  uint64_t per_block = ring_bytes + mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4;
+  per_block = (per_block + 255) & ~(uint64_t)255;
+  int grid = (int)std::min<size_t>(k, 2048);
+  int rc;
+  if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
+  if (k > c->jobs_cap) {
+    if (c->d_jobs) hipFree(c->d_jobs);
+    c->d_jobs = nullptr;
+    c->jobs_cap = 0;
+    if (hipMalloc(&c->d_jobs, sizeof(mib::DecJob) * k) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+    c->jobs_cap = k;
+  }
+  HIP_OK(hipMemcpyAsync(c->d_jobs, jobs.data(), sizeof(mib::DecJob) * k, hipMemcpyHostToDevice, stream));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->profiling) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, stream);
+  }
+  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, stream));
+  if (c->profiling) hipEventRecord(e1, stream);
+  HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * k, hipMemcpyDeviceToHost, stream));
+  HIP_OK(hipStreamSynchronize(stream));
+  if (c->profiling) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    c->add_time("decode_streams_kernel", ms);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  }
+  return 0;
+}
+
+int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, size_t k, uint8_t *d_out,
+                   const uint64_t *out_offsets, int64_t *out_sizes, int *status, void *stream) {
+  if (!c || (k && (!d_in || !in_offsets || !d_out || !out_offsets))) return MIB_E_INVALID_ARG;
+  if (ensure_init() != 0) return MIB_E_NO_DEVICE;
+  hipSetDevice(c->device);
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  c->times.clear();
+  std::vector<uint8_t> heads(2 * k);
+  std::vector<mib::DecJob> jobs(k);
+  for (size_t i = 0; i < k; i++) {
+    uint64_t n = in_offsets[i + 1] - in_offsets[i];
+    if (n) HIP_OK(hipMemcpyAsync(&heads[2 * i], d_in + in_offsets[i], std::min<uint64_t>(n, 2), hipMemcpyDeviceToHost, st));
+  }
+  HIP_OK(hipStreamSynchronize(st));
+  for (size_t i = 0; i < k; i++) {
+    mib::DecJob &j = jobs[i];
+    memset(&j, 0, sizeof(j));
+    j.in = d_in + in_offsets[i];
+    j.in_len = in_offsets[i + 1] - in_offsets[i];
+    j.out = d_out + out_offsets[i];
+    j.out_cap = out_offsets[i + 1] - out_offsets[i];
+    j.out_size = -1;
+    j.max_ring_log = peek_window_bits(&heads[2 * i], (size_t)std::min<uint64_t>(j.in_len, 2));
+  }
+  int rc = decode_jobs(c, jobs, st);
+  if (rc) return rc;
+  int worst = 0;
+  for (size_t i = 0; i < k; i++) {
+    out_sizes[i] = jobs[i].result_len;
+    status[i] = jobs[i].status;
+    if (jobs[i].status) worst = jobs[i].status;
+  }
+  return worst == MIB_E_NEED_SPACE ? MIB_E_NEED_SPACE : 0;
+}
+
+// one host stream through the device (brotliDecode semantics of decode.ts:18-65)
+int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, int64_t max_out, int64_t exact_out,
+               mib_buf *out) {
+  if (!out || (!in && n)) return MIB_E_INVALID_ARG;
+  out->data = nullptr;
+  out->size = 0;
+  mib_ctx *c = default_ctx();
+  if (!c) return MIB_E_NO_DEVICE;
+  hipSetDevice(c->device);
+  int64_t out_size = -1;
+  if (exact_out >= 0) {
+    out_size = exact_out;   // legacy numeric signature: no peek (decode.ts:27-44)
+  } else {
+    int64_t est = mib_decoded_size(in, n);
+    if (est > 0) out_size = est;
+  }
+  if (max_out >= 0 && out_size >= 0 && out_size > max_out) return MIB_E_OUTPUT_LIMIT;
+  int known = out_size > 0;
+  uint64_t cap = known ? (uint64_t)out_size : std::max<uint64_t>(1 << 20, 4 * (uint64_t)n + 4096);
+  uint8_t *d_in = nullptr, *d_out = nullptr, *d_dict = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d_in, n + 16) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  if (n) hipMemcpy(d_in, in, n, hipMemcpyHostToDevice);
+  if (dict) {
+    if (hipMalloc(&d_dict, dict_n + 16) != hipSuccess) {
+      hipFree(d_in);
+      return MIB_E_OUT_OF_MEMORY;
+    }
+    if (dict_n) hipMemcpy(d_dict, dict, dict_n, hipMemcpyHostToDevice);
+  }
+  for (;;) {
+    if (hipMalloc(&d_out, cap + 64) != hipSuccess) {
+      rc = MIB_E_OUT_OF_MEMORY;
+      break;
+    }
+    std::vector<mib::DecJob> jobs(1);
+    mib::DecJob &j = jobs[0];
+    memset(&j, 0, sizeof(j));
+    j.in = d_in;
+    j.in_len = n;
+    j.out = d_out;
+    j.out_cap = cap;
+    j.out_size = known ? out_size : -1;
+    j.dict = d_dict;
+    j.dict_len = dict ? dict_n : 0;
+    j.max_ring_log = peek_window_bits(in, n);
+    rc = decode_jobs(c, jobs, c->stream);
+    if (rc) break;
+    rc = jobs[0].status;
+    if (rc == MIB_E_NEED_SPACE && !known && cap < ((uint64_t)1 << 33)) {
+      hipFree(d_out);
+      d_out = nullptr;
+      cap *= 4;
+      continue;
+    }
+    if (rc == 0) {
+      uint64_t len = (uint64_t)jobs[0].result_len;
+      out->data = (uint8_t *)malloc(len ? len : 1);
+      out->size = len;
+      if (len) hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost);
+      if (max_out >= 0 && (int64_t)len > max_out) {   // the header can lie about the size (decode.ts:57-62)
+        mib_buf_free(out);
+        rc = MIB_E_OUTPUT_LIMIT;
+      }
+    }
+    break;
+  }
+  if (d_out) hipFree(d_out);
+  if (d_dict) hipFree(d_dict);
+  hipFree(d_in);
+  return rc;
+}
+
+int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
+  mib_ctx *c = default_ctx();
+  if (!c) return MIB_E_NO_DEVICE;
+  hipSetDevice(c->device);
+  std::vector<uint64_t> ioff(k + 1, 0), ooff(k + 1, 0);
+  for (size_t i = 0; i < k; i++) {
+    ioff[i + 1] = ioff[i] + ((in[i].size + 255) & ~(size_t)255);
+    int64_t est = mib_decoded_size(in[i].data, in[i].size);
+    uint64_t cap = est > 0 ? (uint64_t)est : std::max<uint64_t>(1 << 16, 8 * (uint64_t)in[i].size);
+    ooff[i + 1] = ooff[i] + ((cap + 64 + 255) & ~(uint64_t)255);
+  }
+  uint8_t *d_in = nullptr, *d_out = nullptr;
+  if (hipMalloc(&d_in, ioff[k] + 16) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  for (size_t i = 0; i < k; i++)
+    if (in[i].size) hipMemcpy(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice);
+  std::vector<int64_t> sizes(k);
+  int rc = 0;
+  for (size_t i = 0; i < k; i++) out[i].data = nullptr, out[i].size = 0;
+  if (hipMalloc(&d_out, ooff[k] + 64) != hipSuccess) {
+    hipFree(d_in);
+    return MIB_E_OUT_OF_MEMORY;
+  }
+  // exact input lengths, padded slots
+  std::vector<mib::DecJob> jobs(k);
+  for (size_t i = 0; i < k; i++) {
+    mib::DecJob &j = jobs[i];
+    memset(&j, 0, sizeof(j));
+    j.in = d_in + ioff[i];
+    j.in_len = in[i].size;
+    j.out = d_out + ooff[i];
+    j.out_cap = ooff[i + 1] - ooff[i] - 64;
+    int64_t est = mib_decoded_size(in[i].data, in[i].size);
+    j.out_size = est > 0 ? est : -1;
+    j.max_ring_log = peek_window_bits(in[i].data, in[i].size);
+  }
+  rc = decode_jobs(c, jobs, c->stream);
+  if (rc == 0) {
+    for (size_t i = 0; i < k; i++) {
+      status[i] = jobs[i].status;
+      if (jobs[i].status == 0) {
+        uint64_t len = (uint64_t)jobs[i].result_len;
+        out[i].data = (uint8_t *)malloc(len ? len : 1);
+        out[i].size = len;
+        if (len) hipMemcpy(out[i].data, d_out + ooff[i], len, hipMemcpyDeviceToHost);
+      } else if (jobs[i].status == MIB_E_NEED_SPACE) {
+        // retry this one alone with the growing single-stream path
+        mib_buf b;
+        status[i] = mib_decode(in[i].data, in[i].size, nullptr, 0, -1, -1, &b);
+        out[i] = b;
+      }
+    }
+  }
+  hipFree(d_out);
+  hipFree(d_in);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,269 @@
+"""Python mirror of countertype/brotli-lib's public API over the brotli_amd C ABI.
+
+    brotliEncode(input, options)   src/encode/encode.ts:50-90
+    BrotliEncoder(options)         src/encode/encode.ts:290-490
+    brotliDecode(data, options)    src/decode/decode.ts:18-65   (options dict or legacy int)
+    brotliDecodedSize(data)        src/decode/decode.ts:9-11
+    EncoderMode                    src/encode/enc-constants.ts:56-60
+
+Same argument meaning and error behaviour as the reference: decoder failures raise
+``BrotliError("Brotli error code: N")`` with the reference's N, ``maxOutputSize`` raises
+``BrotliError("Decompressed size X exceeds limit Y")``.  All compute runs in the HIP
+library (libbrotli_amd.so, built in-tree by __graft_entry__.build()); there is no CPU
+fallback -- without an MI355X the calls raise.
+"""
+import ctypes
+import os
+
+__all__ = ['brotliEncode', 'BrotliEncoder', 'brotliDecode', 'brotliDecodedSize', 'EncoderMode', 'BrotliError',
+           'encode_batch', 'decode_batch', 'DeviceContext', 'library_path']
+
+_PKG = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_LIB_PATH = os.path.join(_PKG, 'libbrotli_amd.so')
+
+
+def library_path():
+    return _LIB_PATH
+
+
+class EncoderMode:
+    GENERIC = 0
+    TEXT = 1
+    FONT = 2
+
+
+class BrotliError(Exception):
+    def __init__(self, message, code=None):
+        super().__init__(message)
+        self.code = code
+
+
+class _Opts(ctypes.Structure):
+    _fields_ = [('quality', ctypes.c_int), ('lgwin', ctypes.c_int), ('mode', ctypes.c_int),
+                ('size_hint', ctypes.c_uint64)]
+
+
+class _Buf(ctypes.Structure):
+    _fields_ = [('data', ctypes.POINTER(ctypes.c_uint8)), ('size', ctypes.c_size_t)]
+
+
+class _Span(ctypes.Structure):
+    _fields_ = [('data', ctypes.c_void_p), ('size', ctypes.c_size_t)]
+
+
+class _KTime(ctypes.Structure):
+    _fields_ = [('name', ctypes.c_char * 32), ('ms', ctypes.c_double), ('launches', ctypes.c_uint32)]
+
+
+_lib = None
+
+
+def _L():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise BrotliError('brotli_amd: %s not built (run __graft_entry__.build())' % _LIB_PATH)
+        lib = ctypes.CDLL(_LIB_PATH)
+        u8p = ctypes.c_char_p
+        lib.mib_strerror.restype = ctypes.c_char_p
+        lib.mib_strerror.argtypes = [ctypes.c_int]
+        lib.mib_init.argtypes = [ctypes.c_int]
+        lib.mib_encode.argtypes = [u8p, ctypes.c_size_t, ctypes.POINTER(_Opts), ctypes.POINTER(_Buf)]
+        lib.mib_decode.argtypes = [u8p, ctypes.c_size_t, u8p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.POINTER(_Buf)]
+        lib.mib_decoded_size.argtypes = [u8p, ctypes.c_size_t]
+        lib.mib_decoded_size.restype = ctypes.c_int64
+        lib.mib_buf_free.argtypes = [ctypes.POINTER(_Buf)]
+        lib.mib_encoder_new.argtypes = [ctypes.POINTER(_Opts)]
+        lib.mib_encoder_new.restype = ctypes.c_void_p
+        lib.mib_encoder_update.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
+        lib.mib_encoder_finish.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Buf)]
+        lib.mib_encoder_free.argtypes = [ctypes.c_void_p]
+        lib.mib_encode_batch.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.POINTER(_Opts),
+                                         ctypes.POINTER(_Buf), ctypes.POINTER(ctypes.c_int)]
+        lib.mib_decode_batch.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.POINTER(_Buf),
+                                         ctypes.POINTER(ctypes.c_int)]
+        lib.mib_ctx_new.argtypes = [ctypes.c_int]
+        lib.mib_ctx_new.restype = ctypes.c_void_p
+        lib.mib_ctx_free.argtypes = [ctypes.c_void_p]
+        lib.mib_ctx_encode.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Opts), ctypes.c_void_p,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p]
+        lib.mib_ctx_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
+        lib.mib_ctx_kernel_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(_KTime), ctypes.c_int]
+        lib.mib_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib = lib
+    return _lib
+
+
+def _err(code, what=''):
+    msg = _L().mib_strerror(code).decode()
+    return BrotliError(msg, code)
+
+
+def _take(buf):
+    data = ctypes.string_at(buf.data, buf.size) if buf.size else b''
+    _L().mib_buf_free(ctypes.byref(buf))
+    return data
+
+
+def _opts(options):
+    """option clamping of encode.ts:54-71 / BrotliEncoder constructor :293-310"""
+    options = options or {}
+    o = _Opts(11, 22, EncoderMode.GENERIC, 0)
+    if options.get('quality') is not None:
+        o.quality = max(0, min(11, int(options['quality'])))
+    if options.get('lgwin') is not None:
+        o.lgwin = max(10, min(24, int(options['lgwin'])))
+    if options.get('mode') is not None:
+        o.mode = int(options['mode'])
+    if options.get('sizeHint') is not None:
+        o.size_hint = int(options['sizeHint'])
+    return o
+
+
+def _bytes(x):
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return bytes(x)
+    return bytes(bytearray(x))
+
+
+def brotliEncode(input, options=None):
+    data = _bytes(input)
+    buf = _Buf()
+    rc = _L().mib_encode(data, len(data), ctypes.byref(_opts(options)), ctypes.byref(buf))
+    if rc:
+        raise _err(rc)
+    return _take(buf)
+
+
+class BrotliEncoder:
+    """Streaming encoder: update() returns the newly completed bytes, finish() the rest."""
+
+    def __init__(self, options=None):
+        self._h = _L().mib_encoder_new(ctypes.byref(_opts(options)))
+        if not self._h:
+            raise BrotliError('brotli_amd: encoder creation failed')
+
+    def update(self, chunk):
+        data = _bytes(chunk)
+        buf = _Buf()
+        rc = _L().mib_encoder_update(self._h, data, len(data), ctypes.byref(buf))
+        if rc:
+            raise _err(rc)
+        return _take(buf)
+
+    def finish(self):
+        buf = _Buf()
+        rc = _L().mib_encoder_finish(self._h, ctypes.byref(buf))
+        if rc:
+            raise _err(rc)
+        return _take(buf)
+
+    def __del__(self):
+        if getattr(self, '_h', None):
+            _L().mib_encoder_free(self._h)
+            self._h = None
+
+
+def brotliDecodedSize(data):
+    data = _bytes(data)
+    return int(_L().mib_decoded_size(data, len(data)))
+
+
+def brotliDecode(buffer, options=None):
+    """decode.ts:18-65: options = {'maxOutputSize', 'customDictionary'} or a legacy int size."""
+    data = _bytes(buffer)
+    exact, max_out, dic = -1, -1, None
+    if isinstance(options, int) and not isinstance(options, bool):
+        exact = options
+    elif options:
+        if options.get('maxOutputSize') is not None:
+            max_out = int(options['maxOutputSize'])
+        if options.get('customDictionary') is not None:
+            dic = _bytes(options['customDictionary'])
+    buf = _Buf()
+    rc = _L().mib_decode(data, len(data), dic, len(dic) if dic is not None else 0, max_out, exact, ctypes.byref(buf))
+    if rc == -103:   # MIB_E_OUTPUT_LIMIT: the reference's wrapper message
+        size = exact if exact >= 0 else brotliDecodedSize(data)
+        raise BrotliError('Decompressed size %d exceeds limit %d' % (size, max_out), rc)
+    if rc:
+        raise _err(rc)
+    return _take(buf)
+
+
+def encode_batch(buffers, options=None):
+    """Encode independent buffers in one GPU launch sequence; returns list of bytes."""
+    k = len(buffers)
+    keep = [_bytes(b) for b in buffers]
+    spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
+    outs = (_Buf * k)()
+    st = (ctypes.c_int * k)()
+    rc = _L().mib_encode_batch(spans, k, ctypes.byref(_opts(options)), outs, st)
+    if rc:
+        raise _err(rc)
+    res = []
+    for i in range(k):
+        if st[i]:
+            raise _err(st[i])
+        res.append(_take(outs[i]))
+    return res
+
+
+def decode_batch(buffers):
+    """Decode independent streams on the GPU; returns a list of bytes or BrotliError."""
+    k = len(buffers)
+    keep = [_bytes(b) for b in buffers]
+    spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
+    outs = (_Buf * k)()
+    st = (ctypes.c_int * k)()
+    rc = _L().mib_decode_batch(spans, k, outs, st)
+    if rc:
+        raise _err(rc)
+    return [(_take(outs[i]) if st[i] == 0 else _err(st[i])) for i in range(k)]
+
+
+class DeviceContext:
+    """Device-resident batches (torch tensors / raw device pointers) for bench and the
+    multi-GPU driver; wraps mib_ctx_* of include/brotli_amd.h."""
+
+    def __init__(self, device=0, profiling=False):
+        self._c = _L().mib_ctx_new(device)
+        if not self._c:
+            raise BrotliError('brotli_amd: no usable device %d' % device)
+        _L().mib_ctx_set_profiling(self._c, 1 if profiling else 0)
+
+    def close(self):
+        if self._c:
+            _L().mib_ctx_free(self._c)
+            self._c = None
+
+    def __del__(self):
+        self.close()
+
+    def encode(self, d_in, in_offsets, d_out, out_cap, options=None, stream=None):
+        k = len(in_offsets) - 1
+        ioff = (ctypes.c_uint64 * (k + 1))(*in_offsets)
+        ooff = (ctypes.c_uint64 * (k + 1))()
+        rc = _L().mib_ctx_encode(self._c, ctypes.byref(_opts(options)), d_in, ioff, k, d_out, out_cap, ooff, stream)
+        if rc:
+            raise _err(rc)
+        return list(ooff)
+
+    def decode(self, d_in, in_offsets, d_out, out_offsets, stream=None):
+        k = len(in_offsets) - 1
+        ioff = (ctypes.c_uint64 * (k + 1))(*in_offsets)
+        ooff = (ctypes.c_uint64 * (k + 1))(*out_offsets)
+        sizes = (ctypes.c_int64 * k)()
+        st = (ctypes.c_int * k)()
+        rc = _L().mib_ctx_decode(self._c, d_in, ioff, k, d_out, ooff, sizes, st, stream)
+        if rc and rc != -104:
+            raise _err(rc)
+        return list(sizes), list(st)
+
+    def kernel_times(self):
+        arr = (_KTime * 32)()
+        n = _L().mib_ctx_kernel_times(self._c, arr, 32)
+        return {arr[i].name.decode(): (arr[i].ms, arr[i].launches) for i in range(min(n, 32))}

@@ -1,0 +1,108 @@
+/*
+ * brotli_amd -- MI355X (gfx950) Brotli encode/decode engine: the C ABI.
+ *
+ * This is the drop-in boundary for countertype/brotli-lib's public surface
+ * (package.json:7-23 exports `.`, `./encode`, `./decode`):
+ *
+ *   brotliEncode(input, {quality, lgwin, mode, sizeHint})  src/encode/encode.ts:22-27,50-90  -> mib_encode
+ *   new BrotliEncoder(opts).update(chunk) / .finish()      src/encode/encode.ts:290-409      -> mib_encoder_*
+ *   brotliDecode(data, {maxOutputSize, customDictionary} | outputSize)
+ *                                                          src/decode/decode.ts:13-65        -> mib_decode
+ *   brotliDecodedSize(data)                                src/decode/decode.ts:9-11         -> mib_decoded_size
+ *   EncoderMode {GENERIC 0, TEXT 1, FONT 2}                src/encode/enc-constants.ts:56-60 -> MIB_MODE_*
+ *
+ * plus batch entry points (host or device-resident buffers) that shard independent buffers
+ * over the GPU.  Every call is synchronous; handles are not thread-safe.
+ * All compute runs on the GPU: there is no CPU fallback, a missing device is an error.
+ *
+ * Return codes: 0 = success; the reference decoder's own negative codes (-1..-30,
+ * engine.ts makeError sites) so a host shim can throw the identical
+ * "Brotli error code: N"; MIB_E_* (<= -100) for conditions of this engine.
+ */
+#ifndef BROTLI_AMD_H_
+#define BROTLI_AMD_H_
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MIB_MODE_GENERIC 0
+#define MIB_MODE_TEXT 1
+#define MIB_MODE_FONT 2
+
+#define MIB_E_NO_DEVICE (-100)      /* no usable gfx950 device / HIP runtime error */
+#define MIB_E_INVALID_ARG (-101)
+#define MIB_E_OUT_OF_MEMORY (-102)
+#define MIB_E_OUTPUT_LIMIT (-103)   /* decoded size exceeds maxOutputSize (decode.ts:46-62) */
+#define MIB_E_NEED_SPACE (-104)     /* device buffer too small (batch/device APIs) */
+#define MIB_E_JS_RANGE_ERROR (-105) /* the reference would throw a JS RangeError here */
+#define MIB_E_JS_TYPE_ERROR (-106)  /* the reference would throw a JS TypeError here */
+#define MIB_E_NO_PROGRESS (-107)    /* decoder iteration guard tripped (never on valid input) */
+
+typedef struct {
+  int quality;        /* 0..11, default 11 (clamped like encode.ts:57-62) */
+  int lgwin;          /* 10..24, default 22 */
+  int mode;           /* MIB_MODE_* */
+  uint64_t size_hint; /* accepted, no effect (as in the reference) */
+} mib_enc_opts;
+
+typedef struct { uint8_t *data; size_t size; } mib_buf;          /* library-allocated result */
+typedef struct { const uint8_t *data; size_t size; } mib_span;   /* borrowed input */
+
+/* defaults of createDefaultParams (enc-constants.ts:209-233) */
+void mib_enc_opts_default(mib_enc_opts *o);
+
+/* Select the device (default 0) and warm the engine up; optional. */
+int mib_init(int device);
+/* Human-readable message for a return code ("Brotli error code: N" for the reference's codes). */
+const char *mib_strerror(int code);
+
+/* brotliEncode (encode.ts:50-90). */
+int mib_encode(const uint8_t *in, size_t n, const mib_enc_opts *o, mib_buf *out);
+
+/* brotliDecode (decode.ts:18-65).  exact_out >= 0: the legacy numeric `outputSize`
+ * signature (truncate / zero-pad to it); -1: none.  max_out: `maxOutputSize`, -1 = none.
+ * dict: `customDictionary` (compound-dictionary semantics, engine.ts:142-159), may be NULL. */
+int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, int64_t max_out,
+               int64_t exact_out, mib_buf *out);
+
+/* brotliDecodedSize (decode.ts:9-11 -> engine.ts:2155-2192): -1 when unknown. */
+int64_t mib_decoded_size(const uint8_t *in, size_t n);
+
+/* BrotliEncoder (encode.ts:290-490): update() returns the newly completed bytes. */
+typedef struct mib_encoder mib_encoder;
+mib_encoder *mib_encoder_new(const mib_enc_opts *o);
+int mib_encoder_update(mib_encoder *e, const uint8_t *in, size_t n, mib_buf *out);
+int mib_encoder_finish(mib_encoder *e, mib_buf *out);
+void mib_encoder_free(mib_encoder *e);
+
+/* Batches of independent buffers in host memory; one result (and status) per buffer. */
+int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status);
+int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status);
+
+void mib_buf_free(mib_buf *b);
+
+/* ---- device-resident batches (inputs already in HBM; used by bench.py and the
+ *      multi-GPU driver).  d_* are device pointers on the context's device; offsets are
+ *      host arrays of k+1 entries; `stream` is a hipStream_t (NULL = the context's own). */
+typedef struct mib_ctx mib_ctx;
+mib_ctx *mib_ctx_new(int device);
+void mib_ctx_free(mib_ctx *c);
+/* Packs the k compressed streams back to back into d_out (capacity out_cap) and fills
+ * out_offsets[0..k].  Returns 0, or MIB_E_NEED_SPACE. */
+int mib_ctx_encode(mib_ctx *c, const mib_enc_opts *o, const uint8_t *d_in, const uint64_t *in_offsets,
+                   size_t k, uint8_t *d_out, uint64_t out_cap, uint64_t *out_offsets, void *stream);
+/* Decodes k streams; stream i's output goes to d_out + out_offsets[i] with capacity
+ * out_offsets[i+1] - out_offsets[i].  out_sizes[i] / status[i] filled (host arrays). */
+int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, size_t k, uint8_t *d_out,
+                   const uint64_t *out_offsets, int64_t *out_sizes, int *status, void *stream);
+/* Per-kernel device time of the last mib_ctx_* call (ms, HIP events on the launch stream). */
+typedef struct { char name[32]; double ms; uint32_t launches; } mib_kernel_time;
+int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max);
+void mib_ctx_set_profiling(mib_ctx *c, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

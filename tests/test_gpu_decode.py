@@ -1,0 +1,102 @@
+"""HIP decoder parity (through the C ABI) against the reference's golden data and the oracle."""
+import base64
+import hashlib
+import json
+import os
+import random
+
+import pytest
+
+import _inputs
+import _oracle
+import brotli_amd
+
+pytestmark = pytest.mark.gpu
+G = _inputs.GOLDEN
+
+
+def _cases(name):
+    with open(os.path.join(G, name)) as f:
+        return json.load(f)['cases']
+
+
+def test_canonical_vectors_bit_exact():
+    n = 0
+    for nm in sorted(os.listdir(os.path.join(G, 'vectors'))):
+        if '.compressed' not in nm:
+            continue
+        with open(os.path.join(G, 'vectors', nm), 'rb') as f:
+            comp = f.read()
+        with open(os.path.join(G, 'vectors', nm.split('.compressed')[0]), 'rb') as f:
+            exp = f.read()
+        assert brotli_amd.brotliDecode(comp) == exp, nm
+        n += 1
+    assert n == 45
+
+
+def test_bench_streams_match_reference_hashes():
+    for c in _cases('decode_vectors.json'):
+        with open(os.path.join(G, c['path']), 'rb') as f:
+            out = brotli_amd.brotliDecode(f.read())
+        assert hashlib.sha256(out).hexdigest() == c['sha256'], c['path']
+
+
+def test_error_corpus_matches_reference():
+    """same bytes or the same 'Brotli error code: N' as the reference on ~700 corrupted streams"""
+    for c in _cases('decode_errors.json'):
+        data = base64.b64decode(c['in_b64'])
+        if c.get('hang'):
+            # the reference never returns (Bug J); we return what the oracle (Bug J fixed) returns
+            exp = _oracle.decode(data)
+        elif 'error' in c:
+            exp = c['error']
+        else:
+            exp = c['sha256']
+        try:
+            got = hashlib.sha256(brotli_amd.brotliDecode(data)).hexdigest()
+        except brotli_amd.BrotliError as e:
+            got = str(e)
+        if isinstance(exp, int):
+            exp = 'Brotli error code: %d' % exp
+        elif isinstance(exp, bytes):
+            exp = hashlib.sha256(exp).hexdigest()
+        assert got == exp, (c['in_b64'][:60], got, exp)
+
+
+def test_batch_decode_matches_oracle():
+    streams, exps = [], []
+    for nm in sorted(os.listdir(os.path.join(G, 'vectors'))):
+        if '.compressed' in nm:
+            with open(os.path.join(G, 'vectors', nm), 'rb') as f:
+                streams.append(f.read())
+            exps.append(_oracle.decode(streams[-1]))
+    outs = brotli_amd.decode_batch(streams)
+    assert outs == exps
+
+
+def test_decode_options_semantics():
+    """maxOutputSize (decode.ts:46-62), legacy outputSize truncation / zero padding (engine.ts:2210-2220)"""
+    with open(os.path.join(G, 'vectors', 'alice29.txt.compressed'), 'rb') as f:
+        comp = f.read()
+    with open(os.path.join(G, 'vectors', 'alice29.txt'), 'rb') as f:
+        plain = f.read()
+    with pytest.raises(brotli_amd.BrotliError, match='exceeds limit'):
+        brotli_amd.brotliDecode(comp, {'maxOutputSize': 1000})
+    assert brotli_amd.brotliDecode(comp, {'maxOutputSize': len(plain)}) == plain
+    assert brotli_amd.brotliDecode(comp, 100) == _oracle.decode(comp, 100) == plain[:100]
+    assert brotli_amd.brotliDecode(comp, len(plain) + 50) == _oracle.decode(comp, len(plain) + 50)
+
+
+def test_random_truncations_match_oracle():
+    rng = random.Random(7)
+    with open(os.path.join(G, 'bench', 'enc-ttf.br'), 'rb') as f:
+        comp = f.read()
+    for _ in range(40):
+        cut = rng.randrange(len(comp))
+        data = comp[:cut]
+        exp = _oracle.decode(data)
+        try:
+            got = brotli_amd.brotliDecode(data)
+        except brotli_amd.BrotliError as e:
+            got = e.code
+        assert got == exp, cut
