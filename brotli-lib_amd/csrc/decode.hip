@@ -839,17 +839,20 @@ __device__ int copy_from_compound(Dec &s, int fence) {
 }
 
 // LZ77 copy of `cl` bytes at ring position pos from distance dist (no fence crossing).
+// An overlapping copy (dist < cl) repeats the dist bytes before pos, so every byte is a
+// function of pre-copy data only: out[pos + j] = ring[src + j % dist]; all 64 lanes work.
 __device__ void ring_copy_fast(Dec &s, int src, int cl, int dist) {
   uint8_t *r = s.ring;
   int dst = s.pos;
   if (dist >= cl) {
     for (int k = s.lane; k < cl; k += 64) r[dst + k] = r[src + k];
   } else {
-    int chunk = dist < 64 ? dist : 64;
-    for (int off = 0; off < cl; off += chunk) {
-      int k = off + s.lane;
-      if (s.lane < chunk && k < cl) r[dst + k] = r[src + k];
-      wave_sync();
+    int q = s.lane % dist;
+    int qstep = 64 % dist;
+    for (int k = s.lane; k < cl; k += 64) {
+      r[dst + k] = r[src + q];
+      q += qstep;
+      if (q >= dist) q -= dist;
     }
   }
   wave_sync();
@@ -1048,14 +1051,17 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               while (s.j < s.copy_len) {
                 int rem = s.copy_len - s.j;
                 int room = fence - s.pos;
-                int chunk = rem < 64 ? rem : 64;
-                if (dist < chunk) chunk = dist;
+                int chunk = rem < 4096 ? rem : 4096;
+                if (dist >= s.ring_size - 4096) chunk = rem < 64 ? rem : 64;
                 if (dist >= s.ring_size - 64) chunk = 1;
                 if (room < chunk) chunk = room;
                 if (chunk < 1) chunk = 1;
-                if (s.lane < chunk) {
-                  int p = s.pos + s.lane;
-                  uint8_t v = ring[(p - dist) & rmask];
+                // byte p copies the byte dist back, or (overlap) its periodic image before pos
+                int base = s.pos - dist;
+                for (int k = s.lane; k < chunk; k += 64) {
+                  int p = s.pos + k;
+                  int srcp = base + (dist > k ? k : k % dist);
+                  uint8_t v = ring[srcp & rmask];
                   if (p < s.ring_cap) ring[p] = v;
                 }
                 wave_sync();
@@ -1223,7 +1229,8 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     // bits or produces output), low enough that a bug cannot spin a GPU forever
     s.guard = 0;
     s.guard_limit = 64ull * (job.in_len + 64) * 8 + 4ull * job.out_cap + (1ull << 26);
-    // initState (:160-178)
+    // initState (:160-178): fresh zeroed byteBuffer (its stale tail is observable) and block trees
+    for (int i = lane; i < (int)sizeof(lds.win); i += 64) lds.win[i] = 0;
     for (int i = lane; i <= kBlockTreesCap; i += 64) lds.block_trees[i] = 0;
     __syncthreads();
     if (lane == 0) lds.block_trees[0] = 7;

@@ -384,7 +384,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     rc = decode_jobs(c, jobs, c->stream);
     if (rc) break;
     rc = jobs[0].status;
-    if (rc == MIB_E_NEED_SPACE && !known && cap < ((uint64_t)1 << 33)) {
+    if (rc == MIB_E_NEED_SPACE && !known && cap < ((uint64_t)1 << 31)) {   // JS caps a Uint8Array near 2^31
       hipFree(d_out);
       d_out = nullptr;
       cap *= 4;
