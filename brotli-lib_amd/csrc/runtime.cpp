@@ -253,6 +253,12 @@ void mib_ctx_free(mib_ctx *c) {
 
 void mib_ctx_set_profiling(mib_ctx *c, int on) { c->profiling = on != 0; }
 
+// internal (encode.hip)
+mib_ctx *mib_default_ctx(void) { return default_ctx(); }
+void *mib_ctx_stream_of(mib_ctx *c) { return (void *)c->stream; }
+int mib_ctx_device_of(mib_ctx *c) { return c->device; }
+void mib_ctx_clear_times(mib_ctx *c) { c->times.clear(); }
+
 int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max) {
   int n = std::min<int>(max, (int)c->times.size());
   for (int i = 0; i < n; i++) out[i] = c->times[i];

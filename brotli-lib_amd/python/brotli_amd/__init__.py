@@ -63,6 +63,13 @@ def _L():
     if _lib is None:
         if not os.path.exists(_LIB_PATH):
             raise BrotliError('brotli_amd: %s not built (run __graft_entry__.build())' % _LIB_PATH)
+        # PyTorch-ROCm ships its own libamdhip64 (same soname).  Loading torch first makes the
+        # library bind to that one runtime; the other order would put two HIP runtimes in the
+        # process and torch's device init would fail.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(_LIB_PATH)
         u8p = ctypes.c_char_p
         lib.mib_strerror.restype = ctypes.c_char_p
