@@ -202,3 +202,74 @@ def glyf_stream(length, seed=1000):
     if len(out) < length:
         out = (out * (length // max(1, len(out)) + 1))
     return out[:length]
+
+
+def enwik_device(total, seed, device):
+    """``total`` bytes of enwik-style text generated directly in device memory (torch).
+
+    Same piece tables and distributions as ``enwik_text`` (so the same statistics), drawn
+    with a seeded torch generator on the device: one GiB takes well under a second, where
+    the numpy path needs ~100 s.  Deterministic for (total, seed) on a given torch build;
+    it is bench input only -- parity fixtures use ``enwik_text``.
+    """
+    import torch
+    words, cdf = _words()
+    rng = np.random.default_rng(0x5EED0000 + seed)
+    nw = len(words)
+    caps = [w[:1].upper() + w[1:] for w in words]
+    seps = [b' ', b', ', b'. ', b'.\n', b'\n', b'; ', b' (', b') ', b': ', b'\n\n']
+    sep_p = np.array([0.80, 0.06, 0.05, 0.015, 0.035, 0.01, 0.008, 0.008, 0.007, 0.007])
+    marks = [(b'', b''), (b'[[', b']]'), (b'{{', b'}}'), (b"'''", b"'''"), (b'&quot;', b'&quot;'), (b'[[Category:', b']]')]
+    mark_p = np.array([0.925, 0.045, 0.006, 0.012, 0.008, 0.004])
+    headers = []
+    for h in range(512):
+        t = rng.integers(0, min(nw, 3000), size=3)
+        title = ' '.join(caps[i] for i in t[: 1 + h % 3])
+        pid = int(rng.integers(1, 10 ** 7))
+        headers.append(('</text>\n  </page>\n  <page>\n    <title>%s</title>\n    <id>%d</id>\n'
+                        '    <revision><id>%d</id><timestamp>20%02d-%02d-%02dT12:00:00Z</timestamp></revision>\n'
+                        '    <text xml:space="preserve">' % (title, pid, pid * 7 + 13, h % 9 + 1, h % 12 + 1,
+                                                              h % 28 + 1)).encode())
+    pieces = [b''] + [w.encode() for w in words] + [c.encode() for c in caps] + seps
+    pieces += [m[0] for m in marks] + [m[1] for m in marks] + headers
+    W0, C0 = 1, 1 + nw
+    S0 = C0 + nw
+    MP0 = S0 + len(seps)
+    MS0 = MP0 + len(marks)
+    H0 = MS0 + len(marks)
+    flat, starts, lens = _pieces_table(pieces)
+    dev = torch.device(device)
+    flat_t = torch.from_numpy(flat.copy()).to(dev)
+    starts_t = torch.from_numpy(starts).to(dev)
+    lens_t = torch.from_numpy(lens).to(dev)
+    cdf_t = torch.from_numpy(cdf).to(dev)
+    sep_pt = torch.from_numpy(sep_p / sep_p.sum()).to(dev)
+    mark_pt = torch.from_numpy(mark_p / mark_p.sum()).to(dev)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0000 + seed)
+    out = torch.empty(total, dtype=torch.uint8, device=dev)
+    have = 0
+    while have < total:
+        n = int(min(max(4096, (total - have) // 5), 1 << 23))
+        wid = torch.searchsorted(cdf_t, torch.rand(n, generator=g, device=dev, dtype=torch.float64)).clamp_(max=nw - 1)
+        sep = torch.multinomial(sep_pt, n, replacement=True, generator=g)
+        cap = torch.zeros(n, dtype=torch.bool, device=dev)
+        cap[1:] = (sep[:-1] == 2) | (sep[:-1] == 3) | (sep[:-1] == 9)
+        word_piece = torch.where(cap, C0 + wid, W0 + wid)
+        mk = torch.multinomial(mark_pt, n, replacement=True, generator=g)
+        pre = torch.where(mk > 0, MP0 + mk, torch.zeros_like(mk))
+        suf = torch.where(mk > 0, MS0 + mk, torch.zeros_like(mk))
+        sep_piece = S0 + sep
+        brk = torch.rand(n, generator=g, device=dev) < 1.0 / 900
+        hdr = H0 + torch.randint(0, len(headers), (n,), generator=g, device=dev)
+        sep_piece = torch.where(brk, hdr, sep_piece)
+        ids = torch.stack([pre, word_piece, suf, sep_piece], dim=1).reshape(-1)
+        ln = lens_t[ids]
+        csum = torch.cumsum(ln, 0)
+        tot = int(csum[-1])
+        take = min(tot, total - have)
+        base = torch.repeat_interleave(starts_t[ids] - (csum - ln), ln, output_size=tot)
+        idx = base + torch.arange(tot, device=dev)
+        out[have:have + take] = flat_t[idx[:take]]
+        have += take
+    return out
