@@ -1272,3 +1272,20 @@ extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t 
 extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut) {
   return hipMemcpyToSymbol(HIP_SYMBOL(mib::kCmdLut), host_lut, sizeof(int16_t) * 704 * 4);
 }
+
+// First two bytes of each stream (window bits peek for scratch sizing) in one launch.
+namespace mib {
+__global__ void peek_heads_kernel(const uint8_t *in, const uint64_t *offsets, int k, uint8_t *heads) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) {
+    uint64_t a = offsets[i], n = offsets[i + 1] - a;
+    heads[2 * i] = n > 0 ? in[a] : 0;
+    heads[2 * i + 1] = n > 1 ? in[a + 1] : 0;
+  }
+}
+}  // namespace mib
+
+extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t *d_offsets, int k, uint8_t *d_heads,
+                                            hipStream_t stream) {
+  hipLaunchKernelGGL(mib::peek_heads_kernel, dim3((k + 255) / 256), dim3(256), 0, stream, d_in, d_offsets, k, d_heads);
+  return hipGetLastError();
+}

@@ -174,53 +174,100 @@ __global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint3
     vals[g] = g;
   }
 }
-__global__ void rank_kernel(const uint32_t *sorted_vals, uint32_t total, uint32_t *rank) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x)
-    rank[sorted_vals[i]] = i;
+// ---------------------------------------------------------------- 2. matches
+// One thread per SORTED entry: a bucket is a run of equal keys with positions ascending, so
+// the candidates of entry r are entries r-1, r-2, ... (most recent first) -- the
+// reference's hash chain / tree candidates (hash-binary-tree.ts:156-227), depth by
+// quality.  A 256-entry tile plus the 64 entries before it is staged in LDS with the 8
+// bytes following each position, so most candidates are rejected or measured without
+// touching HBM; only matches of 8+ bytes extend through global memory.  The staircase of
+// strictly increasing lengths (shortest distance for each length) is kept, longest last.
+constexpr int kTile = 256;
+constexpr int kBack = 64;
+
+__device__ __forceinline__ uint64_t load_prefix8(const uint8_t *p, uint32_t avail) {
+  if (avail >= 8) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (8 * i);
+    return v;
+  }
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < avail; i++) v |= (uint64_t)p[i] << (8 * i);
+  return v;
 }
 
-// ---------------------------------------------------------------- 2. matches
-// Per position: walk the bucket backwards (most recent first) up to `depth` candidates,
-// keep the staircase of strictly increasing lengths (shortest distance for each length).
-__global__ void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
-                                    const uint32_t *sorted_vals, const uint32_t *rank, uint32_t total, int depth,
-                                    uint64_t *matches, uint8_t *nmatch) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
-    uint32_t j = pos_job[g >> kSegBits];
-    const Job &jb = jobs[j];
-    uint32_t p = g - jb.pos_base;
-    uint32_t r = rank[g];
-    uint32_t key = sorted_keys[r];
-    int cnt = 0;
-    if (key != kInvalidKey) {
-      uint32_t max_dist = (1u << jb.lgwin) - 16;
-      uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
-      uint32_t limit = seg_end - p;          // copies never cross a parse segment
-      const uint8_t *cur = jb.data + p;
-      uint32_t best = 3;
-      uint64_t local[kMaxMatches];
-      for (int t = 1; t <= depth && r >= (uint32_t)t; t++) {
-        if (sorted_keys[r - t] != key) break;
-        uint32_t c = sorted_vals[r - t] - jb.pos_base;
-        uint32_t d = p - c;
-        if (d > max_dist) break;
-        if (best >= limit) break;
-        if (cur[best] != jb.data[c + best]) continue;
-        uint32_t len = match_len(cur, jb.data + c, limit);
-        if (len > best) {
-          best = len;
-          if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
-            for (int q = 1; q < kMaxMatches; q++) local[q - 1] = local[q];
-            cnt--;
-          }
-          local[cnt++] = ((uint64_t)d << 32) | len;
-          if (len >= limit || len >= 4096) break;
-        }
+__global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *sorted_keys,
+                                                             const uint32_t *sorted_vals, uint32_t total, int depth,
+                                                             uint64_t *matches, uint8_t *nmatch) {
+  __shared__ uint32_t skey[kTile + kBack];
+  __shared__ uint32_t spos[kTile + kBack];
+  __shared__ uint64_t spre[kTile + kBack];
+  const uint32_t r0 = blockIdx.x * kTile;
+  for (int t = threadIdx.x; t < kTile + kBack; t += kTile) {
+    int64_t r = (int64_t)r0 - kBack + t;
+    uint32_t key = 0xFFFFFFFEu, g = 0;
+    uint64_t pre = 0;
+    if (r >= 0 && r < (int64_t)total) {
+      key = sorted_keys[r];
+      g = sorted_vals[r];
+      if (key != kInvalidKey) {
+        const Job &jb = jobs[key >> 17];
+        uint32_t p = g - jb.pos_base;
+        pre = load_prefix8(jb.data + p, jb.n - p);
       }
-      for (int q = 0; q < cnt; q++) matches[(uint64_t)g * kMaxMatches + q] = local[q];
     }
-    nmatch[g] = (uint8_t)cnt;
+    skey[t] = key;
+    spos[t] = g;
+    spre[t] = pre;
   }
+  __syncthreads();
+  const uint32_t r = r0 + threadIdx.x;
+  if (r >= total) return;
+  const int me = kBack + threadIdx.x;
+  const uint32_t key = skey[me], g = spos[me];
+  int cnt = 0;
+  if (key != kInvalidKey) {
+    const Job &jb = jobs[key >> 17];
+    const uint32_t p = g - jb.pos_base;
+    const uint32_t max_dist = (1u << jb.lgwin) - 16;
+    const uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
+    const uint32_t limit = seg_end - p;   // copies never cross a parse segment
+    const uint8_t *cur = jb.data + p;
+    const uint64_t mine = spre[me];
+    uint32_t best = 3;
+    uint64_t local[kMaxMatches];
+    const int dmax = min(depth, kBack);
+    for (int t = 1; t <= dmax; t++) {
+      const int e = me - t;
+      if (skey[e] != key) break;
+      const uint32_t d = g - spos[e];
+      if (d > max_dist || best >= limit) break;
+      const uint64_t x = mine ^ spre[e];
+      uint32_t len;
+      if (x) {
+        len = (uint32_t)(__ffsll((unsigned long long)x) - 1) >> 3;
+        if (len <= best) continue;
+        len = min(len, limit);
+      } else {
+        const uint8_t *cand = cur - d;
+        if (best >= 8 && cur[best] != cand[best]) continue;
+        len = 8 + match_len(cur + 8, cand + 8, limit > 8 ? limit - 8 : 0);
+        len = min(len, limit);
+      }
+      len = min(len, 65535u);   // copy lengths travel as u16 through the parse
+      if (len > best) {
+        best = len;
+        if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
+          for (int q = 1; q < kMaxMatches; q++) local[q - 1] = local[q];
+          cnt--;
+        }
+        local[cnt++] = ((uint64_t)d << 32) | len;
+        if (len >= limit || len >= 4096) break;
+      }
+    }
+    for (int q = 0; q < cnt; q++) matches[(uint64_t)g * kMaxMatches + q] = local[q];
+  }
+  nmatch[g] = (uint8_t)cnt;
 }
 
 // ---------------------------------------------------------------- literal cost model per stream
@@ -237,18 +284,50 @@ __global__ void lit_histo_kernel(const Job *jobs, const Seg *segs, uint32_t *lit
 }
 
 // ---------------------------------------------------------------- 3. DP parse, wave per segment
-__device__ __forceinline__ float fast_log2f(float v) { return __log2f(v); }
+// Shortest path over positions (updateNodes / computeShortestPathFromNodes,
+// backward-references-hq.ts:267-406): node i holds the cheapest cost of reaching i, the
+// insert length since the last copy, and the path's last distance.  Edges: one literal;
+// the staircase matches of i (lanes relax consecutive lengths in parallel); a copy at the
+// path's last distance (short code 0).  A match longer than kLongCopy is taken outright and
+// the parse jumps to its end, as the reference does (:518-533).
+//
+// Everything a position needs that does not depend on the DP state (its matches, its
+// literal byte, the bytes ahead) is staged into LDS 64 positions at a time with coalesced
+// loads; the only load left inside the serial loop is the 64-byte window at the path's
+// last distance, issued before the relaxations that hide it.
+constexpr int kBatch = 64;
+// The DP block is one wave: LDS traffic of a wave is processed in order, so a compiler
+// fence at wavefront scope is all the lanes need between dependent LDS steps (a
+// workgroup barrier would also drain the outstanding global stores/loads every time).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+constexpr int kWin = kBatch + 64;
+constexpr float kInf = 3.0e38f;
+constexpr int kChunks = (kLongCopy + 64) / 64;   // length chunks of 64 lanes covering 0..kLongCopy
+
+// node meta: last distance (32) | copy length that reached it (16, 0 = literal) | insert length (16)
+__device__ __forceinline__ uint64_t pack_node(uint32_t ld, uint32_t clen, uint32_t ins) {
+  return (uint64_t)ld | ((uint64_t)clen << 32) | ((uint64_t)min(ins, 65535u) << 48);
+}
+__device__ __forceinline__ uint64_t node_choice(uint64_t m) {   // (distance << 32) | length, 0 = literal
+  uint32_t cl = (uint32_t)(m >> 32) & 0xFFFF;
+  return cl ? (((uint64_t)(uint32_t)m << 32) | cl) : 0ull;
+}
 
 __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, const uint32_t *lit_histo,
                                                 const uint64_t *matches, const uint8_t *nmatch,
                                                 uint64_t *choice /* per position+1 */) {
   __shared__ float cost[kRing];
-  __shared__ uint32_t ins[kRing];
-  __shared__ uint32_t lastd[kRing];
-  __shared__ uint64_t ch[kRing];
+  __shared__ uint64_t meta[kRing];
   __shared__ float litc[256];
   __shared__ float cmdc[704];
   __shared__ float distc[128];
+  __shared__ uint8_t win[kWin];
+  __shared__ uint8_t bnm[kBatch];
+  __shared__ uint64_t bmt[kBatch * kMaxMatches];   // (distance << 32) | length
+  __shared__ float bmc[kBatch * kMaxMatches];      // distance symbol cost + extra bits
   const int lane = threadIdx.x;
   const Seg sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
@@ -268,128 +347,184 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
     for (int i = lane; i < 128; i += 64) distc[i] = log2f(20.f + i);
   }
   for (int i = lane; i < kRing; i += 64) {
-    cost[i] = 3.0e38f;
-    ins[i] = 0;
-    lastd[i] = 0;
-    ch[i] = 0;
+    cost[i] = kInf;
+    meta[i] = 0;
   }
-  __syncthreads();
+  // copy code / extra bits of the lengths this lane relaxes (l = 64 k + lane)
+  int ccl[kChunks];
+  float cxl[kChunks];
+#pragma unroll
+  for (int k = 0; k < kChunks; k++) {
+    uint32_t l = max(2u, (uint32_t)(64 * k + lane));
+    ccl[k] = copy_code(l);
+    cxl[k] = (float)kCopyExtra[ccl[k]];
+  }
+  wave_sync();
   const uint32_t a = sg.start, b = sg.end;
   const uint32_t gbase = jb.pos_base;
   if (lane == 0) cost[a % kRing] = 0.f;
-  __syncthreads();
-  for (uint32_t i = a; i < b;) {
-    const int slot = i % kRing;
-    const float ci = cost[slot];
-    const uint32_t ins_i = ins[slot], ld = lastd[slot];
-    // the start node belongs to the previous segment's end (written there)
-    if (lane == 0 && i != a) choice[gbase + i] = ch[slot];
-    __syncthreads();
-    if (lane == 0) cost[slot] = 3.0e38f;   // slot now free for position i + kRing
-    // literal edge
+  // the path's last distance: verified run [c_from, c_upto) of data[p] == data[p - c_ld]
+  uint32_t c_ld = 0, c_from = 0, c_upto = 0;
+  bool c_end = false;   // c_upto is a mismatch (or the segment end), not just "verified so far"
+  uint32_t i = a;
+  while (i < b) {
+    // ---- stage the next batch: matches and their distance costs, literal bytes
+    const uint32_t i0 = i;
+    const uint32_t nb = min((uint32_t)kBatch, b - i0);
+    wave_sync();
     {
-      int ns = (i + 1) % kRing;
-      float c = ci + litc[data[i]];
-      if (lane == 0 && c < cost[ns]) {
-        cost[ns] = c;
-        ins[ns] = ins_i + 1;
-        lastd[ns] = ld;
-        ch[ns] = 0;   // literal
+      int nm = 0;
+      if ((uint32_t)lane < nb) nm = nmatch[gbase + i0 + lane];
+      bnm[lane] = (uint8_t)nm;
+      const uint64_t *src = matches + (uint64_t)(gbase + i0 + lane) * kMaxMatches;
+      for (int q = 0; q < nm; q++) {
+        uint64_t m = src[q];
+        uint32_t extra;
+        uint32_t dp = dist_prefix((uint32_t)(m >> 32) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
+        bmt[lane * kMaxMatches + q] = m;
+        bmc[lane * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
       }
+      for (int t = lane; t < kWin; t += 64) win[t] = (i0 + t < b) ? data[i0 + t] : 0;
     }
-    __syncthreads();
-    const int ic = ins_code(ins_i);
-    const float base = ci + (float)kInsExtra[ic];
-    const uint32_t limit = b - i;
-    // copy at the last distance of the path (short code 0): lanes compare 64 bytes at a time
-    if (ld != 0 && ld <= i) {
-      uint32_t len = 0;
-      for (;;) {
-        uint32_t k = len + lane;
-        bool eq = k < limit && data[i + k] == data[i - ld + k];
-        uint64_t ok = __ballot(eq);
-        if (ok == ~0ull) {
-          len += 64;
-          if (len >= limit || len >= kLongCopy) break;
-          continue;
+    wave_sync();
+    bool forced = false;
+    while (i < i0 + nb) {
+      const int slot = i % kRing;
+      const float ci = cost[slot];
+      const uint64_t mi = meta[slot];
+      const uint32_t ld = (uint32_t)mi, ins_i = (uint32_t)(mi >> 48);
+      const uint32_t off = i - i0;
+      const uint32_t limit = b - i;
+      wave_sync();
+      if (lane == 0) {
+        cost[slot] = kInf;   // the slot now serves position i + kRing
+        const int ns = (i + 1) % kRing;
+        const float c = ci + litc[win[off]];
+        if (c < cost[ns]) {
+          cost[ns] = c;
+          meta[ns] = pack_node(ld, 0, ins_i + 1);
         }
-        len += __ffsll((unsigned long long)~ok) - 1;
-        break;
       }
-      len = min(len, min(limit, (uint32_t)kLongCopy));
-      for (uint32_t l0 = 2; l0 <= len; l0 += 64) {
-        uint32_t l = l0 + lane;
-        if (l <= len) {
-          int cc = copy_code(l);
-          int cmd = combine_codes(ic, cc, true);
-          float c = base + (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-          int ts = (i + l) % kRing;
-          if (c < cost[ts]) {
-            cost[ts] = c;
-            ins[ts] = 0;
-            lastd[ts] = ld;
-            ch[ts] = ((uint64_t)ld << 32) | l;
+      wave_sync();
+      const int ic = ins_code(ins_i);
+      const float base = ci + (float)kInsExtra[ic];
+      // ---- copy at the path's last distance (short code 0): run length from the cache
+      uint32_t ldlen = 0;
+      if (ld != 0 && ld <= i) {
+        if (!(ld == c_ld && i >= c_from && i <= c_upto)) {
+          c_ld = ld;
+          c_from = c_upto = i;
+          c_end = false;
+        }
+        while (!c_end && c_upto - i <= (uint32_t)kLongCopy) {
+          const uint32_t k = c_upto + lane;
+          const bool eq = k < b && data[k] == data[k - ld];
+          const uint64_t ok = __ballot(eq);
+          if (ok == ~0ull) {
+            c_upto += 64;
+          } else {
+            c_upto += __ffsll((unsigned long long)~ok) - 1;
+            c_end = true;
           }
         }
+        ldlen = min(c_upto - i, limit);
       }
-      __syncthreads();
-    }
-    // hash matches: staircase of (distance, length)
-    const int nm = nmatch[gbase + i];
-    uint32_t prev_len = 3;
-    uint32_t skip_to = 0;
-    for (int q = 0; q < nm; q++) {
-      uint64_t m = matches[(uint64_t)(gbase + i) * kMaxMatches + q];
-      uint32_t d = (uint32_t)(m >> 32), L = min((uint32_t)m, limit);
-      if (L <= prev_len) continue;
-      uint32_t extra;
-      uint32_t dp = dist_prefix(d + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
-      float dcost = base + (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
-      if (L > (uint32_t)kLongCopy) {
-        // forceful long copy (the reference keeps only the longest match and skips ahead,
-        // backward-references-hq.ts:518-533): commit the path through i
-        int cc = copy_code(L);
-        int cmd = combine_codes(ic, cc, false);
-        float c = dcost + (float)kCopyExtra[cc] + cmdc[cmd];
-        skip_to = i + L;
-        // every pending node is abandoned: the parse continues from the copy's end
-        __syncthreads();
-        for (int t = lane; t < kRing; t += 64) cost[t] = 3.0e38f;
-        __syncthreads();
+      uint32_t fd = 0, fl = 0;   // forced long copy
+      float fc = 0.f;
+      if (ldlen > (uint32_t)kLongCopy) {
+        while (!c_end && c_upto - i < 65535u) {   // take the whole run
+          const uint32_t k = c_upto + lane;
+          const bool eq = k < b && data[k] == data[k - ld];
+          const uint64_t ok = __ballot(eq);
+          if (ok == ~0ull) {
+            c_upto += 64;
+          } else {
+            c_upto += __ffsll((unsigned long long)~ok) - 1;
+            c_end = true;
+          }
+        }
+        fl = min(min(c_upto - i, limit), 65535u);
+        fd = ld;
+        const int cc = copy_code(fl);
+        const int cmd = combine_codes(ic, cc, true);
+        fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+      } else {
+        // ---- hash matches: the staircase of (distance, length)
+        const int nm = bnm[off];
+        uint32_t prev_len = 3;
+        for (int q = 0; q < nm; q++) {
+          const uint64_t m = bmt[off * kMaxMatches + q];
+          const uint32_t d = (uint32_t)(m >> 32), L = min((uint32_t)m, limit);
+          if (L <= prev_len) continue;
+          const float dcost = base + bmc[off * kMaxMatches + q];
+          if (L > (uint32_t)kLongCopy) {
+            fd = d;
+            fl = L;
+            const int cc = copy_code(L);
+            fc = dcost + (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
+            break;
+          }
+#pragma unroll
+          for (int k = 0; k < kChunks; k++) {
+            if (64 * k + 63 <= (int)prev_len || 64 * k > (int)L) continue;
+            const uint32_t l = 64 * k + lane;
+            if (l > prev_len && l <= L) {
+              const float c = dcost + cxl[k] + cmdc[combine_codes(ic, ccl[k], false)];
+              const int ts = (i + l) % kRing;
+              if (c < cost[ts]) {
+                cost[ts] = c;
+                meta[ts] = pack_node(d, l, 0);
+              }
+            }
+          }
+          prev_len = L;
+        }
+        wave_sync();
+        if (!fl && ldlen >= 2) {
+#pragma unroll
+          for (int k = 0; k < kChunks; k++) {
+            if (64 * k > (int)ldlen) continue;
+            const uint32_t l = 64 * k + lane;
+            if (l >= 2 && l <= ldlen) {
+              const int cmd = combine_codes(ic, ccl[k], true);
+              const float c = base + cxl[k] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+              const int ts = (i + l) % kRing;
+              if (c < cost[ts]) {
+                cost[ts] = c;
+                meta[ts] = pack_node(ld, l, 0);
+              }
+            }
+          }
+          wave_sync();
+        }
+      }
+      if (fl) {
+        // forceful long copy (backward-references-hq.ts:518-533): flush the batch's
+        // finished nodes, abandon every pending node, resume at the copy's end
+        for (uint32_t p = i0 + lane; p <= i; p += 64)
+          if (p != a) choice[gbase + p] = node_choice(meta[p % kRing]);
+        wave_sync();
+        for (int t = lane; t < kRing; t += 64) cost[t] = kInf;
+        wave_sync();
+        const uint32_t skip_to = i + fl;
         if (lane == 0) {
-          ch[skip_to % kRing] = ((uint64_t)d << 32) | L;
-          cost[skip_to % kRing] = c;
-          ins[skip_to % kRing] = 0;
-          lastd[skip_to % kRing] = d;
+          cost[skip_to % kRing] = fc;
+          meta[skip_to % kRing] = pack_node(fd, fl, 0);
         }
+        wave_sync();
+        i = skip_to;
+        forced = true;
         break;
       }
-      for (uint32_t l0 = prev_len + 1; l0 <= L; l0 += 64) {
-        uint32_t l = l0 + lane;
-        if (l <= L) {
-          int cc = copy_code(l);
-          int cmd = combine_codes(ic, cc, false);
-          float c = dcost + (float)kCopyExtra[cc] + cmdc[cmd];
-          int ts = (i + l) % kRing;
-          if (c < cost[ts]) {
-            cost[ts] = c;
-            ins[ts] = 0;
-            lastd[ts] = d;
-            ch[ts] = ((uint64_t)d << 32) | l;
-          }
-        }
-      }
-      prev_len = L;
+      i++;
     }
-    __syncthreads();
-    if (skip_to) {   // positions inside the forced copy get no outgoing edges
-      i = skip_to;
-      continue;
+    if (!forced) {   // the batch's nodes are final: one coalesced store of their choices
+      const uint32_t p = i0 + lane;
+      if ((uint32_t)lane < nb && p != a) choice[gbase + p] = node_choice(meta[p % kRing]);
     }
-    i++;
   }
   // the segment's end node
-  if (lane == 0) choice[gbase + b] = ch[b % kRing];
+  if (lane == 0) choice[gbase + b] = node_choice(meta[b % kRing]);
 }
 
 // ---------------------------------------------------------------- 4. backtrack, lane per segment
@@ -1309,7 +1444,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   }
   Arena ar{ws->buf};
   uint32_t *keys = ar.take<uint32_t>(total), *vals = ar.take<uint32_t>(total);
-  uint32_t *skeys = ar.take<uint32_t>(total), *svals = ar.take<uint32_t>(total), *rank = ar.take<uint32_t>(total);
+  uint32_t *skeys = ar.take<uint32_t>(total), *svals = ar.take<uint32_t>(total);
   void *sort_ws = ar.take<uint8_t>(sort_tmp);
   uint64_t *matches = ar.take<uint64_t>((size_t)total * kMaxMatches);
   uint8_t *nmatch = ar.take<uint8_t>(total);
@@ -1354,12 +1489,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.start("radix_sort");
     CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, 32, st));
     tm.stop();
-    tm.start("rank");
-    hipLaunchKernelGGL(rank_kernel, dim3(pgrid), dim3(256), 0, st, svals, total, rank);
-    tm.stop();
     tm.start("find_matches");
-    hipLaunchKernelGGL(find_matches_kernel, dim3(pgrid), dim3(256), 0, st, d_jobs, d_seg_job, skeys, svals, rank, total,
-                       depth, matches, nmatch);
+    hipLaunchKernelGGL(find_matches_kernel, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, d_jobs, skeys, svals,
+                       total, depth, matches, nmatch);
     tm.stop();
     tm.start("lit_histo");
     hipLaunchKernelGGL(lit_histo_kernel, dim3(nsegs), dim3(256), 0, st, d_jobs, d_segs, lit_h);

@@ -19,6 +19,8 @@
 extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
                                         uint64_t ring_bytes, int grid, hipStream_t stream);
 extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut);
+extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t *d_offsets, int k, uint8_t *d_heads,
+                                            hipStream_t stream);
 
 
 
@@ -104,6 +106,8 @@ struct mib_ctx {
   uint64_t scratch_bytes = 0;
   mib::DecJob *d_jobs = nullptr;
   size_t jobs_cap = 0;
+  uint8_t *d_aux = nullptr;   // small per-call staging (offsets, header peeks)
+  uint64_t aux_bytes = 0;
   // encode workspace (encode.hip)
   void *enc_ws = nullptr;
   // profiling
@@ -246,6 +250,7 @@ void mib_ctx_free(mib_ctx *c) {
   hipSetDevice(c->device);
   if (c->d_scratch) hipFree(c->d_scratch);
   if (c->d_jobs) hipFree(c->d_jobs);
+  if (c->d_aux) hipFree(c->d_aux);
   if (c->enc_ws) mib_encode_ws_free(c->enc_ws);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -313,13 +318,18 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
   hipSetDevice(c->device);
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   c->times.clear();
-  std::vector<uint8_t> heads(2 * k);
+  std::vector<uint8_t> heads(2 * k + 2);
   std::vector<mib::DecJob> jobs(k);
-  for (size_t i = 0; i < k; i++) {
-    uint64_t n = in_offsets[i + 1] - in_offsets[i];
-    if (n) HIP_OK(hipMemcpyAsync(&heads[2 * i], d_in + in_offsets[i], std::min<uint64_t>(n, 2), hipMemcpyDeviceToHost, st));
+  if (k) {   // window bits of every stream, gathered on the device in one launch
+    int rc = grow((void **)&c->d_aux, &c->aux_bytes, (k + 1) * 8 + 2 * k + 256);
+    if (rc) return rc;
+    uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_aux);
+    uint8_t *d_heads = c->d_aux + ((k + 1) * 8 + 255) / 256 * 256;
+    HIP_OK(hipMemcpyAsync(d_off, in_offsets, (k + 1) * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(mib_decode_peek_heads(d_in, d_off, (int)k, d_heads, st));
+    HIP_OK(hipMemcpyAsync(heads.data(), d_heads, 2 * k, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
   }
-  HIP_OK(hipStreamSynchronize(st));
   for (size_t i = 0; i < k; i++) {
     mib::DecJob &j = jobs[i];
     memset(&j, 0, sizeof(j));
