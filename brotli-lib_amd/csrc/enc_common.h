@@ -1,0 +1,227 @@
+// brotli_amd encoder: definitions shared by the encoder's kernel files (enc_*.hip) and
+// the host orchestration (encode.hip).  See encode.hip for the pipeline overview.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace mib {
+namespace enc {
+
+constexpr uint32_t kSegBits = 16;
+constexpr uint32_t kSeg = 1u << kSegBits;     // 64 KiB parse segments
+constexpr int kMaxMatches = 6;                // staircase entries kept per position
+constexpr int kRing = 512;                    // DP node window (> kLongCopy + 64)
+constexpr int kLongCopy = 325;                // MAX_ZOPFLI_LEN_QUALITY_11 (enc-constants.ts:33)
+constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
+constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
+constexpr int kHdrBytes = 64;                 // metablock header (without trees)
+constexpr int kTreeBytes = 1024;              // one serialised prefix code
+constexpr int kBlock = 256;                   // threads of the per-segment entropy / emit blocks
+
+struct Job {                // one stream (or streaming chunk) to encode
+  const uint8_t *data;      // its bytes (device)
+  uint32_t n;
+  uint32_t pos_base;        // global position index of byte 0 (sort / per-position arrays)
+  uint32_t seg_base;        // first segment
+  uint32_t nseg;
+  uint32_t mb_base;         // first metablock
+  uint32_t nmb;
+  uint32_t lgwin;
+  uint32_t npostfix, ndirect;
+  uint32_t uncompressed;    // 1: quality 0 / n < 64 path; 2: compressed form was larger
+  uint32_t hdr_lgwin;       // window bits written before the first metablock, 0 = none
+  uint32_t final_;          // last chunk of the stream: ISLAST metablock (else a byte-aligning flush)
+  int32_t dc_in[4];         // the decoder's distance ring at the start (streaming continues it)
+  int32_t dc_out[4];        // and after the last command
+  uint64_t out_off;         // byte offset of its scratch output slice
+  uint64_t out_cap;
+  uint64_t total_bits;      // written by offsets / stored
+};
+
+struct Seg {
+  uint32_t job, start, end;   // stream-local [start, end)
+  uint32_t mb;                // metablock (global index)
+  uint32_t cmd_off;           // command slice (capacity (end-start)/2 + 4)
+  uint32_t ncmd;              // backtrack: copy commands
+  uint32_t tail_lits;         // backtrack: literals after the last copy (all of them if none)
+  uint32_t last_dist;         // backtrack: distance of the last copy (0: none)
+  uint32_t carry_in;          // carry: literals owed by earlier segments of the metablock
+  uint32_t prev_dist;         // carry: the decoder's last distance when the segment starts
+  uint32_t extra_ins;         // carry: trailing insert-only command of the metablock (0: none)
+  uint32_t pad;
+  uint64_t bit_off;           // offsets: stream-relative bit position
+  uint64_t bits;              // sizes
+};
+
+struct Mb {                   // one metablock (storeMetaBlockTrivial layout, metablock.ts:290-389)
+  uint32_t job, start, end;   // stream-local
+  uint32_t first_seg, nseg;
+  uint32_t is_last;
+  uint32_t hdr_bits;          // header bits before the prefix codes
+  uint32_t tree_bits[3];      // literal, command, distance code
+  uint32_t pad;
+  uint64_t bit_off;           // of the header, stream-relative
+};
+
+struct Cmd {                  // one command with its prefix codes (command.ts:29-208)
+  uint32_t ins, copy;         // copy == 0: trailing insert-only command
+  uint32_t dist;              // its distance (for the distance ring)
+  uint32_t dist_extra;
+  uint16_t cmd_prefix, dist_prefix;   // dist_prefix: code | nbits << 10, code 0 = last distance
+};
+
+struct RawCmd { uint32_t ins, len, dist; };
+
+struct Codes {   // per metablock Huffman codes
+  uint8_t ld[256];
+  uint16_t lc[256];
+  uint8_t cd[704];
+  uint16_t cc[704];
+  uint8_t dd[128];
+  uint16_t dcd[128];
+};
+
+// ---------------------------------------------------------------- coding helpers (command.ts)
+__device__ __forceinline__ int log2floor_u(uint32_t v) { return 31 - __clz(v); }
+// (each kernel file gets its own copy: device code is not linked across files)
+static __device__ __constant__ uint32_t kInsBase[24] = {0,   1,   2,   3,   4,   5,    6,    8,    10,   14,   18,   26,
+                                                        34,  50,  66,  98,  130, 194,  322,  578,  1090, 2114, 6210, 22594};
+static __device__ __constant__ uint32_t kInsExtra[24] = {0, 0, 0, 0, 0, 0, 1, 1,  2,  2,  3,  3,
+                                                         4, 4, 5, 5, 6, 7, 8, 9, 10, 12, 14, 24};
+static __device__ __constant__ uint32_t kCopyBase[24] = {2,  3,  4,  5,  6,   7,   8,   9,   10,  12,   14,   18,
+                                                         22, 30, 38, 54, 70, 102, 134, 198, 326, 582, 1094, 2118};
+static __device__ __constant__ uint32_t kCopyExtra[24] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1,  2,  2,
+                                                          3, 3, 4, 4, 5, 5, 6, 7, 8, 9, 10, 24};
+
+__device__ __forceinline__ int ins_code(uint32_t n) {
+  if (n < 6) return (int)n;
+  if (n < 130) {
+    int nb = log2floor_u(n - 2) - 1;
+    return (nb << 1) + (int)((n - 2) >> nb) + 2;
+  }
+  if (n < 2114) return log2floor_u(n - 66) + 10;
+  if (n < 6210) return 21;
+  if (n < 22594) return 22;
+  return 23;
+}
+__device__ __forceinline__ int copy_code(uint32_t n) {
+  if (n < 10) return (int)n - 2;
+  if (n < 134) {
+    int nb = log2floor_u(n - 6) - 1;
+    return (nb << 1) + (int)((n - 6) >> nb) + 4;
+  }
+  if (n < 2118) return log2floor_u(n - 70) + 12;
+  return 23;
+}
+__device__ __forceinline__ int combine_codes(int ic, int cc, bool use_last) {
+  int bits64 = (cc & 7) | ((ic & 7) << 3);
+  if (use_last && ic < 8 && cc < 16) return cc < 8 ? bits64 : (bits64 | 64);
+  int off = 2 * ((cc >> 3) + 3 * (ic >> 3));
+  off = (off << 5) + 0x40 + ((0x520D40 >> off) & 0xC0);
+  return off | bits64;
+}
+// prefixEncodeCopyDistance (command.ts:111-135): code | nbits << 10, extra
+__device__ __forceinline__ uint32_t dist_prefix(uint32_t dcode, int ndirect, int npostfix, uint32_t *extra) {
+  if (dcode < (uint32_t)(16 + ndirect)) {
+    *extra = 0;
+    return dcode;
+  }
+  uint32_t dist = (1u << (npostfix + 2)) + (dcode - 16 - (uint32_t)ndirect);
+  int bucket = log2floor_u(dist) - 1;
+  uint32_t pmask = (1u << npostfix) - 1, postfix = dist & pmask, prefix = (dist >> bucket) & 1;
+  uint32_t offset = (2 + prefix) << bucket;
+  uint32_t nbits = (uint32_t)(bucket - npostfix);
+  *extra = (dist - offset) >> npostfix;
+  return (nbits << 10) | (16 + (uint32_t)ndirect + ((2 * (nbits - 1) + prefix) << npostfix) + postfix);
+}
+
+__device__ __forceinline__ uint32_t load_u32(const uint8_t *p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint32_t hash4(const uint8_t *p) { return (load_u32(p) * 0x1E35A7BDu) >> 15; }
+
+// length of the common prefix of a[] and b[], up to limit
+__device__ __forceinline__ uint32_t match_len(const uint8_t *a, const uint8_t *b, uint32_t limit) {
+  uint32_t m = 0;
+  while (m + 4 <= limit) {
+    uint32_t x = load_u32(a + m) ^ load_u32(b + m);
+    if (x) return m + (__ffs(x) - 1) / 8;
+    m += 4;
+  }
+  while (m < limit && a[m] == b[m]) m++;
+  return m;
+}
+
+// A block that is a single wave: LDS traffic of a wave is processed in order, so a compiler
+// fence at wavefront scope is all the lanes need between dependent LDS steps (a
+// workgroup barrier would also drain the outstanding global stores/loads every time).
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Serial LSB-first bit writer into a zeroed byte buffer (headers, prefix codes).
+struct BitW {
+  uint8_t *buf;
+  uint64_t pos;
+  __device__ void put(int nbits, uint64_t v) {
+    while (nbits > 0) {
+      int k = nbits < 32 ? nbits : 32;
+      uint64_t vv = v & ((1ull << k) - 1);
+      uint64_t word = vv << (pos & 7);
+      uint8_t *b = buf + (pos >> 3);
+      int nb = (int)(((pos & 7) + k + 7) >> 3);
+      for (int i = 0; i < nb; i++) b[i] |= (uint8_t)(word >> (8 * i));
+      pos += k;
+      v >>= k;
+      nbits -= k;
+    }
+  }
+};
+
+// encodeWindowBits (bit-writer.ts:172-194)
+__device__ __forceinline__ void put_window_bits(BitW &w, int lg) {
+  if (lg == 16) w.put(1, 0);
+  else if (lg == 17) w.put(7, 1);
+  else if (lg > 17) w.put(4, (uint32_t)(((lg - 17) << 1) | 1));
+  else w.put(7, (uint32_t)(((lg - 8) << 4) | 1));
+}
+
+// Bits of one command: prefix code, extra bits, literals, distance (storeCommandExtra /
+// BlockEncoder, metablock.ts:273-287,392-501).
+__device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Cmd &c, const uint8_t *lits) {
+  const int ic = ins_code(c.ins);
+  const int cc = copy_code(c.copy ? c.copy : 2);
+  uint32_t bits = cd.cd[c.cmd_prefix] + kInsExtra[ic] + kCopyExtra[cc];
+  for (uint32_t k = 0; k < c.ins; k++) bits += cd.ld[lits[k]];
+  if (c.copy && c.cmd_prefix >= 128) bits += cd.dd[c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
+  return bits;
+}
+
+// ---------------------------------------------------------------- kernel launchers (host)
+void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys,
+                      uint32_t *vals);
+void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
+                         int depth, uint64_t *matches, uint8_t *nmatch);
+void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
+void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
+               const uint64_t *matches, const uint8_t *nmatch, uint64_t *choice);
+void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
+void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
+void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const RawCmd *raw, Cmd *cmds,
+                  uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd);
+void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds);
+void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
+                    const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr);
+void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Cmd *cmds, const uint32_t *cmd_pos,
+                  const Codes *codes);
+void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out);
+void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
+                 const uint32_t *cmd_pos, const Codes *codes, const uint8_t *trees, const uint8_t *hdr, uint8_t *out);
+void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out);
+void launch_pack(hipStream_t st, const Job *jobs, int njobs, const uint64_t *dst_off, const uint8_t *src, uint8_t *dst);
+
+}  // namespace enc
+}  // namespace mib

@@ -1,0 +1,572 @@
+// Entropy coding: commands -> prefix codes, per-metablock
+// histograms, length-limited Huffman codes and their serialisation, bit sizes / offsets.
+//
+// Every stage here is parallel over segments (a block each) or over (metablock, alphabet);
+// the only per-stream serial steps (carry, offsets, dist_ring) touch O(segments) values.
+#include <hipcub/hipcub.hpp>
+
+#include "enc_common.h"
+
+namespace mib {
+namespace enc {
+
+// ---------------------------------------------------------------- carry: lane per stream
+// Literals left after a segment's last copy belong to the next command, which may be in a
+// later segment; a metablock's final literals form an insert-only command (createInsertCommand
+// path of encode.ts:240-262).  Also the decoder's last distance at each segment start: the
+// distance ring's slot 0 always holds the previous copy's distance (a code-0 command does not
+// push, but reuses exactly that distance), so code 0 is decidable per segment in parallel.
+__global__ void carry_kernel(Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  Job &jb = jobs[j];
+  if (jb.uncompressed) return;
+  uint32_t pd = (uint32_t)jb.dc_in[0];
+  for (uint32_t m = 0; m < jb.nmb; m++) {
+    const Mb &mb = mbs[jb.mb_base + m];
+    uint32_t carry = 0;
+    for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
+      Seg &sg = segs[s];
+      sg.carry_in = carry;
+      sg.prev_dist = pd;
+      sg.extra_ins = 0;
+      if (sg.ncmd) {
+        carry = sg.tail_lits;
+        pd = sg.last_dist;
+      } else {
+        carry += sg.tail_lits;
+      }
+    }
+    if (carry) segs[mb.first_seg + mb.nseg - 1].extra_ins = carry;
+  }
+}
+
+// ---------------------------------------------------------------- codes + histograms
+// Block per segment: command prefix codes (getInsertLengthCode / getCopyLengthCode /
+// combineLengthCodes / prefixEncodeCopyDistance, command.ts:29-179), command positions
+// (block scan), and the metablock's literal / command / distance histograms (LDS, then one
+// global atomic per non-zero bin).
+__global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Seg *segs, const RawCmd *raw, Cmd *cmds,
+                                                       uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
+  typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
+  __shared__ typename Scan::TempStorage scan_tmp;
+  __shared__ uint32_t sh_l[256], sh_c[704], sh_d[128];
+  __shared__ uint32_t sh_run;
+  const Seg sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  if (jb.uncompressed) return;
+  const int t = threadIdx.x;
+  for (int i = t; i < 704; i += kBlock) sh_c[i] = 0;
+  for (int i = t; i < 256; i += kBlock) sh_l[i] = 0;
+  if (t < 128) sh_d[t] = 0;
+  if (t == 0) sh_run = sg.start - sg.carry_in;
+  __syncthreads();
+  const RawCmd *r = raw + sg.cmd_off;
+  Cmd *out = cmds + sg.cmd_off;
+  uint32_t *outp = cmd_pos + sg.cmd_off;
+  const uint32_t nraw = sg.ncmd, n = nraw + (sg.extra_ins ? 1 : 0);
+  for (uint32_t base = 0; base < n; base += kBlock) {
+    const uint32_t q = base + t;
+    uint32_t ins = 0, len = 0, d = 0, prevd = 0;
+    if (q < nraw) {
+      const RawCmd rc = r[q];
+      ins = rc.ins + (q == 0 ? sg.carry_in : 0);
+      len = rc.len;
+      d = rc.dist;
+      prevd = q ? r[q - 1].dist : sg.prev_dist;
+    } else if (q < n) {
+      ins = sg.extra_ins;
+    }
+    uint32_t off, total;
+    Scan(scan_tmp).ExclusiveSum(ins + len, off, total);
+    const uint32_t pos = sh_run + off;
+    __syncthreads();
+    if (t == 0) sh_run += total;
+    if (q < n) {
+      Cmd c;
+      c.ins = ins;
+      c.copy = len;
+      c.dist = d;
+      c.dist_extra = 0;
+      c.dist_prefix = 0;
+      const int ic = ins_code(ins);
+      if (len) {
+        const uint32_t dcode = d == prevd ? 0 : d + 15;
+        uint32_t extra;
+        const uint32_t dp = dist_prefix(dcode, (int)jb.ndirect, (int)jb.npostfix, &extra);
+        c.dist_extra = extra;
+        c.dist_prefix = (uint16_t)dp;
+        c.cmd_prefix = (uint16_t)combine_codes(ic, copy_code(len), dcode == 0);
+        if (c.cmd_prefix >= 128) atomicAdd(&sh_d[dp & 0x3FF], 1u);
+      } else {   // insert-only: copy code 0 with the implicit last distance when possible
+        c.cmd_prefix = (uint16_t)combine_codes(ic, 0, ic < 8);
+      }
+      atomicAdd(&sh_c[c.cmd_prefix], 1u);
+      out[q] = c;
+      outp[q] = pos;
+      for (uint32_t k = 0; k < ins; k++) atomicAdd(&sh_l[jb.data[pos + k]], 1u);
+    }
+    __syncthreads();
+  }
+  const uint32_t m = sg.mb;
+  for (int i = t; i < 704; i += kBlock)
+    if (sh_c[i]) atomicAdd(&hc[m * 704 + i], sh_c[i]);
+  for (int i = t; i < 256; i += kBlock)
+    if (sh_l[i]) atomicAdd(&hl[m * 256 + i], sh_l[i]);
+  if (t < 128 && sh_d[t]) atomicAdd(&hd[m * 128 + t], sh_d[t]);
+}
+
+// ---------------------------------------------------------------- distance ring after a chunk
+// (streaming: the next chunk's code-0 decisions start from it) lane per stream, backwards
+// over the last commands: every explicit distance was pushed.
+__global__ void dist_ring_kernel(Job *jobs, int njobs, const Seg *segs, const Cmd *cmds) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  Job &jb = jobs[j];
+  if (jb.uncompressed) return;
+  int32_t ring[4];
+  int got = 0;
+  for (int s = (int)(jb.seg_base + jb.nseg) - 1; s >= (int)jb.seg_base && got < 4; s--) {
+    const Seg &sg = segs[s];
+    const Cmd *c = cmds + sg.cmd_off;
+    for (int q = (int)sg.ncmd - 1; q >= 0 && got < 4; q--)
+      if ((c[q].dist_prefix & 0x3FF) != 0) ring[got++] = (int32_t)c[q].dist;
+  }
+  for (int q = 0; q < 4; q++) jb.dc_out[q] = q < got ? ring[q] : jb.dc_in[q - got];
+}
+
+// ---------------------------------------------------------------- Huffman codes
+// Block (one wave) per (metablock, alphabet).  createHuffmanTree (entropy-encode.ts:24-131):
+// leaves sorted by (count ascending, symbol descending) -- ranks computed by the 64 lanes --
+// two-queue merge and depth walk by lane 0, count-limit doubling until depth <= 15;
+// convertBitDepthsToSymbols (:234-258); buildAndStoreHuffmanTree simple / complex forms
+// (context-map.ts:215-347).
+__device__ void tree_depths(const uint32_t *h, const int16_t *sorted, int n, uint32_t lc, int limit, uint8_t *depth,
+                            uint32_t *cnt, int16_t *left, int16_t *val, bool *ok) {
+  for (int k = 0; k < n; k++) {
+    uint32_t c = h[sorted[k]];
+    cnt[k] = c > lc ? c : lc;
+    left[k] = -1;
+    val[k] = sorted[k];
+  }
+  cnt[n] = cnt[n + 1] = 0xFFFFFFFFu;
+  left[n] = left[n + 1] = -1;
+  val[n] = val[n + 1] = -1;
+  int i = 0, j = n + 1;
+  for (int k = n - 1; k > 0; k--) {
+    int l, r;
+    if (cnt[i] <= cnt[j]) l = i++; else l = j++;
+    if (cnt[i] <= cnt[j]) r = i++; else r = j++;
+    const int je = 2 * n - k;
+    cnt[je] = cnt[l] + cnt[r];
+    left[je] = (int16_t)l;
+    val[je] = (int16_t)r;
+    cnt[je + 1] = 0xFFFFFFFFu;
+    left[je + 1] = -1;
+    val[je + 1] = -1;
+  }
+  int16_t stack[18];
+  int level = 0, p = 2 * n - 1;
+  stack[0] = -1;
+  *ok = true;
+  for (;;) {
+    if (left[p] >= 0) {
+      level++;
+      if (level > limit) {
+        *ok = false;
+        return;
+      }
+      stack[level] = val[p];
+      p = left[p];
+      continue;
+    }
+    depth[val[p]] = (uint8_t)level;
+    while (level >= 0 && stack[level] == -1) level--;
+    if (level < 0) return;
+    p = stack[level];
+    stack[level] = -1;
+  }
+}
+
+__device__ void depths_to_codes(const uint8_t *depth, int len, uint16_t *code) {
+  uint32_t bl[16] = {0}, next[16] = {0};
+  for (int i = 0; i < len; i++) bl[depth[i]]++;
+  bl[0] = 0;
+  uint32_t c = 0;
+  for (int i = 1; i <= 15; i++) {
+    c = (c + bl[i - 1]) << 1;
+    next[i] = c;
+  }
+  for (int i = 0; i < len; i++) {
+    code[i] = 0;
+    if (!depth[i]) continue;
+    uint32_t v = next[depth[i]]++, r = 0;
+    for (int b = 0; b < depth[i]; b++) r |= ((v >> b) & 1) << (depth[i] - 1 - b);
+    code[i] = (uint16_t)r;
+  }
+}
+
+// small serial Huffman for the 18 code-length codes (limit 5)
+__device__ void small_depths(const uint32_t *h, int len, int limit, uint8_t *depth) {
+  int16_t sorted[18];
+  uint32_t cnt[40];
+  int16_t left[40], val[40];
+  for (int i = 0; i < len; i++) depth[i] = 0;
+  int n = 0;
+  for (int i = len - 1; i >= 0; i--)
+    if (h[i]) sorted[n++] = (int16_t)i;
+  if (n == 0) return;
+  if (n == 1) {
+    depth[sorted[0]] = 1;
+    return;
+  }
+  for (uint32_t lc = 1;; lc *= 2) {
+    // insertion sort: count ascending, value descending
+    for (int a = 1; a < n; a++) {
+      int16_t v = sorted[a];
+      uint32_t cv = h[v] > lc ? h[v] : lc;
+      int k = a - 1;
+      while (k >= 0) {
+        uint32_t ck = h[sorted[k]] > lc ? h[sorted[k]] : lc;
+        if (ck > cv || (ck == cv && sorted[k] < v)) {
+          sorted[k + 1] = sorted[k];
+          k--;
+        } else {
+          break;
+        }
+      }
+      sorted[k + 1] = v;
+    }
+    bool ok;
+    tree_depths(h, sorted, n, lc, limit, depth, cnt, left, val, &ok);
+    if (ok) return;
+    for (int i = 0; i < len; i++) depth[i] = 0;
+  }
+}
+
+__device__ void put_varlen_u8(BitW &w, int n) {
+  if (n == 0) {
+    w.put(1, 0);
+  } else {
+    int nb = 31 - __clz(n);
+    w.put(1, 1);
+    w.put(3, (uint32_t)nb);
+    w.put(nb, (uint32_t)(n - (1 << nb)));
+  }
+}
+
+// complex prefix code serialisation: run-length code the depths (16 / 17), then a
+// depth-5 code for those (writeHuffmanTree / storeHuffmanTreeOfHuffmanTree)
+__device__ void store_complex(BitW &w, const uint8_t *depth, int asize) {
+  uint8_t rle_code[720];
+  uint8_t rle_extra[720];
+  int nr = 0;
+  int nl = asize;
+  while (nl > 0 && depth[nl - 1] == 0) nl--;
+  int prev = 8;
+  for (int i = 0; i < nl;) {
+    int v = depth[i], reps = 1;
+    while (i + reps < nl && depth[i + reps] == v) reps++;
+    i += reps;
+    if (v == 0) {
+      if (reps == 11) {
+        rle_code[nr] = 0;
+        rle_extra[nr++] = 0;
+        reps--;
+      }
+      if (reps < 3) {
+        for (int q = 0; q < reps; q++) {
+          rle_code[nr] = 0;
+          rle_extra[nr++] = 0;
+        }
+      } else {
+        int s0 = nr;
+        reps -= 3;
+        for (;;) {
+          rle_code[nr] = 17;
+          rle_extra[nr++] = (uint8_t)(reps & 7);
+          reps >>= 3;
+          if (!reps) break;
+          reps--;
+        }
+        for (int x = s0, y = nr - 1; x < y; x++, y--) {
+          uint8_t tt = rle_code[x]; rle_code[x] = rle_code[y]; rle_code[y] = tt;
+          tt = rle_extra[x]; rle_extra[x] = rle_extra[y]; rle_extra[y] = tt;
+        }
+      }
+    } else {
+      if (prev != v) {
+        rle_code[nr] = (uint8_t)v;
+        rle_extra[nr++] = 0;
+        reps--;
+      }
+      if (reps == 7) {
+        rle_code[nr] = (uint8_t)v;
+        rle_extra[nr++] = 0;
+        reps--;
+      }
+      if (reps < 3) {
+        for (int q = 0; q < reps; q++) {
+          rle_code[nr] = (uint8_t)v;
+          rle_extra[nr++] = 0;
+        }
+      } else {
+        int s0 = nr;
+        reps -= 3;
+        for (;;) {
+          rle_code[nr] = 16;
+          rle_extra[nr++] = (uint8_t)(reps & 3);
+          reps >>= 2;
+          if (!reps) break;
+          reps--;
+        }
+        for (int x = s0, y = nr - 1; x < y; x++, y--) {
+          uint8_t tt = rle_code[x]; rle_code[x] = rle_code[y]; rle_code[y] = tt;
+          tt = rle_extra[x]; rle_extra[x] = rle_extra[y]; rle_extra[y] = tt;
+        }
+      }
+      prev = v;
+    }
+  }
+  uint32_t clh[18] = {0};
+  for (int k = 0; k < nr; k++) clh[rle_code[k]]++;
+  int ncodes = 0, first = 0;
+  for (int k = 0; k < 18; k++)
+    if (clh[k]) {
+      if (!ncodes) first = k;
+      ncodes++;
+    }
+  uint8_t cld[18];
+  uint16_t clc[18];
+  small_depths(clh, 18, 5, cld);
+  depths_to_codes(cld, 18, clc);
+  const int order[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+  const uint32_t sym[6] = {0, 7, 3, 2, 1, 15};
+  const int blen[6] = {2, 4, 3, 2, 2, 4};
+  int to_store = 18;
+  if (ncodes > 1)
+    while (to_store > 0 && cld[order[to_store - 1]] == 0) to_store--;
+  int skip = 0;
+  if (cld[order[0]] == 0 && cld[order[1]] == 0) {
+    skip = 2;
+    if (cld[order[2]] == 0) skip = 3;
+  }
+  w.put(2, (uint32_t)skip);
+  for (int k = skip; k < to_store; k++) {
+    int l = cld[order[k]];
+    w.put(blen[l], sym[l]);
+  }
+  if (ncodes == 1) cld[first] = 0;
+  for (int k = 0; k < nr; k++) {
+    int c = rle_code[k];
+    w.put(cld[c], clc[c]);
+    if (c == 16) w.put(2, rle_extra[k]);
+    else if (c == 17) w.put(3, rle_extra[k]);
+  }
+}
+
+__global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
+                                                     const uint32_t *hc, const uint32_t *hd, Codes *codes,
+                                                     uint8_t *trees, uint8_t *hdr) {
+  __shared__ uint32_t h[704];
+  __shared__ int16_t nzs[704];
+  __shared__ int16_t sorted[704];
+  __shared__ uint32_t cnt[2 * 704 + 2];
+  __shared__ int16_t left[2 * 704 + 2], val[2 * 704 + 2];
+  __shared__ uint8_t depth[704];
+  __shared__ uint16_t code[704];
+  __shared__ uint8_t buf[kTreeBytes];
+  __shared__ int sh_ok;
+  const int m = blockIdx.x / 3, t = blockIdx.x % 3;
+  const int lane = threadIdx.x;
+  Mb &mb = mbs[m];
+  const Job &jb = jobs[mb.job];
+  if (jb.uncompressed) return;
+  const int asize = t == 0 ? 256 : t == 1 ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
+  const uint32_t *src = t == 0 ? hl + m * 256 : t == 1 ? hc + m * 704 : hd + m * 128;
+  for (int i = lane; i < asize; i += 64) {
+    h[i] = src[i];
+    depth[i] = 0;
+    code[i] = 0;
+  }
+  for (int i = lane; i < kTreeBytes; i += 64) buf[i] = 0;
+  wave_sync();
+  // compact the used symbols (ascending)
+  int n = 0;
+  for (int c0 = 0; c0 < asize; c0 += 64) {
+    const int i = c0 + lane;
+    const bool f = i < asize && h[i] != 0;
+    const uint64_t mask = __ballot(f);
+    if (f) nzs[n + __popcll(mask & ((1ull << lane) - 1))] = (int16_t)i;
+    n += __popcll(mask);
+  }
+  wave_sync();
+  int max_bits = 0;
+  for (int c = asize - 1; c; c >>= 1) max_bits++;
+  if (n > 1) {
+    for (uint32_t lc = 1;; lc *= 2) {
+      for (int a = lane; a < n; a += 64) {
+        const int si = nzs[a];
+        const uint32_t ci = h[si] > lc ? h[si] : lc;
+        int r = 0;
+        for (int b = 0; b < n; b++) {
+          const int sj = nzs[b];
+          const uint32_t cj = h[sj] > lc ? h[sj] : lc;
+          r += (cj < ci || (cj == ci && sj > si)) ? 1 : 0;
+        }
+        sorted[r] = (int16_t)si;
+      }
+      wave_sync();
+      if (lane == 0) {
+        bool ok;
+        tree_depths(h, sorted, n, lc, 15, depth, cnt, left, val, &ok);
+        if (!ok)
+          for (int i = 0; i < asize; i++) depth[i] = 0;
+        sh_ok = ok ? 1 : 0;
+      }
+      wave_sync();
+      if (sh_ok) break;
+    }
+  }
+  if (lane == 0) {
+    BitW w{buf, 0};
+    if (n <= 1) {   // one symbol (or none): simple code, zero-length codeword
+      w.put(4, 1);
+      w.put(max_bits, n ? (uint32_t)nzs[0] : 0u);
+      if (n) depth[nzs[0]] = 0;
+    } else {
+      depths_to_codes(depth, asize, code);
+      if (n <= 4) {
+        int s4[4];
+        for (int i = 0; i < n; i++) s4[i] = nzs[i];
+        for (int i = 1; i < n; i++) {
+          int v = s4[i], k = i;
+          while (k > 0 && depth[s4[k - 1]] > depth[v]) {
+            s4[k] = s4[k - 1];
+            k--;
+          }
+          s4[k] = v;
+        }
+        w.put(2, 1);
+        w.put(2, (uint32_t)(n - 1));
+        for (int i = 0; i < n; i++) w.put(max_bits, (uint32_t)s4[i]);
+        if (n == 4) w.put(1, depth[s4[0]] == 1 ? 1 : 0);
+      } else {
+        store_complex(w, depth, asize);
+      }
+    }
+    mb.tree_bits[t] = (uint32_t)w.pos;
+  }
+  wave_sync();
+  uint8_t *dst = trees + ((size_t)m * 3 + t) * kTreeBytes;
+  for (int i = lane; i < kTreeBytes; i += 64) dst[i] = buf[i];
+  Codes &cd = codes[m];
+  uint8_t *dd = t == 0 ? cd.ld : t == 1 ? cd.cd : cd.dd;
+  uint16_t *cc = t == 0 ? cd.lc : t == 1 ? cd.cc : cd.dcd;
+  for (int i = lane; i < asize; i += 64) {
+    dd[i] = depth[i];
+    cc[i] = code[i];
+  }
+  // the metablock header before the codes (storeMetaBlockTrivial, metablock.ts:290-356)
+  if (t == 0 && lane == 0) {
+    uint8_t *hb = hdr + (size_t)m * kHdrBytes;
+    for (int i = 0; i < kHdrBytes; i++) hb[i] = 0;
+    BitW w{hb, 0};
+    if (mb.start == 0 && jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
+    const uint32_t length = mb.end - mb.start;
+    w.put(1, mb.is_last);
+    if (mb.is_last) w.put(1, 0);
+    const int lg = length == 1 ? 1 : 32 - __clz(length - 1);
+    const int mn = (lg < 16 ? 16 : lg + 3) / 4;
+    w.put(2, (uint32_t)(mn - 4));
+    w.put(mn * 4, length - 1);
+    if (!mb.is_last) w.put(1, 0);
+    put_varlen_u8(w, 0);   // NBLTYPESL - 1
+    put_varlen_u8(w, 0);   // NBLTYPESI - 1
+    put_varlen_u8(w, 0);   // NBLTYPESD - 1
+    w.put(2, jb.npostfix);
+    w.put(4, jb.ndirect >> jb.npostfix);
+    w.put(2, 0);           // literal context mode (one tree: contexts unused)
+    put_varlen_u8(w, 0);   // NTREESL - 1
+    put_varlen_u8(w, 0);   // NTREESD - 1
+    mb.hdr_bits = (uint32_t)w.pos;
+  }
+}
+
+// ---------------------------------------------------------------- sizes: block per segment
+__global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *segs, const Cmd *cmds, const uint32_t *cmd_pos,
+                                                       const Codes *codes) {
+  typedef hipcub::BlockReduce<unsigned long long, kBlock> Reduce;
+  __shared__ typename Reduce::TempStorage tmp;
+  Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  if (jb.uncompressed) return;
+  const Codes &cd = codes[sg.mb];
+  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  unsigned long long bits = 0;
+  for (uint32_t q = threadIdx.x; q < n; q += kBlock)
+    bits += command_bits(cd, cmds[sg.cmd_off + q], jb.data + cmd_pos[sg.cmd_off + q]);
+  unsigned long long total = Reduce(tmp).Sum(bits);
+  if (threadIdx.x == 0) sg.bits = total;
+}
+
+// ---------------------------------------------------------------- offsets: lane per stream
+__global__ void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  Job &jb = jobs[j];
+  if (jb.uncompressed) return;
+  uint64_t pos = 0;
+  for (uint32_t m = 0; m < jb.nmb; m++) {
+    Mb &mb = mbs[jb.mb_base + m];
+    mb.bit_off = pos;
+    pos += (uint64_t)mb.hdr_bits + mb.tree_bits[0] + mb.tree_bits[1] + mb.tree_bits[2];
+    for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
+      segs[s].bit_off = pos;
+      pos += segs[s].bits;
+    }
+    if (mb.is_last) pos = (pos + 7) & ~7ull;
+  }
+  const uint64_t trailer = pos;
+  if (!jb.final_) pos = (pos + 6 + 7) & ~7ull;   // empty metadata block: ISLAST 0, MNIBBLES 0, MSKIPBYTES 0
+  // the stored form is never larger than n + 5 bytes per 16 MiB block + window header + tail
+  const uint64_t stored_bits = 8ull * ((uint64_t)jb.n + 5ull * ((jb.n >> 24) + 1) + 4);
+  if (pos > stored_bits || (pos >> 3) + 8 > jb.out_cap) {
+    jb.uncompressed = 2;   // emit stored metablocks instead
+    for (int q = 0; q < 4; q++) jb.dc_out[q] = jb.dc_in[q];
+    return;
+  }
+  if (!jb.final_) {   // bits 0,1,1,0,0,0 = 6
+    uint32_t *w = reinterpret_cast<uint32_t *>(out + jb.out_off);
+    const uint64_t v = 6ull << (trailer & 31);
+    atomicOr(w + (trailer >> 5), (uint32_t)v);
+    if ((uint32_t)(v >> 32)) atomicOr(w + (trailer >> 5) + 1, (uint32_t)(v >> 32));
+  }
+  jb.total_bits = pos;
+}
+
+// ---------------------------------------------------------------- launchers
+void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
+  hipLaunchKernelGGL(carry_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, mbs);
+}
+void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const RawCmd *raw, Cmd *cmds,
+                  uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
+  hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, raw, cmds, cmd_pos, hl, hc, hd);
+}
+void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds) {
+  hipLaunchKernelGGL(dist_ring_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, cmds);
+}
+void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
+                    const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
+  hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * 3), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, hdr);
+}
+void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Cmd *cmds, const uint32_t *cmd_pos,
+                  const Codes *codes) {
+  hipLaunchKernelGGL(sizes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, cmds, cmd_pos, codes);
+}
+void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
+  hipLaunchKernelGGL(offsets_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, out);
+}
+
+}  // namespace enc
+}  // namespace mib
