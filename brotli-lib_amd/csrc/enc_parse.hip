@@ -5,21 +5,26 @@
 namespace mib {
 namespace enc {
 
-// ---------------------------------------------------------------- 3. DP parse, wave per segment
+// ---------------------------------------------------------------- 3. DP parse
 // Shortest path over positions (updateNodes / computeShortestPathFromNodes,
 // backward-references-hq.ts:267-406): node i holds the cheapest cost of reaching i, the
-// insert length since the last copy, and the path's last distance.  Edges: one literal;
-// the staircase matches of i (lanes relax consecutive lengths in parallel); a copy at the
-// path's last distance (short code 0).  A match longer than kLongCopy is taken outright and
-// the parse jumps to its end, as the reference does (:518-533).
+// insert length since the last copy, and the path's last distance.  Edges out of i: one
+// literal; the staircase matches of i (the shortest distance covering each length); a copy
+// at the path's last distance (short code 0).  A copy longer than kLongCopy is taken
+// outright and the parse jumps to its end, as the reference does (:518-533).
 //
-// Everything a position needs that does not depend on the DP state (its matches, its
-// literal byte, the bytes ahead) is staged into LDS 64 positions at a time with coalesced
-// loads; the only load left inside the serial loop is the 64-byte window at the path's
-// last distance, issued before the relaxations that hide it.
-constexpr int kBatch = 64;
+// One wave runs kG = 4 segments side by side, 16 lanes each: per step every group advances
+// its own segment by one position, its 16 lanes relaxing 16 copy lengths at a time, so the
+// per-position bookkeeping is paid once per 4 positions.  Everything a position needs that
+// does not depend on the parse state (its matches with their distance costs, its literal
+// cost) is staged into LDS 16 positions at a time; the last-distance run is measured
+// 16 bytes per probe and cached while the path keeps that distance.
+constexpr int kG = 4;          // segments per wave
+constexpr int kGL = 16;        // lanes per segment
+constexpr int kBatch = 16;     // positions staged per refill
+constexpr uint32_t kRingMask = kRing - 1;
 constexpr float kInf = 3.0e38f;
-constexpr int kChunks = (kLongCopy + 64) / 64;   // length chunks of 64 lanes covering 0..kLongCopy
+static_assert(kLongCopy + kBatch < kRing, "a batch's nodes must survive until they are flushed");
 
 // node meta: last distance (32) | copy length that reached it (16, 0 = literal) | insert length (16)
 __device__ __forceinline__ uint64_t pack_node(uint32_t ld, uint32_t clen, uint32_t ins) {
@@ -29,239 +34,241 @@ __device__ __forceinline__ uint64_t node_choice(uint64_t m) {   // (distance << 
   uint32_t cl = (uint32_t)(m >> 32) & 0xFFFF;
   return cl ? (((uint64_t)(uint32_t)m << 32) | cl) : 0ull;
 }
+__device__ __forceinline__ uint32_t group_bits(uint64_t ballot, int g) { return (uint32_t)(ballot >> (kGL * g)) & 0xFFFFu; }
 
-__global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, const uint32_t *lit_histo,
+__global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_histo,
                                                 const uint64_t *matches, const uint8_t *nmatch,
                                                 uint64_t *choice /* per position+1 */) {
-  __shared__ float cost[kRing];
-  __shared__ uint64_t meta[kRing];
+  __shared__ float cost[kG][kRing];
+  __shared__ uint64_t meta[kG][kRing];
+  __shared__ float litc[kG][256];
   __shared__ float cmdc[704];
   __shared__ float distc[128];
-  __shared__ float litc[256];
-  __shared__ float blit[kBatch];                   // literal cost of each batch position
-  __shared__ uint8_t bnm[kBatch];
-  __shared__ uint64_t bmt[kBatch * kMaxMatches];   // (distance << 32) | length
-  __shared__ float bmc[kBatch * kMaxMatches];      // distance symbol cost + extra bits
-  const int lane = threadIdx.x;
-  const Seg sg = segs[blockIdx.x];
+  __shared__ float blit[kG][kBatch];
+  __shared__ uint8_t bnm[kG][kBatch];
+  __shared__ uint64_t bmt[kG][kBatch * kMaxMatches];   // (distance << 32) | length
+  __shared__ float bmc[kG][kBatch * kMaxMatches];      // distance symbol cost + extra bits
+  const int lane = threadIdx.x, g = lane / kGL, sl = lane % kGL;
+  const int s = blockIdx.x * kG + g;
+  const bool valid = s < nsegs;
+  const Seg sg = segs[valid ? s : 0];
   const Job &jb = jobs[sg.job];
   const uint8_t *data = jb.data;
-  // cost model: literals from the stream's order-0 histogram (zopfli-cost-model.ts:163-189),
-  // commands / distances from the reference's first-iteration heuristic (:54-64).
+  const uint32_t a = sg.start, b = sg.end, gbase = jb.pos_base;
+  for (int i = lane; i < 704; i += 64) cmdc[i] = log2f(11.f + i);
+  for (int i = lane; i < 128; i += 64) distc[i] = log2f(20.f + i);
+  // literal costs from the stream's order-0 histogram (zopfli-cost-model.ts:163-189)
   {
-    uint32_t total = 0;
-    for (int i = 0; i < 256; i++) total += lit_histo[sg.job * 256 + i];
-    float lt = log2f((float)max(total, 1u));
-    for (int i = lane; i < 256; i += 64) {
-      uint32_t c = lit_histo[sg.job * 256 + i];
-      float v = c ? lt - log2f((float)c) : lt + 2.f;
-      litc[i] = v < 1.f ? 1.f : v;
+    uint32_t part = 0;
+    for (int i = sl; i < 256; i += kGL) part += lit_histo[sg.job * 256 + i];
+    for (int o = kGL / 2; o; o >>= 1) part += __shfl_xor(part, o, kGL);
+    const float lt = log2f((float)max(part, 1u));
+    for (int i = sl; i < 256; i += kGL) {
+      const uint32_t c = lit_histo[sg.job * 256 + i];
+      const float v = c ? lt - log2f((float)c) : lt + 2.f;
+      litc[g][i] = v < 1.f ? 1.f : v;
     }
-    for (int i = lane; i < 704; i += 64) cmdc[i] = log2f(11.f + i);
-    for (int i = lane; i < 128; i += 64) distc[i] = log2f(20.f + i);
   }
-  for (int i = lane; i < kRing; i += 64) {
-    cost[i] = kInf;
-    meta[i] = 0;
+  for (int i = sl; i < kRing; i += kGL) {
+    cost[g][i] = kInf;
+    meta[g][i] = 0;
   }
-  // copy code / extra bits of the lengths this lane relaxes (l = 64 k + lane)
-  int ccl[kChunks];
-  float cxl[kChunks];
-#pragma unroll
-  for (int k = 0; k < kChunks; k++) {
-    uint32_t l = max(2u, (uint32_t)(64 * k + lane));
-    ccl[k] = copy_code(l);
-    cxl[k] = (float)kCopyExtra[ccl[k]];
-  }
-  // command cost per lane length for the current insert code: explicit distance / last distance
-  float cm[kChunks], cml[kChunks];
-  int cached_ic = -1;
   wave_sync();
-  const uint32_t a = sg.start, b = sg.end;
-  const uint32_t gbase = jb.pos_base;
-  if (lane == 0) cost[a % kRing] = 0.f;
+  if (sl == 0) cost[g][a & kRingMask] = 0.f;
+  // command cost of this lane's lengths in chunks 0 and 1 for the current insert code
+  const uint32_t l0c = max(2u, (uint32_t)sl), l1c = kGL + sl;
+  const int cc0 = copy_code(l0c), cc1 = copy_code(l1c);
+  float cm0 = 0.f, cm1 = 0.f, cml0 = 0.f, cml1 = 0.f;
+  int cached_ic = -1;
   // the path's last distance: verified run [c_from, c_upto) of data[p] == data[p - c_ld]
   uint32_t c_ld = 0, c_from = 0, c_upto = 0;
-  bool c_end = false;   // c_upto is a mismatch (or the segment end), not just "verified so far"
-  uint32_t i = a;
-  while (i < b) {
-    // ---- stage the next batch: matches and their distance costs, literal costs
-    const uint32_t i0 = i;
-    const uint32_t nb = min((uint32_t)kBatch, b - i0);
-    wave_sync();
-    {
-      int nm = 0;
-      if ((uint32_t)lane < nb) {
-        nm = nmatch[gbase + i0 + lane];
-        blit[lane] = litc[data[i0 + lane]];
-      }
-      bnm[lane] = (uint8_t)nm;
-      const uint64_t *src = matches + (uint64_t)(gbase + i0 + lane) * kMaxMatches;
-      for (int q = 0; q < nm; q++) {
-        uint64_t m = src[q];
-        uint32_t extra;
-        uint32_t dp = dist_prefix((uint32_t)(m >> 32) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
-        bmt[lane * kMaxMatches + q] = m;
-        bmc[lane * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
+  bool c_end = false;
+  bool active = valid && a < b;
+  uint32_t i = a, i0 = a, nb = 0;
+  bool flushed = true;   // the current batch's choices are already stored
+  wave_sync();
+  for (;;) {
+    // ---- per group: finish a batch (store its choices), finish the segment, or stage
+    if (active && i >= i0 + nb) {
+      if (!flushed && (uint32_t)sl < nb && i0 + sl != a) choice[gbase + i0 + sl] = node_choice(meta[g][(i0 + sl) & kRingMask]);
+      if (i >= b) {
+        if (sl == 0) choice[gbase + b] = node_choice(meta[g][b & kRingMask]);
+        active = false;
+      } else {
+        i0 = i;
+        nb = min((uint32_t)kBatch, b - i0);
+        flushed = false;
+        int nm = 0;
+        if ((uint32_t)sl < nb) {
+          nm = nmatch[gbase + i0 + sl];
+          blit[g][sl] = litc[g][data[i0 + sl]];
+        }
+        bnm[g][sl] = (uint8_t)nm;
+        const uint64_t *src = matches + (uint64_t)(gbase + i0 + sl) * kMaxMatches;
+        for (int q = 0; q < nm; q++) {
+          const uint64_t m = src[q];
+          uint32_t extra;
+          const uint32_t dp = dist_prefix((uint32_t)(m >> 32) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
+          bmt[g][sl * kMaxMatches + q] = m;
+          bmc[g][sl * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
+        }
       }
     }
     wave_sync();
-    bool forced = false;
-    while (i < i0 + nb) {
-      const int slot = i % kRing;
-      const float ci = cost[slot];
-      const uint64_t mi = meta[slot];
-      const uint32_t ld = (uint32_t)mi, ins_i = (uint32_t)(mi >> 48);
-      const uint32_t off = i - i0;
-      const uint32_t limit = b - i;
-      const float litcost = blit[off];
-      // the staircase of (distance, length), clipped at the segment end
-      const int nm = bnm[off];
-      uint32_t md[kMaxMatches], mL[kMaxMatches];
-      float mc[kMaxMatches];
+    if (!__ballot(active)) break;
+    if (!active) continue;
+    // ---- one position per group
+    const uint32_t slot = i & kRingMask;
+    const float ci = cost[g][slot];
+    const uint64_t mi = meta[g][slot];
+    const uint32_t ld = (uint32_t)mi, ins_i = (uint32_t)(mi >> 48);
+    const uint32_t off = i - i0, limit = b - i;
+    const float litcost = blit[g][off];
+    const int nm = bnm[g][off];
+    uint32_t md[kMaxMatches], mL[kMaxMatches];
+    float mc[kMaxMatches];
+#pragma unroll
+    for (int q = 0; q < kMaxMatches; q++) {
+      const uint64_t m = q < nm ? bmt[g][off * kMaxMatches + q] : 0ull;
+      md[q] = (uint32_t)(m >> 32);
+      mL[q] = min((uint32_t)m, limit);
+      mc[q] = q < nm ? bmc[g][off * kMaxMatches + q] : 0.f;
+    }
+    wave_sync();
+    if (sl == 0) cost[g][slot] = kInf;   // the slot now serves position i + kRing
+    // run length at the path's last distance, from the cache
+    uint32_t ldlen = 0;
+    const bool ldok = ld != 0 && ld <= i;
+    if (ldok && !(ld == c_ld && i >= c_from && i <= c_upto)) {
+      c_ld = ld;
+      c_from = c_upto = i;
+      c_end = false;
+    }
+    while (ldok && !c_end && c_upto - i <= (uint32_t)kLongCopy) {
+      const uint32_t k = c_upto + sl;
+      const bool eq = k < b && data[k] == data[k - ld];
+      const uint32_t ok = group_bits(__ballot(eq), g);
+      if (ok == 0xFFFFu) {
+        c_upto += kGL;
+      } else {
+        c_upto += __ffs(~ok) - 1;
+        c_end = true;
+      }
+    }
+    if (ldok) ldlen = min(c_upto - i, limit);
+    const int ic = ins_code(ins_i);
+    const float base = ci + (float)kInsExtra[ic];
+    // forceful long copy (backward-references-hq.ts:518-533)
+    uint32_t fd = 0, fl = 0;
+    float fc = 0.f;
+    if (ldlen > (uint32_t)kLongCopy) {
+      while (!c_end && c_upto - i < 65535u) {   // take the whole run
+        const uint32_t k = c_upto + sl;
+        const bool eq = k < b && data[k] == data[k - ld];
+        const uint32_t ok = group_bits(__ballot(eq), g);
+        if (ok == 0xFFFFu) {
+          c_upto += kGL;
+        } else {
+          c_upto += __ffs(~ok) - 1;
+          c_end = true;
+        }
+      }
+      fl = min(min(c_upto - i, limit), 65535u);
+      fd = ld;
+      const int cc = copy_code(fl);
+      const int cmd = combine_codes(ic, cc, true);
+      fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+    } else {
 #pragma unroll
       for (int q = 0; q < kMaxMatches; q++) {
-        const uint64_t m = q < nm ? bmt[off * kMaxMatches + q] : 0ull;
-        md[q] = (uint32_t)(m >> 32);
-        mL[q] = min((uint32_t)m, limit);
-        mc[q] = q < nm ? bmc[off * kMaxMatches + q] : 0.f;
+        if (!fl && q < nm && mL[q] > (uint32_t)kLongCopy) {
+          fd = md[q];
+          fl = mL[q];
+          const int cc = copy_code(fl);
+          fc = base + mc[q] + (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
+        }
       }
+    }
+    if (fl) {
+      // store the batch's finished nodes, abandon every pending node, resume at the copy's end
+      for (uint32_t p = i0 + sl; p <= i; p += kGL)
+        if (p != a) choice[gbase + p] = node_choice(meta[g][p & kRingMask]);
       wave_sync();
-      if (lane == 0) cost[slot] = kInf;   // the slot now serves position i + kRing
-      // ---- run length at the path's last distance (short code 0), from the cache
-      uint32_t ldlen = 0;
-      if (ld != 0 && ld <= i) {
-        if (!(ld == c_ld && i >= c_from && i <= c_upto)) {
-          c_ld = ld;
-          c_from = c_upto = i;
-          c_end = false;
-        }
-        while (!c_end && c_upto - i <= (uint32_t)kLongCopy) {
-          const uint32_t k = c_upto + lane;
-          const bool eq = k < b && data[k] == data[k - ld];
-          const uint64_t ok = __ballot(eq);
-          if (ok == ~0ull) {
-            c_upto += 64;
-          } else {
-            c_upto += __ffsll((unsigned long long)~ok) - 1;
-            c_end = true;
-          }
-        }
-        ldlen = min(c_upto - i, limit);
+      for (int t = sl; t < kRing; t += kGL) cost[g][t] = kInf;
+      wave_sync();
+      i += fl;
+      if (sl == 0) {
+        cost[g][i & kRingMask] = fc;
+        meta[g][i & kRingMask] = pack_node(fd, fl, 0);
       }
-      const int ic = ins_code(ins_i);
-      const float base = ci + (float)kInsExtra[ic];
-      // ---- forceful long copy (backward-references-hq.ts:518-533)
-      uint32_t fd = 0, fl = 0;
-      float fc = 0.f;
-      if (ldlen > (uint32_t)kLongCopy) {
-        while (!c_end && c_upto - i < 65535u) {   // take the whole run
-          const uint32_t k = c_upto + lane;
-          const bool eq = k < b && data[k] == data[k - ld];
-          const uint64_t ok = __ballot(eq);
-          if (ok == ~0ull) {
-            c_upto += 64;
-          } else {
-            c_upto += __ffsll((unsigned long long)~ok) - 1;
-            c_end = true;
-          }
+      flushed = true;
+      nb = 0;
+      i0 = i;
+      continue;
+    }
+    if (ic != cached_ic) {
+      cached_ic = ic;
+      cm0 = (float)kCopyExtra[cc0] + cmdc[combine_codes(ic, cc0, false)];
+      cm1 = (float)kCopyExtra[cc1] + cmdc[combine_codes(ic, cc1, false)];
+      int cmd = combine_codes(ic, cc0, true);
+      cml0 = (float)kCopyExtra[cc0] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+      cmd = combine_codes(ic, cc1, true);
+      cml1 = (float)kCopyExtra[cc1] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+    }
+    // relax every edge out of i: lane sl of chunk k takes length 16 k + sl, choosing the
+    // literal (length 1), the shortest-distance match covering it, or the last distance
+    uint32_t maxlen = max(1u, ldlen);
+#pragma unroll
+    for (int q = 0; q < kMaxMatches; q++)
+      if (q < nm) maxlen = max(maxlen, mL[q]);
+    for (uint32_t k = 0; kGL * k <= maxlen; k++) {
+      const uint32_t l = kGL * k + sl;
+      float best = kInf;
+      uint64_t bm = 0;
+      if (l == 1) {
+        best = ci + litcost;
+        bm = pack_node(ld, 0, ins_i + 1);
+      } else if (l >= 2 && l <= maxlen) {
+        float cmx, cml;
+        if (k == 0) {
+          cmx = cm0;
+          cml = cml0;
+        } else if (k == 1) {
+          cmx = cm1;
+          cml = cml1;
+        } else {
+          const int cc = copy_code(l);
+          const int cmd = combine_codes(ic, cc, true);
+          cmx = (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
+          cml = (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
         }
-        fl = min(min(c_upto - i, limit), 65535u);
-        fd = ld;
-        const int cc = copy_code(fl);
-        const int cmd = combine_codes(ic, cc, true);
-        fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-      } else {
+        bool found = false;
 #pragma unroll
         for (int q = 0; q < kMaxMatches; q++) {
-          if (!fl && q < nm && mL[q] > (uint32_t)kLongCopy) {
-            fd = md[q];
-            fl = mL[q];
-            const int cc = copy_code(fl);
-            fc = base + mc[q] + (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
+          if (!found && q < nm && mL[q] >= l) {
+            found = true;
+            best = base + mc[q] + cmx;
+            bm = pack_node(md[q], l, 0);
+          }
+        }
+        if (l <= ldlen) {
+          const float c2 = base + cml;
+          if (c2 < best) {
+            best = c2;
+            bm = pack_node(ld, l, 0);
           }
         }
       }
-      if (fl) {
-        // flush the batch's finished nodes, abandon every pending node, resume at the end
-        for (uint32_t p = i0 + lane; p <= i; p += 64)
-          if (p != a) choice[gbase + p] = node_choice(meta[p % kRing]);
-        wave_sync();
-        for (int t = lane; t < kRing; t += 64) cost[t] = kInf;
-        wave_sync();
-        const uint32_t skip_to = i + fl;
-        if (lane == 0) {
-          cost[skip_to % kRing] = fc;
-          meta[skip_to % kRing] = pack_node(fd, fl, 0);
-        }
-        wave_sync();
-        i = skip_to;
-        forced = true;
-        break;
-      }
-      if (ic != cached_ic) {
-        cached_ic = ic;
-#pragma unroll
-        for (int k = 0; k < kChunks; k++) {
-          cm[k] = cxl[k] + cmdc[combine_codes(ic, ccl[k], false)];
-          const int cmd = combine_codes(ic, ccl[k], true);
-          cml[k] = cxl[k] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+      if (best < kInf) {
+        const uint32_t ts = (i + l) & kRingMask;
+        if (best < cost[g][ts]) {
+          cost[g][ts] = best;
+          meta[g][ts] = bm;
         }
       }
-      // ---- relax every edge out of i: lane l of chunk k takes length 64 k + l, choosing
-      // the literal (l = 1), the shortest-distance match covering l, or the last distance
-      uint32_t maxlen = 1;
-#pragma unroll
-      for (int q = 0; q < kMaxMatches; q++)
-        if (q < nm) maxlen = max(maxlen, mL[q]);
-      maxlen = max(maxlen, ldlen);
-#pragma unroll
-      for (int k = 0; k < kChunks; k++) {
-        if (64 * k > (int)maxlen) break;
-        const uint32_t l = 64 * k + lane;
-        float best = kInf;
-        uint64_t bm = 0;
-        if (l == 1) {
-          best = ci + litcost;
-          bm = pack_node(ld, 0, ins_i + 1);
-        } else if (l >= 2 && l <= maxlen) {
-          if (l >= 4) {
-            bool found = false;
-#pragma unroll
-            for (int q = 0; q < kMaxMatches; q++) {
-              if (!found && q < nm && mL[q] >= l) {
-                found = true;
-                best = base + mc[q] + cm[k];
-                bm = pack_node(md[q], l, 0);
-              }
-            }
-          }
-          if (l <= ldlen) {
-            const float c2 = base + cml[k];
-            if (c2 < best) {
-              best = c2;
-              bm = pack_node(ld, l, 0);
-            }
-          }
-        }
-        if (best < kInf) {
-          const int ts = (i + l) % kRing;
-          if (best < cost[ts]) {
-            cost[ts] = best;
-            meta[ts] = bm;
-          }
-        }
-      }
-      wave_sync();
-      i++;
     }
-    if (!forced) {   // the batch's nodes are final: one coalesced store of their choices
-      const uint32_t p = i0 + lane;
-      if ((uint32_t)lane < nb && p != a) choice[gbase + p] = node_choice(meta[p % kRing]);
-    }
+    i++;
   }
-  // the segment's end node
-  if (lane == 0) choice[gbase + b] = node_choice(meta[b % kRing]);
 }
 
 // ---------------------------------------------------------------- 4. backtrack, lane per segment
@@ -322,7 +329,8 @@ __global__ void backtrack_kernel(const Job *jobs, Seg *segs, int nsegs, const ui
 
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                const uint64_t *matches, const uint8_t *nmatch, uint64_t *choice) {
-  hipLaunchKernelGGL(dp_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, lit_h, matches, nmatch, choice);
+  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kG - 1) / kG), dim3(64), 0, st, jobs, segs, nsegs, lit_h, matches, nmatch,
+                     choice);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {
   hipLaunchKernelGGL(backtrack_kernel, dim3((nsegs + 63) / 64), dim3(64), 0, st, jobs, segs, nsegs, choice, raw);
