@@ -9,16 +9,17 @@ namespace enc {
 // Shortest path over positions (updateNodes / computeShortestPathFromNodes,
 // backward-references-hq.ts:267-406): node i holds the cheapest cost of reaching i, the
 // insert length since the last copy, and the path's last distance.  Edges out of i: one
-// literal; the staircase matches of i (the shortest distance covering each length); a copy
-// at the path's last distance (short code 0).  A copy longer than kLongCopy is taken
-// outright and the parse jumps to its end, as the reference does (:518-533).
+// literal, and the staircase matches of i (the shortest distance covering each length),
+// priced with short code 0 when the distance is the path's last distance.  A copy longer
+// than kLongCopy is taken outright and the parse jumps to its end, as the reference does
+// (:518-533).
 //
 // One wave runs kG = 4 segments side by side, 16 lanes each: per step every group advances
 // its own segment by one position, its 16 lanes relaxing 16 copy lengths at a time, so the
-// per-position bookkeeping is paid once per 4 positions.  Everything a position needs that
-// does not depend on the parse state (its matches with their distance costs, its literal
-// cost) is staged into LDS 16 positions at a time; the last-distance run is measured
-// 16 bytes per probe and cached while the path keeps that distance.
+// per-position bookkeeping is paid once per 4 positions.  Everything a position needs (its
+// matches with their distance costs, its literal cost) is staged into LDS 16 positions at
+// a time from registers that were loaded one batch ahead, so the serial loop itself never
+// waits on global memory.
 constexpr int kG = 4;          // segments per wave
 constexpr int kGL = 16;        // lanes per segment
 constexpr int kBatch = 16;     // positions staged per refill
@@ -34,7 +35,20 @@ __device__ __forceinline__ uint64_t node_choice(uint64_t m) {   // (distance << 
   uint32_t cl = (uint32_t)(m >> 32) & 0xFFFF;
   return cl ? (((uint64_t)(uint32_t)m << 32) | cl) : 0ull;
 }
-__device__ __forceinline__ uint32_t group_bits(uint64_t ballot, int g) { return (uint32_t)(ballot >> (kGL * g)) & 0xFFFFu; }
+
+struct Staged {   // one position's parse inputs, loaded ahead
+  uint64_t m[kMaxMatches];
+  uint32_t nm;
+  uint32_t lit;
+};
+__device__ __forceinline__ void load_staged(Staged &st, const uint64_t *matches, const uint8_t *nmatch, const uint8_t *data,
+                                            uint32_t g, uint32_t p) {
+  st.nm = nmatch[g];
+  st.lit = data[p];
+  const uint64_t *src = matches + (uint64_t)g * kMaxMatches;
+#pragma unroll
+  for (int q = 0; q < kMaxMatches; q++) st.m[q] = src[q];   // entries past nm are ignored
+}
 
 __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_histo,
                                                 const uint64_t *matches, const uint8_t *nmatch,
@@ -80,12 +94,16 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
   const int cc0 = copy_code(l0c), cc1 = copy_code(l1c);
   float cm0 = 0.f, cm1 = 0.f, cml0 = 0.f, cml1 = 0.f;
   int cached_ic = -1;
-  // the path's last distance: verified run [c_from, c_upto) of data[p] == data[p - c_ld]
-  uint32_t c_ld = 0, c_from = 0, c_upto = 0;
-  bool c_end = false;
   bool active = valid && a < b;
   uint32_t i = a, i0 = a, nb = 0;
   bool flushed = true;   // the current batch's choices are already stored
+  // the batch after the current one, in registers
+  Staged pf;
+  uint32_t pf_at = 0xFFFFFFFFu;
+  if (active && a + sl < b) {
+    load_staged(pf, matches, nmatch, data, gbase + a + sl, a + sl);
+    pf_at = a;
+  }
   wave_sync();
   for (;;) {
     // ---- per group: finish a batch (store its choices), finish the segment, or stage
@@ -98,19 +116,31 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
         i0 = i;
         nb = min((uint32_t)kBatch, b - i0);
         flushed = false;
+        Staged cur;
+        if (pf_at == i0) {
+          cur = pf;
+        } else if (i0 + sl < b) {   // the parse jumped past the prefetched batch
+          load_staged(cur, matches, nmatch, data, gbase + i0 + sl, i0 + sl);
+        }
+        // prefetch the next batch
+        const uint32_t nx = i0 + nb;
+        if (nx + sl < b) load_staged(pf, matches, nmatch, data, gbase + nx + sl, nx + sl);
+        pf_at = nx;
         int nm = 0;
         if ((uint32_t)sl < nb) {
-          nm = nmatch[gbase + i0 + sl];
-          blit[g][sl] = litc[g][data[i0 + sl]];
+          nm = (int)cur.nm;
+          blit[g][sl] = litc[g][cur.lit];
         }
         bnm[g][sl] = (uint8_t)nm;
-        const uint64_t *src = matches + (uint64_t)(gbase + i0 + sl) * kMaxMatches;
-        for (int q = 0; q < nm; q++) {
-          const uint64_t m = src[q];
-          uint32_t extra;
-          const uint32_t dp = dist_prefix((uint32_t)(m >> 32) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
-          bmt[g][sl * kMaxMatches + q] = m;
-          bmc[g][sl * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
+#pragma unroll
+        for (int q = 0; q < kMaxMatches; q++) {
+          if (q < nm) {
+            const uint64_t m = cur.m[q];
+            uint32_t extra;
+            const uint32_t dp = dist_prefix((uint32_t)(m >> 32) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
+            bmt[g][sl * kMaxMatches + q] = m;
+            bmc[g][sl * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
+          }
         }
       }
     }
@@ -136,57 +166,29 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
     }
     wave_sync();
     if (sl == 0) cost[g][slot] = kInf;   // the slot now serves position i + kRing
-    // run length at the path's last distance, from the cache
-    uint32_t ldlen = 0;
-    const bool ldok = ld != 0 && ld <= i;
-    if (ldok && !(ld == c_ld && i >= c_from && i <= c_upto)) {
-      c_ld = ld;
-      c_from = c_upto = i;
-      c_end = false;
-    }
-    while (ldok && !c_end && c_upto - i <= (uint32_t)kLongCopy) {
-      const uint32_t k = c_upto + sl;
-      const bool eq = k < b && data[k] == data[k - ld];
-      const uint32_t ok = group_bits(__ballot(eq), g);
-      if (ok == 0xFFFFu) {
-        c_upto += kGL;
-      } else {
-        c_upto += __ffs(~ok) - 1;
-        c_end = true;
-      }
-    }
-    if (ldok) ldlen = min(c_upto - i, limit);
     const int ic = ins_code(ins_i);
     const float base = ci + (float)kInsExtra[ic];
+    if (ic != cached_ic) {
+      cached_ic = ic;
+      cm0 = (float)kCopyExtra[cc0] + cmdc[combine_codes(ic, cc0, false)];
+      cm1 = (float)kCopyExtra[cc1] + cmdc[combine_codes(ic, cc1, false)];
+      int cmd = combine_codes(ic, cc0, true);
+      cml0 = (float)kCopyExtra[cc0] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+      cmd = combine_codes(ic, cc1, true);
+      cml1 = (float)kCopyExtra[cc1] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+    }
     // forceful long copy (backward-references-hq.ts:518-533)
-    uint32_t fd = 0, fl = 0;
+    uint32_t fl = 0, fd = 0;
     float fc = 0.f;
-    if (ldlen > (uint32_t)kLongCopy) {
-      while (!c_end && c_upto - i < 65535u) {   // take the whole run
-        const uint32_t k = c_upto + sl;
-        const bool eq = k < b && data[k] == data[k - ld];
-        const uint32_t ok = group_bits(__ballot(eq), g);
-        if (ok == 0xFFFFu) {
-          c_upto += kGL;
-        } else {
-          c_upto += __ffs(~ok) - 1;
-          c_end = true;
-        }
-      }
-      fl = min(min(c_upto - i, limit), 65535u);
-      fd = ld;
-      const int cc = copy_code(fl);
-      const int cmd = combine_codes(ic, cc, true);
-      fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-    } else {
 #pragma unroll
-      for (int q = 0; q < kMaxMatches; q++) {
-        if (!fl && q < nm && mL[q] > (uint32_t)kLongCopy) {
-          fd = md[q];
-          fl = mL[q];
-          const int cc = copy_code(fl);
-          fc = base + mc[q] + (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
-        }
+    for (int q = 0; q < kMaxMatches; q++) {
+      if (!fl && q < nm && mL[q] > (uint32_t)kLongCopy) {
+        fd = md[q];
+        fl = mL[q];
+        const int cc = copy_code(fl);
+        const bool last = fd == ld;
+        const int cmd = combine_codes(ic, cc, last);
+        fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (last ? (cmd < 128 ? 0.f : distc[0]) : mc[q]);
       }
     }
     if (fl) {
@@ -206,18 +208,9 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
       i0 = i;
       continue;
     }
-    if (ic != cached_ic) {
-      cached_ic = ic;
-      cm0 = (float)kCopyExtra[cc0] + cmdc[combine_codes(ic, cc0, false)];
-      cm1 = (float)kCopyExtra[cc1] + cmdc[combine_codes(ic, cc1, false)];
-      int cmd = combine_codes(ic, cc0, true);
-      cml0 = (float)kCopyExtra[cc0] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-      cmd = combine_codes(ic, cc1, true);
-      cml1 = (float)kCopyExtra[cc1] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-    }
     // relax every edge out of i: lane sl of chunk k takes length 16 k + sl, choosing the
-    // literal (length 1), the shortest-distance match covering it, or the last distance
-    uint32_t maxlen = max(1u, ldlen);
+    // literal (length 1) or the shortest-distance match covering it
+    uint32_t maxlen = 1;
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++)
       if (q < nm) maxlen = max(maxlen, mL[q]);
@@ -228,7 +221,7 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
       if (l == 1) {
         best = ci + litcost;
         bm = pack_node(ld, 0, ins_i + 1);
-      } else if (l >= 2 && l <= maxlen) {
+      } else if (l >= 4 && l <= maxlen) {
         float cmx, cml;
         if (k == 0) {
           cmx = cm0;
@@ -247,15 +240,8 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
         for (int q = 0; q < kMaxMatches; q++) {
           if (!found && q < nm && mL[q] >= l) {
             found = true;
-            best = base + mc[q] + cmx;
+            best = base + (md[q] == ld ? cml : mc[q] + cmx);
             bm = pack_node(md[q], l, 0);
-          }
-        }
-        if (l <= ldlen) {
-          const float c2 = base + cml;
-          if (c2 < best) {
-            best = c2;
-            bm = pack_node(ld, l, 0);
           }
         }
       }
