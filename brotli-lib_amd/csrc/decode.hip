@@ -54,6 +54,8 @@ enum : int {
 constexpr int kBlockTreesCap = 3091;   // engine.ts:163 Int32Array(3091)
 
 // LDS working set of one stream (one wave).
+constexpr int kLdsTableInts = 4096;   // 16 KiB of prefix-code tables in LDS (one tree per alphabet fits)
+
 struct Lds {
   uint8_t win[4160 + 64];    // byteBuffer (4160) + read slack
   int lens[1080];            // code lengths scratch
@@ -77,7 +79,8 @@ struct Dec {
   int mbl, input_end, is_uncompressed, is_metadata;
   int lit_blen, n_lit_types, cmd_blen, n_cmd_types, dist_blen, n_dist_types;
   int rings[10], dist_rb_idx;
-  int32_t *lit_group, *cmd_group, *dist_group;   // HBM scratch
+  int32_t *lit_group, *cmd_group, *dist_group;   // LDS when the metablock's codes fit, else HBM scratch
+  int32_t *tab_lds, *tab_hbm;
   uint8_t *ctx_modes, *ctx_map, *dist_ctx_map;   // HBM scratch
   int trivial_lit_ctx, lit_tree_idx, cmd_tree_idx;
   int j, insert_len, copy_len, dist_code, distance;
@@ -98,7 +101,13 @@ struct Dec {
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
-__device__ __forceinline__ void wave_sync() { __syncthreads(); }
+// A block is one wave: a wave's LDS and global accesses are performed in order, so the
+// lanes only need a compiler fence at wavefront scope between dependent steps.  (A
+// workgroup barrier would also wait for every outstanding ring store, once per command.)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
 // ---------------------------------------------------------------- bit reader
 __device__ __forceinline__ uint32_t half_at(const Dec &s, int h) {
@@ -586,10 +595,12 @@ __device__ int read_partition(Dec &s, int tt, int ntypes) {   // :679-704
 
 __device__ int decode_tree_group(Dec &s, int amax, int alimit, int n, int32_t *group) {
   int next = n;
+  // tables in LDS must not run past the LDS area (complete codes never do)
+  const int cap = s.lit_group == s.tab_lds ? (int)(s.tab_lds + kLdsTableInts - group) : kNoCap;
   for (int i = 0; i < n; i++) {
     if (s.lane == 0) group[i] = next;
     wave_sync();
-    int r = read_huffman_code(s, amax, alimit, group, kNoCap, i);
+    int r = read_huffman_code(s, amax, alimit, group, cap, i);
     if (r < 0) return r;
     next += r;
   }
@@ -631,7 +642,11 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
   s.trivial_lit_ctx = __any(nontrivial) ? 0 : 1;
   if ((r = decode_context_map(s, s.n_dist_types << 2, s.dist_ctx_map, ctxmap_table)) < 0) return r;
   int ndist_trees = r;
-  // groups live back to back in the table scratch: literal, command, distance
+  // groups live back to back: literal, command, distance.  A metablock with few prefix
+  // codes (the common case: one tree per alphabet) gets them in LDS, so every symbol
+  // lookup is an LDS read instead of a dependent HBM load.
+  const int need = nlit_trees * (1 + 630) + s.n_cmd_types * (1 + 1080) + ndist_trees * (1 + 1080);
+  s.lit_group = need <= kLdsTableInts ? s.tab_lds : s.tab_hbm;
   s.cmd_group = s.lit_group + (size_t)nlit_trees * (1 + 630);
   if ((r = decode_tree_group(s, 256, 256, nlit_trees, s.lit_group)) < 0) return r;
   s.dist_group = s.cmd_group + (size_t)s.n_cmd_types * (1 + 1080);
@@ -1166,6 +1181,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
 __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int njobs, uint8_t *scratch,
                                                             uint64_t per_block, uint64_t ring_bytes) {
   __shared__ Lds lds;
+  __shared__ int32_t ltab[kLdsTableInts];
   uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
   uint8_t *ring = base;
   int32_t *tables = reinterpret_cast<int32_t *>(base + ring_bytes);
@@ -1205,6 +1221,8 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     for (int i = 0; i < 10; i++) s.rings[i] = 0;
     s.rings[0] = 16; s.rings[1] = 15; s.rings[2] = 11; s.rings[3] = 4;
     s.dist_rb_idx = 3;
+    s.tab_lds = ltab;
+    s.tab_hbm = tables;
     s.lit_group = tables;
     s.cmd_group = tables;
     s.dist_group = tables;
