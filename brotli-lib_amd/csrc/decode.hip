@@ -36,8 +36,6 @@ __constant__ int16_t kCmdLut[704 * 4];   // engine.ts:65-90, filled by the host 
 static __device__ const int kMaxHuffTable[23] = {256, 402, 436, 468, 500, 534, 566, 598, 630, 662, 694, 726,
                                                  758, 790, 822, 854, 886, 920, 952, 984, 1016, 1048, 1080};
 static __device__ const uint8_t kCodeLenOrder[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-static __device__ const int8_t kDistIdxOff[16] = {0, 3, 2, 1, 0, 0, 0, 0, 0, 0, 3, 3, 3, 3, 3, 3};
-static __device__ const int8_t kDistValOff[16] = {0, 0, 0, 0, -1, 1, -2, 2, -3, 3, -1, 1, -2, 2, -3, 3};
 static __device__ const int kFixedCL[16] = {0x020000, 0x020004, 0x020003, 0x030002, 0x020000, 0x020004,
                                             0x020003, 0x040001, 0x020000, 0x020004, 0x020003, 0x030002,
                                             0x020000, 0x020004, 0x020003, 0x040005};
@@ -915,88 +913,181 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
       case ST_MAIN_LOOP:
       case ST_INSERT_LOOP:
       case ST_COPY_LOOP: {
+        // The command / literal / copy loop runs on registers: the bit reader, positions,
+        // lengths and block counters are loaded from `s` once, saved back around every
+        // cold call (refill, block switch) and on every exit.
         int phase = s.running;
         uint8_t *ring = s.ring;
+        const uint8_t *win = s.l->win;
+        const int ring_cap = s.ring_cap, npostfix = s.npostfix, ndirect = s.ndirect, max_back = s.max_back;
+        const int32_t *cmd_g = s.cmd_group, *dist_g = s.dist_group, *lit_g = s.lit_group;
+        const int lane = s.lane;
+        uint32_t acc;
+        int bo, ho, pos, j, mbl, insert_len, copy_len, dist_code, distance, cmd_blen, lit_blen, dist_blen, max_dist;
+        uint64_t guard;
+#define HOT_LOAD()                                                                                      \
+  do {                                                                                                  \
+    acc = s.acc; bo = s.bo; ho = s.ho; pos = s.pos; j = s.j; mbl = s.mbl; insert_len = s.insert_len;    \
+    copy_len = s.copy_len; dist_code = s.dist_code; distance = s.distance; cmd_blen = s.cmd_blen;       \
+    lit_blen = s.lit_blen; dist_blen = s.dist_blen; max_dist = s.max_dist; guard = s.guard;              \
+  } while (0)
+#define HOT_SAVE()                                                                                      \
+  do {                                                                                                  \
+    s.acc = acc; s.bo = bo; s.ho = ho; s.pos = pos; s.j = j; s.mbl = mbl; s.insert_len = insert_len;    \
+    s.copy_len = copy_len; s.dist_code = dist_code; s.distance = distance; s.cmd_blen = cmd_blen;       \
+    s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist; s.guard = guard;              \
+  } while (0)
+#define LHALF(h) (((h) < 0 || (h) >= 2080) ? 0u : ((uint32_t)win[2 * (h)] | ((uint32_t)win[2 * (h) + 1] << 8)))
+#define LFILL16()                                     \
+  do {                                                \
+    if (bo >= 16) {                                   \
+      acc = (LHALF(ho) << 16) | (acc >> 16);          \
+      ho++;                                           \
+      bo -= 16;                                       \
+    }                                                 \
+  } while (0)
+#define LREFILL()                                     \
+  do {                                                \
+    if (ho > 2030) {                                  \
+      HOT_SAVE();                                     \
+      int r_ = read_more_input(s);                    \
+      if (r_ < 0) return r_;                          \
+      HOT_LOAD();                                     \
+    }                                                 \
+  } while (0)
+        HOT_LOAD();
+        auto lbits = [&](int n) -> int {
+          int v = (int)((acc >> (bo & 31)) & ((1u << n) - 1u));
+          bo += n;
+          return v;
+        };
+        auto lmany = [&](int n) -> int {
+          int lo = lbits(16);
+          acc = (LHALF(ho) << 16) | (acc >> 16);
+          ho++;
+          bo -= 16;
+          return lo | (lbits(n - 16) << 16);
+        };
+        auto lsym = [&](const int32_t *g, int idx) -> int {   // read_symbol on registers
+          int off = g[idx];
+          uint32_t v = acc >> (bo & 31);
+          off += (int)(v & 0xFF);
+          int e0 = g[off];
+          int nb = e0 >> 16;
+          if (nb <= 8) {
+            bo += nb;
+            return e0 & 0xFFFF;
+          }
+          off += e0 & 0xFFFF;
+          off += (int)((v & ((1u << nb) - 1u)) >> 8);
+          int e1 = g[off];
+          bo += (e1 >> 16) + 8;
+          return e1 & 0xFFFF;
+        };
+        int cmd_tree_idx = s.cmd_tree_idx;
+        uint32_t dtrees = 0;   // the 4 distance trees of the current distance block type
+        for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
         for (;;) {
-          if (++s.guard > s.guard_limit) return MIB_E_NO_PROGRESS;
+          if (++guard > s.guard_limit) {
+            HOT_SAVE();
+            return MIB_E_NO_PROGRESS;
+          }
           if (phase == ST_MAIN_LOOP) {   // command (:1080-1152)
-            if (s.mbl <= 0) {
+            if (mbl <= 0) {
               s.running = ST_BLOCK_START;
               break;
             }
-            MAYBE_REFILL(s);
-            if (s.cmd_blen == 0) {
+            LREFILL();
+            if (cmd_blen == 0) {
+              HOT_SAVE();
               s.cmd_blen = decode_block_type_and_length(s, 1, s.n_cmd_types);
               s.cmd_tree_idx = s.rings[7];
+              HOT_LOAD();
+              cmd_tree_idx = s.cmd_tree_idx;
             }
-            s.cmd_blen--;
-            fill16(s);
-            int sym = read_symbol(s, s.cmd_group, kNoCap, s.cmd_tree_idx);
-            int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
-            s.dist_code = kCmdLut[4 * sym + 3];
-            fill16(s);
-            int ib = cbits & 0xFF;
-            s.insert_len = ins_off + (ib <= 16 ? bits(s, ib) : many_bits(s, ib));
-            fill16(s);
-            int cb = cbits >> 8;
-            s.copy_len = copy_off + (cb <= 16 ? bits(s, cb) : many_bits(s, cb));
-            s.j = 0;
+            cmd_blen--;
+            LFILL16();
+            const int sym = lsym(cmd_g, cmd_tree_idx);
+            const int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
+            dist_code = kCmdLut[4 * sym + 3];
+            LFILL16();
+            const int ib = cbits & 0xFF;
+            insert_len = ins_off + (ib <= 16 ? lbits(ib) : lmany(ib));
+            LFILL16();
+            const int cb = cbits >> 8;
+            copy_len = copy_off + (cb <= 16 ? lbits(cb) : lmany(cb));
+            j = 0;
             phase = ST_INSERT_LOOP;
           }
           if (phase <= ST_INSERT_LOOP) {   // literals (:1154-1276)
             int stop = 0;
-            while (s.j < s.insert_len) {
-              MAYBE_REFILL(s);
-              if (s.lit_blen == 0) {
+            while (j < insert_len) {
+              LREFILL();
+              if (lit_blen == 0) {
+                HOT_SAVE();
                 lit_block_switch(s);
                 if (!s.trivial_lit_ctx) build_ctx_tree_base(s);
+                HOT_LOAD();
               }
-              int a = s.insert_len - s.j, b = s.lit_blen, c2 = fence - s.pos, d = 2031 - s.ho;
+              int a = insert_len - j, b = lit_blen, c2 = fence - pos, d = 2031 - ho;
               int batch = a < b ? a : b;
               if (c2 < batch) batch = c2;
               if (d < batch) batch = d;
               if (d <= 0 && batch <= 0 && a > 0 && b > 0 && c2 > 0) batch = 1;   // Bug J fix
-              s.lit_blen -= batch;
-              int end = s.j + batch;
+              lit_blen -= batch;
+              const int end = j + batch;
               if (s.trivial_lit_ctx) {
-                const int32_t *g = s.lit_group;
-                int ti = s.lit_tree_idx;
-                while (s.j < end) {
-                  fill16(s);
-                  int v = read_symbol(s, g, kNoCap, ti);
-                  if (s.lane == 0 && s.pos < s.ring_cap) ring[s.pos] = (uint8_t)v;
-                  s.pos++;
-                  s.j++;
+                const int root = lit_g[s.lit_tree_idx];
+                while (j < end) {
+                  LFILL16();
+                  const uint32_t v = acc >> (bo & 31);
+                  int off = root + (int)(v & 0xFF);
+                  const int e0 = lit_g[off];
+                  const int nb = e0 >> 16;
+                  int val;
+                  if (nb <= 8) {
+                    bo += nb;
+                    val = e0 & 0xFFFF;
+                  } else {
+                    off += e0 & 0xFFFF;
+                    off += (int)((v & ((1u << nb) - 1u)) >> 8);
+                    const int e1 = lit_g[off];
+                    bo += (e1 >> 16) + 8;
+                    val = e1 & 0xFFFF;
+                  }
+                  if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)val;
+                  pos++;
+                  j++;
                 }
               } else {
-                int p1 = ring[(s.pos - 1) & rmask], p2 = ring[(s.pos - 2) & rmask];
-                const int32_t *g = s.lit_group;
+                int p1 = ring[(pos - 1) & rmask], p2 = ring[(pos - 2) & rmask];
                 const int32_t *ctb = s.l->ctx_tree_base;
-                while (s.j < end) {
-                  int ctx = kRfcContextLut[s.clo1 + p1] | kRfcContextLut[s.clo2 + p2];
+                const int clo1 = s.clo1, clo2 = s.clo2;
+                while (j < end) {
+                  const int ctx = kRfcContextLut[clo1 + p1] | kRfcContextLut[clo2 + p2];
                   p2 = p1;
-                  fill16(s);
+                  LFILL16();
                   int off = ctb[ctx];
-                  uint32_t v = peek(s);
+                  const uint32_t v = acc >> (bo & 31);
                   off += (int)(v & 0xFF);
-                  int e0 = g[off], nb = e0 >> 16;
+                  const int e0 = lit_g[off], nb = e0 >> 16;
                   if (nb <= 8) {
-                    s.bo += nb;
+                    bo += nb;
                     p1 = e0 & 0xFFFF;
                   } else {
                     off += e0 & 0xFFFF;
                     off += (int)((v & ((1u << nb) - 1u)) >> 8);
-                    int e1 = g[off];
-                    s.bo += (e1 >> 16) + 8;
+                    const int e1 = lit_g[off];
+                    bo += (e1 >> 16) + 8;
                     p1 = e1 & 0xFFFF;
                   }
-                  if (s.lane == 0 && s.pos < s.ring_cap) ring[s.pos] = (uint8_t)p1;
-                  s.pos++;
-                  s.j++;
+                  if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)p1;
+                  pos++;
+                  j++;
                 }
               }
               wave_sync();
-              if (s.pos >= fence) {
+              if (pos >= fence) {
                 s.next_running = ST_INSERT_LOOP;
                 s.running = ST_INIT_WRITE;
                 stop = 1;
@@ -1004,97 +1095,135 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               }
             }
             if (stop) break;
-            s.mbl -= s.insert_len;   // distance (:1277-1377)
-            if (s.mbl <= 0) {
+            mbl -= insert_len;   // distance (:1277-1377)
+            if (mbl <= 0) {
               s.running = ST_BLOCK_START;
               break;
             }
-            int dc = s.dist_code;
+            int dc = dist_code;
             if (dc < 0) {
-              s.distance = s.rings[s.dist_rb_idx];
+              distance = s.rings[s.dist_rb_idx];
             } else {
-              MAYBE_REFILL(s);
-              if (s.dist_blen == 0) {
+              LREFILL();
+              if (dist_blen == 0) {
+                HOT_SAVE();
                 s.dist_blen = decode_block_type_and_length(s, 2, s.n_dist_types);
                 s.dist_ctx_map_slice = s.rings[9] << 2;
+                HOT_LOAD();
+                dtrees = 0;
+                for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
               }
-              s.dist_blen--;
-              fill16(s);
-              int tree = s.dist_ctx_map[s.dist_ctx_map_slice + dc];
-              dc = read_symbol(s, s.dist_group, kNoCap, tree);
+              dist_blen--;
+              LFILL16();
+              dc = lsym(dist_g, (int)((dtrees >> (8 * dc)) & 0xFF));
               if (dc < 16) {
-                int idx = (s.dist_rb_idx + kDistIdxOff[dc]) & 3;
-                s.distance = s.rings[idx] + kDistValOff[dc];
-                if (s.distance < 0) return ERR(s, -12);
-              } else {
-                int eb = dist_extra[dc], bv;
-                if (s.bo + eb <= 32) {
-                  bv = (int)(peek(s) & ((1u << eb) - 1u));
-                  s.bo += eb;
-                } else {
-                  fill16(s);
-                  bv = eb <= 16 ? bits(s, eb) : many_bits(s, eb);
+                // short codes: ring slot and value offsets (kDistIdxOff / kDistValOff, packed)
+                const int idx = (s.dist_rb_idx + (int)((0xfff0006cu >> (2 * dc)) & 3)) & 3;
+                distance = s.rings[idx] + (int)((0xc298b0a626dbull >> (3 * dc)) & 7) - 3;
+                if (distance < 0) {
+                  HOT_SAVE();
+                  return ERR(s, -12);
                 }
-                s.distance = dist_offset[dc] + (bv << s.npostfix);
+              } else {
+                // calculateDistanceLut (:705-726) in closed form
+                int eb, doff;
+                if (dc < 16 + ndirect) {
+                  eb = 0;
+                  doff = dc - 15;
+                } else {
+                  const int dcp = dc - ndirect - 16, hcode = dcp >> npostfix, lcode = dcp & ((1 << npostfix) - 1);
+                  eb = 1 + (hcode >> 1);
+                  doff = ((((2 + (hcode & 1)) << eb) - 4) << npostfix) + lcode + ndirect + 1;
+                }
+                int bv;
+                if (bo + eb <= 32) {
+                  bv = (int)((acc >> (bo & 31)) & ((1u << eb) - 1u));
+                  bo += eb;
+                } else {
+                  LFILL16();
+                  bv = eb <= 16 ? lbits(eb) : lmany(eb);
+                }
+                distance = doff + (bv << npostfix);
               }
             }
-            if (s.max_dist != s.max_back && s.pos < s.max_back) s.max_dist = s.pos;
-            else s.max_dist = s.max_back;
-            if (s.distance > s.max_dist) {
+            if (max_dist != max_back && pos < max_back) max_dist = pos;
+            else max_dist = max_back;
+            if (distance > max_dist) {
               s.running = ST_USE_DICTIONARY;
               break;
             }
             if (dc > 0) {
               s.dist_rb_idx = (s.dist_rb_idx + 1) & 3;
-              s.rings[s.dist_rb_idx] = s.distance;
+              s.rings[s.dist_rb_idx] = distance;
             }
-            if (s.copy_len > s.mbl) return ERR(s, -9);
-            s.j = 0;
+            if (copy_len > mbl) {
+              HOT_SAVE();
+              return ERR(s, -9);
+            }
+            j = 0;
             phase = ST_COPY_LOOP;
           }
           {   // copy (:1379-1433)
-            int dist = s.distance, cl = s.copy_len - s.j;
-            int src = (s.pos - dist) & rmask;
-            if (src + cl < rmask && s.pos + cl < rmask) {
-              ring_copy_fast(s, src, cl, dist);
-              s.j = s.copy_len;
-              s.mbl -= cl;
-              s.pos += cl;
+            const int dist = distance, cl = copy_len - j;
+            const int src = (pos - dist) & rmask;
+            if (src + cl < rmask && pos + cl < rmask) {
+              if (dist >= cl) {
+                for (int k = lane; k < cl; k += 64) ring[pos + k] = ring[src + k];
+              } else {
+                int q = lane % dist;
+                const int qstep = 64 % dist;
+                for (int k = lane; k < cl; k += 64) {
+                  ring[pos + k] = ring[src + q];
+                  q += qstep;
+                  if (q >= dist) q -= dist;
+                }
+              }
+              wave_sync();
+              j = copy_len;
+              mbl -= cl;
+              pos += cl;
             } else {
               // ring wrap and/or fence inside the copy: chunks that never read their own writes
               int cut = 0;
-              while (s.j < s.copy_len) {
-                int rem = s.copy_len - s.j;
-                int room = fence - s.pos;
+              while (j < copy_len) {
+                const int rem = copy_len - j;
+                const int room = fence - pos;
                 int chunk = rem < 4096 ? rem : 4096;
                 if (dist >= s.ring_size - 4096) chunk = rem < 64 ? rem : 64;
                 if (dist >= s.ring_size - 64) chunk = 1;
                 if (room < chunk) chunk = room;
                 if (chunk < 1) chunk = 1;
                 // byte p copies the byte dist back, or (overlap) its periodic image before pos
-                int base = s.pos - dist;
-                for (int k = s.lane; k < chunk; k += 64) {
-                  int p = s.pos + k;
-                  int srcp = base + (dist > k ? k : k % dist);
-                  uint8_t v = ring[srcp & rmask];
-                  if (p < s.ring_cap) ring[p] = v;
+                const int base = pos - dist;
+                for (int k = lane; k < chunk; k += 64) {
+                  const int p = pos + k;
+                  const int srcp = base + (dist > k ? k : k % dist);
+                  const uint8_t v = ring[srcp & rmask];
+                  if (p < ring_cap) ring[p] = v;
                 }
                 wave_sync();
-                s.mbl -= chunk;
-                s.pos += chunk;
-                s.j += chunk;
-                if (s.pos >= fence) {
+                mbl -= chunk;
+                pos += chunk;
+                j += chunk;
+                if (pos >= fence) {
                   s.next_running = ST_COPY_LOOP;
                   s.running = ST_INIT_WRITE;
                   break;
                 }
               }
-              if (s.j < s.copy_len) cut = 1;
+              if (j < copy_len) cut = 1;
               if (cut) break;
             }
             phase = ST_MAIN_LOOP;
           }
         }
+        HOT_SAVE();
+        s.cmd_tree_idx = cmd_tree_idx;
+#undef HOT_LOAD
+#undef HOT_SAVE
+#undef LHALF
+#undef LFILL16
+#undef LREFILL
         continue;
       }
       case ST_USE_DICTIONARY:
