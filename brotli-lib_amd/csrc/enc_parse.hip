@@ -14,15 +14,18 @@ namespace enc {
 // than kLongCopy is taken outright and the parse jumps to its end, as the reference does
 // (:518-533).
 //
-// One wave runs kG = 4 segments side by side, 16 lanes each: per step every group advances
-// its own segment by one position, its 16 lanes relaxing 16 copy lengths at a time, so the
-// per-position bookkeeping is paid once per 4 positions.  Everything a position needs (its
+// One wave runs kG = 2 segments side by side, 32 lanes each: per step every group advances
+// its own segment by one position, its 32 lanes relaxing 32 copy lengths at a time, so the
+// per-position bookkeeping is paid once per 2 positions.  (Measured on MI355X, 1 GiB of
+// text: 1 x 64 lanes 696 ms, 2 x 32 474 ms, 4 x 16 518 ms, 8 x 8 897 ms -- beyond two
+// groups the groups' divergent refills and long-match chunks cost more than they save.)  Everything a position needs (its
 // matches with their distance costs, its literal cost) is staged into LDS 16 positions at
 // a time from registers that were loaded one batch ahead, so the serial loop itself never
 // waits on global memory.
-constexpr int kG = 4;          // segments per wave
-constexpr int kGL = 16;        // lanes per segment
-constexpr int kBatch = 16;     // positions staged per refill
+constexpr int kGL = 32;        // lanes per segment
+constexpr int kG = 64 / kGL;   // segments per wave
+constexpr int kBatch = kGL;    // positions staged per refill (one per lane)
+constexpr int kCache = kGL >= 32 ? 1 : 32 / kGL;   // length chunks whose command costs stay in registers
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr float kInf = 3.0e38f;
 static_assert(kLongCopy + kBatch < kRing, "a batch's nodes must survive until they are flushed");
@@ -53,15 +56,16 @@ __device__ __forceinline__ void load_staged(Staged &st, const uint64_t *matches,
 __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_histo,
                                                 const uint64_t *matches, const uint8_t *nmatch,
                                                 uint64_t *choice /* per position+1 */) {
-  __shared__ float cost[kG][kRing];
-  __shared__ uint64_t meta[kG][kRing];
-  __shared__ float litc[kG][256];
+  // per-group rows are padded so the 4 groups' same-offset accesses fall in different banks
+  __shared__ float cost[kG][kRing + 1];
+  __shared__ uint64_t meta[kG][kRing + 1];
+  __shared__ uint16_t litc[kG][256 + 2];   // literal cost x 256
   __shared__ float cmdc[704];
   __shared__ float distc[128];
-  __shared__ float blit[kG][kBatch];
-  __shared__ uint8_t bnm[kG][kBatch];
-  __shared__ uint64_t bmt[kG][kBatch * kMaxMatches];   // (distance << 32) | length
-  __shared__ float bmc[kG][kBatch * kMaxMatches];      // distance symbol cost + extra bits
+  __shared__ float blit[kG][kBatch + 1];
+  __shared__ uint8_t bnm[kG][kBatch + 4];
+  __shared__ uint64_t bmt[kG][kBatch * kMaxMatches + 1];   // (distance << 32) | length
+  __shared__ float bmc[kG][kBatch * kMaxMatches + 1];      // distance symbol cost + extra bits
   const int lane = threadIdx.x, g = lane / kGL, sl = lane % kGL;
   const int s = blockIdx.x * kG + g;
   const bool valid = s < nsegs;
@@ -80,7 +84,7 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
     for (int i = sl; i < 256; i += kGL) {
       const uint32_t c = lit_histo[sg.job * 256 + i];
       const float v = c ? lt - log2f((float)c) : lt + 2.f;
-      litc[g][i] = v < 1.f ? 1.f : v;
+      litc[g][i] = (uint16_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f);
     }
   }
   for (int i = sl; i < kRing; i += kGL) {
@@ -90,9 +94,13 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
   wave_sync();
   if (sl == 0) cost[g][a & kRingMask] = 0.f;
   // command cost of this lane's lengths in chunks 0 and 1 for the current insert code
-  const uint32_t l0c = max(2u, (uint32_t)sl), l1c = kGL + sl;
-  const int cc0 = copy_code(l0c), cc1 = copy_code(l1c);
-  float cm0 = 0.f, cm1 = 0.f, cml0 = 0.f, cml1 = 0.f;
+  int ccA[kCache];
+  float cmA[kCache], cmlA[kCache];
+#pragma unroll
+  for (int c = 0; c < kCache; c++) {
+    ccA[c] = copy_code(max(2u, (uint32_t)(kGL * c + sl)));
+    cmA[c] = cmlA[c] = 0.f;
+  }
   int cached_ic = -1;
   bool active = valid && a < b;
   uint32_t i = a, i0 = a, nb = 0;
@@ -129,7 +137,7 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
         int nm = 0;
         if ((uint32_t)sl < nb) {
           nm = (int)cur.nm;
-          blit[g][sl] = litc[g][cur.lit];
+          blit[g][sl] = (float)litc[g][cur.lit] * (1.f / 256.f);
         }
         bnm[g][sl] = (uint8_t)nm;
 #pragma unroll
@@ -170,12 +178,12 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
     const float base = ci + (float)kInsExtra[ic];
     if (ic != cached_ic) {
       cached_ic = ic;
-      cm0 = (float)kCopyExtra[cc0] + cmdc[combine_codes(ic, cc0, false)];
-      cm1 = (float)kCopyExtra[cc1] + cmdc[combine_codes(ic, cc1, false)];
-      int cmd = combine_codes(ic, cc0, true);
-      cml0 = (float)kCopyExtra[cc0] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-      cmd = combine_codes(ic, cc1, true);
-      cml1 = (float)kCopyExtra[cc1] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+#pragma unroll
+      for (int c = 0; c < kCache; c++) {
+        cmA[c] = (float)kCopyExtra[ccA[c]] + cmdc[combine_codes(ic, ccA[c], false)];
+        const int cmd = combine_codes(ic, ccA[c], true);
+        cmlA[c] = (float)kCopyExtra[ccA[c]] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
+      }
     }
     // forceful long copy (backward-references-hq.ts:518-533)
     uint32_t fl = 0, fd = 0;
@@ -208,7 +216,7 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
       i0 = i;
       continue;
     }
-    // relax every edge out of i: lane sl of chunk k takes length 16 k + sl, choosing the
+    // relax every edge out of i: lane sl of chunk k takes length kGL k + sl, choosing the
     // literal (length 1) or the shortest-distance match covering it
     uint32_t maxlen = 1;
 #pragma unroll
@@ -222,14 +230,16 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
         best = ci + litcost;
         bm = pack_node(ld, 0, ins_i + 1);
       } else if (l >= 4 && l <= maxlen) {
-        float cmx, cml;
-        if (k == 0) {
-          cmx = cm0;
-          cml = cml0;
-        } else if (k == 1) {
-          cmx = cm1;
-          cml = cml1;
-        } else {
+        float cmx = 0.f, cml = 0.f;
+        bool cached = false;
+#pragma unroll
+        for (int c = 0; c < kCache; c++)
+          if (k == (uint32_t)c) {
+            cmx = cmA[c];
+            cml = cmlA[c];
+            cached = true;
+          }
+        if (!cached) {
           const int cc = copy_code(l);
           const int cmd = combine_codes(ic, cc, true);
           cmx = (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
