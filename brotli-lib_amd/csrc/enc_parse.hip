@@ -18,10 +18,10 @@ namespace enc {
 // its own segment by one position, its 32 lanes relaxing 32 copy lengths at a time, so the
 // per-position bookkeeping is paid once per 2 positions.  (Measured on MI355X, 1 GiB of
 // text: 1 x 64 lanes 696 ms, 2 x 32 474 ms, 4 x 16 518 ms, 8 x 8 897 ms -- beyond two
-// groups the groups' divergent refills and long-match chunks cost more than they save.)  Everything a position needs (its
-// matches with their distance costs, its literal cost) is staged into LDS 16 positions at
-// a time from registers that were loaded one batch ahead, so the serial loop itself never
-// waits on global memory.
+// groups the groups' divergent refills and long-match chunks cost more than they save.)
+// Everything a position needs (its matches with their distance costs, its literal cost) is
+// staged into LDS kBatch positions at a time from registers that were loaded one batch
+// ahead, so the serial loop itself never waits on global memory.
 constexpr int kGL = 32;        // lanes per segment
 constexpr int kG = 64 / kGL;   // segments per wave
 constexpr int kBatch = kGL;    // positions staged per refill (one per lane)
