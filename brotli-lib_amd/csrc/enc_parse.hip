@@ -267,59 +267,96 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
   }
 }
 
-// ---------------------------------------------------------------- 4. backtrack, lane per segment
+// ---------------------------------------------------------------- 4. backtrack, wave per segment
 // computeShortestPathFromNodes / createCommandsFromPath (backward-references-hq.ts:384-406,
 // 610-673) without the distance ring: that is stitched per segment in enc_entropy.hip.
-__global__ void backtrack_kernel(const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {
-  int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nsegs) return;
+// The path is walked from the segment end in windows of 64 positions: one coalesced load
+// of the window's choices, a ballot of its copy nodes, then a scalar walk that skips each
+// literal run with a bit scan and each copy with its length.
+__global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice,
+                                                       RawCmd *raw) {
+  const int s = blockIdx.x;
+  const int lane = threadIdx.x;
   Seg &sg = segs[s];
   const Job &jb = jobs[sg.job];
   const uint64_t *c = choice + jb.pos_base;
   RawCmd *out = raw + sg.cmd_off;
-  // walk back, writing commands from the end of the slice downward
-  uint32_t cap = (sg.end - sg.start) / 2 + 2;
-  uint32_t w = cap;
-  uint32_t p = sg.end, lits = 0, tail = 0;
+  const uint32_t a = sg.start;
+  const uint32_t cap = (sg.end - a) / 2 + 2;
+  uint32_t w = cap;   // commands are written from the end of the slice downward
+  uint32_t cur = sg.end, lits = 0, tail = 0;
   bool seen_copy = false;
   uint32_t pend_len = 0, pend_dist = 0, last_dist = 0;
-  while (p > sg.start) {
-    uint64_t v = c[p];
+  while (cur > a) {
+    const uint32_t nvalid = min(64u, cur - a);
+    const uint32_t p = cur - lane;
+    uint64_t v = 0;
+    if ((uint32_t)lane < nvalid) v = c[p];
     uint32_t len = (uint32_t)v;
-    if (len > p - sg.start) len = 0;   // never taken; a literal is always a valid edge
-    if (len == 0) {
-      lits++;
-      p--;
-      continue;
+    if ((uint32_t)lane >= nvalid || len > p - a) len = 0;   // a literal is always a valid edge
+    const uint32_t dist = (uint32_t)(v >> 32);
+    const uint64_t copies = __ballot(len != 0);
+    uint32_t x = 0;
+    for (;;) {
+      const uint64_t rest = x < 64 ? (copies >> x) : 0ull;
+      const uint32_t y = rest ? x + (uint32_t)(__ffsll((unsigned long long)rest) - 1) : nvalid;
+      if (y >= nvalid) {   // literals to the window's end
+        lits += nvalid - x;
+        cur -= nvalid;
+        break;
+      }
+      lits += y - x;
+      const uint32_t L = __builtin_amdgcn_readlane(len, y);
+      const uint32_t D = __builtin_amdgcn_readlane(dist, y);
+      if (!seen_copy) {
+        tail = lits;
+        seen_copy = true;
+        last_dist = D;
+      } else {
+        w--;
+        if (lane == 0) {
+          out[w].ins = lits;
+          out[w].len = pend_len;
+          out[w].dist = pend_dist;
+        }
+      }
+      lits = 0;
+      pend_len = L;
+      pend_dist = D;
+      x = y + L;
+      if (x >= nvalid) {
+        cur -= x;
+        break;
+      }
     }
-    if (!seen_copy) {
-      tail = lits;
-      seen_copy = true;
-      last_dist = (uint32_t)(v >> 32);
-    } else {
-      w--;
-      out[w].ins = lits;
-      out[w].len = pend_len;
-      out[w].dist = pend_dist;
-    }
-    lits = 0;
-    pend_len = len;
-    pend_dist = (uint32_t)(v >> 32);
-    p -= len;
   }
   if (seen_copy) {
+    if (lane == 0) {
+      out[w - 1].ins = lits;
+      out[w - 1].len = pend_len;
+      out[w - 1].dist = pend_dist;
+    }
     w--;
-    out[w].ins = lits;
-    out[w].len = pend_len;
-    out[w].dist = pend_dist;
   } else {
     tail = lits;
   }
-  uint32_t n = cap - w;
-  for (uint32_t q = 0; q < n; q++) out[q] = out[w + q];
-  sg.ncmd = n;
-  sg.tail_lits = tail;
-  sg.last_dist = last_dist;
+  const uint32_t n = cap - w;
+  wave_sync();
+  // move the commands to the front of the slice; a chunk is read into registers before it
+  // is written, and a later chunk's source lies above every earlier chunk's destination
+  for (uint32_t q0 = 0; q0 < n; q0 += 64) {
+    RawCmd t;
+    const uint32_t q = q0 + lane;
+    if (q < n) t = out[w + q];
+    wave_sync();
+    if (q < n) out[q] = t;
+    wave_sync();
+  }
+  if (lane == 0) {
+    sg.ncmd = n;
+    sg.tail_lits = tail;
+    sg.last_dist = last_dist;
+  }
 }
 
 
@@ -329,7 +366,7 @@ void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, cons
                      choice);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {
-  hipLaunchKernelGGL(backtrack_kernel, dim3((nsegs + 63) / 64), dim3(64), 0, st, jobs, segs, nsegs, choice, raw);
+  hipLaunchKernelGGL(backtrack_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, nsegs, choice, raw);
 }
 
 }  // namespace enc
