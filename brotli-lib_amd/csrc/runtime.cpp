@@ -367,7 +367,10 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     int64_t est = mib_decoded_size(in, n);
     if (est > 0) out_size = est;
   }
-  if (max_out >= 0 && out_size >= 0 && out_size > max_out) return MIB_E_OUTPUT_LIMIT;
+  if (max_out >= 0 && out_size >= 0 && out_size > max_out) {
+    out->size = (size_t)out_size;   // the size that exceeded the limit (decode.ts:46-50)
+    return MIB_E_OUTPUT_LIMIT;
+  }
   int known = out_size > 0;
   uint64_t cap = known ? (uint64_t)out_size : std::max<uint64_t>(1 << 20, 4 * (uint64_t)n + 4096);
   uint8_t *d_in = nullptr, *d_out = nullptr, *d_dict = nullptr;
@@ -413,6 +416,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
       if (len) hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost);
       if (max_out >= 0 && (int64_t)len > max_out) {   // the header can lie about the size (decode.ts:57-62)
         mib_buf_free(out);
+        out->size = len;
         rc = MIB_E_OUTPUT_LIMIT;
       }
     }

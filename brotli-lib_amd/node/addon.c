@@ -1,0 +1,263 @@
+/*
+ * brotli_amd.node -- Node-API binding of the brotli_amd C ABI (include/brotli_amd.h).
+ *
+ * This is the native half of the drop-in for countertype/brotli-lib's public surface
+ * (package.json:7-23); index.js is the JavaScript half that keeps the reference's argument
+ * handling and error messages.  Every function is synchronous on the JS thread, like the
+ * reference's.  Result bytes are copied into a fresh Node Buffer and the library buffer
+ * is released at once (mib_buf_free).
+ */
+#include <node_api.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/brotli_amd.h"
+
+#define CHECK(env, call)                                   \
+  do {                                                     \
+    if ((call) != napi_ok) {                               \
+      napi_throw_error((env), NULL, "brotli_amd: N-API"); \
+      return NULL;                                         \
+    }                                                      \
+  } while (0)
+
+static int get_bytes(napi_env env, napi_value v, const uint8_t **p, size_t *n) {
+  bool is_typed = false, is_buf = false;
+  napi_is_typedarray(env, v, &is_typed);
+  if (is_typed) {
+    napi_typedarray_type t;
+    size_t len, off;
+    void *data;
+    napi_value ab;
+    if (napi_get_typedarray_info(env, v, &t, &len, &data, &ab, &off) != napi_ok) return -1;
+    size_t el = (t == napi_uint8_array || t == napi_int8_array || t == napi_uint8_clamped_array) ? 1 : 0;
+    if (!el) return -1;
+    *p = (const uint8_t *)data;
+    *n = len;
+    return 0;
+  }
+  napi_is_buffer(env, v, &is_buf);
+  if (is_buf) {
+    void *data;
+    if (napi_get_buffer_info(env, v, &data, n) != napi_ok) return -1;
+    *p = (const uint8_t *)data;
+    return 0;
+  }
+  return -1;
+}
+
+static napi_value throw_code(napi_env env, int code) {
+  napi_throw_error(env, NULL, mib_strerror(code));
+  return NULL;
+}
+
+static napi_value take(napi_env env, mib_buf *b) {
+  napi_value out;
+  void *dst;
+  if (napi_create_buffer_copy(env, b->size, b->size ? (const void *)b->data : (const void *)"", &dst, &out) != napi_ok) {
+    mib_buf_free(b);
+    napi_throw_error(env, NULL, "brotli_amd: out of host memory");
+    return NULL;
+  }
+  mib_buf_free(b);
+  return out;
+}
+
+static int get_int(napi_env env, napi_value v, int dflt) {
+  napi_valuetype t;
+  int32_t r;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_number) return dflt;
+  if (napi_get_value_int32(env, v, &r) != napi_ok) return dflt;
+  return r;
+}
+static int64_t get_i64(napi_env env, napi_value v, int64_t dflt) {
+  napi_valuetype t;
+  int64_t r;
+  if (napi_typeof(env, v, &t) != napi_ok || t != napi_number) return dflt;
+  if (napi_get_value_int64(env, v, &r) != napi_ok) return dflt;
+  return r;
+}
+
+/* encode(bytes, quality, lgwin, mode) -> Buffer */
+static napi_value js_encode(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  const uint8_t *p;
+  size_t n;
+  if (argc < 1 || get_bytes(env, argv[0], &p, &n)) {
+    napi_throw_type_error(env, NULL, "input must be a Uint8Array");
+    return NULL;
+  }
+  mib_enc_opts o;
+  mib_enc_opts_default(&o);
+  o.quality = get_int(env, argc > 1 ? argv[1] : NULL, o.quality);
+  o.lgwin = get_int(env, argc > 2 ? argv[2] : NULL, o.lgwin);
+  o.mode = get_int(env, argc > 3 ? argv[3] : NULL, o.mode);
+  mib_buf b = {0, 0};
+  int rc = mib_encode(p, n, &o, &b);
+  if (rc) return throw_code(env, rc);
+  return take(env, &b);
+}
+
+/* decode(bytes, maxOutputSize|-1, exactSize|-1, dictionary|null) -> Buffer
+ * throws Error("Brotli error code: N") or, for the size limit, an Error whose message
+ * index.js rewrites; err.size carries the offending size. */
+static napi_value js_decode(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  const uint8_t *p, *d = NULL;
+  size_t n, dn = 0;
+  if (argc < 1 || get_bytes(env, argv[0], &p, &n)) {
+    napi_throw_type_error(env, NULL, "input must be a Uint8Array");
+    return NULL;
+  }
+  int64_t max_out = argc > 1 ? get_i64(env, argv[1], -1) : -1;
+  int64_t exact = argc > 2 ? get_i64(env, argv[2], -1) : -1;
+  if (argc > 3 && get_bytes(env, argv[3], &d, &dn)) d = NULL;
+  mib_buf b = {0, 0};
+  int rc = mib_decode(p, n, d, d ? dn : 0, max_out, exact, &b);
+  if (rc == MIB_E_OUTPUT_LIMIT) {
+    napi_value err, msg, sz;
+    napi_create_string_utf8(env, "Decompressed size exceeds limit", NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_create_int64(env, (int64_t)b.size, &sz);
+    napi_set_named_property(env, err, "size", sz);
+    napi_throw(env, err);
+    return NULL;
+  }
+  if (rc) return throw_code(env, rc);
+  return take(env, &b);
+}
+
+static napi_value js_decoded_size(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1], out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  const uint8_t *p;
+  size_t n;
+  if (argc < 1 || get_bytes(env, argv[0], &p, &n)) {
+    napi_throw_type_error(env, NULL, "input must be a Uint8Array");
+    return NULL;
+  }
+  CHECK(env, napi_create_int64(env, mib_decoded_size(p, n), &out));
+  return out;
+}
+
+static void encoder_finalize(napi_env env, void *data, void *hint) {
+  (void)env;
+  (void)hint;
+  mib_encoder_free((mib_encoder *)data);
+}
+
+/* encoderNew(quality, lgwin, mode) -> external handle */
+static napi_value js_encoder_new(napi_env env, napi_callback_info info) {
+  size_t argc = 3;
+  napi_value argv[3], out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  mib_enc_opts o;
+  mib_enc_opts_default(&o);
+  o.quality = get_int(env, argc > 0 ? argv[0] : NULL, o.quality);
+  o.lgwin = get_int(env, argc > 1 ? argv[1] : NULL, o.lgwin);
+  o.mode = get_int(env, argc > 2 ? argv[2] : NULL, o.mode);
+  mib_encoder *e = mib_encoder_new(&o);
+  if (!e) return throw_code(env, MIB_E_OUT_OF_MEMORY);
+  CHECK(env, napi_create_external(env, e, encoder_finalize, NULL, &out));
+  return out;
+}
+
+static napi_value js_encoder_update(napi_env env, napi_callback_info info) {
+  size_t argc = 2;
+  napi_value argv[2];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void *h;
+  const uint8_t *p;
+  size_t n;
+  if (argc < 2 || napi_get_value_external(env, argv[0], &h) != napi_ok || get_bytes(env, argv[1], &p, &n)) {
+    napi_throw_type_error(env, NULL, "update(chunk: Uint8Array)");
+    return NULL;
+  }
+  mib_buf b = {0, 0};
+  int rc = mib_encoder_update((mib_encoder *)h, p, n, &b);
+  if (rc) return throw_code(env, rc);
+  return take(env, &b);
+}
+
+static napi_value js_encoder_finish(napi_env env, napi_callback_info info) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  void *h;
+  if (argc < 1 || napi_get_value_external(env, argv[0], &h) != napi_ok) {
+    napi_throw_type_error(env, NULL, "finish()");
+    return NULL;
+  }
+  mib_buf b = {0, 0};
+  int rc = mib_encoder_finish((mib_encoder *)h, &b);
+  if (rc) return throw_code(env, rc);
+  return take(env, &b);
+}
+
+/* encodeBatch([bytes...], quality, lgwin, mode) -> [Buffer...]: one GPU launch sequence */
+static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
+  size_t argc = 4;
+  napi_value argv[4], out;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  uint32_t k = 0;
+  bool is_arr = false;
+  if (argc < 1 || napi_is_array(env, argv[0], &is_arr) != napi_ok || !is_arr) {
+    napi_throw_type_error(env, NULL, "encodeBatch(inputs: Uint8Array[])");
+    return NULL;
+  }
+  CHECK(env, napi_get_array_length(env, argv[0], &k));
+  mib_enc_opts o;
+  mib_enc_opts_default(&o);
+  o.quality = get_int(env, argc > 1 ? argv[1] : NULL, o.quality);
+  o.lgwin = get_int(env, argc > 2 ? argv[2] : NULL, o.lgwin);
+  o.mode = get_int(env, argc > 3 ? argv[3] : NULL, o.mode);
+  mib_span *in = (mib_span *)calloc(k ? k : 1, sizeof(mib_span));
+  mib_buf *res = (mib_buf *)calloc(k ? k : 1, sizeof(mib_buf));
+  int *st = (int *)calloc(k ? k : 1, sizeof(int));
+  for (uint32_t i = 0; i < k; i++) {
+    napi_value e;
+    napi_get_element(env, argv[0], i, &e);
+    if (get_bytes(env, e, &in[i].data, &in[i].size)) {
+      free(in), free(res), free(st);
+      napi_throw_type_error(env, NULL, "encodeBatch: every input must be a Uint8Array");
+      return NULL;
+    }
+  }
+  int rc = mib_encode_batch(in, k, &o, res, st);
+  free(in);
+  if (rc) {
+    free(res), free(st);
+    return throw_code(env, rc);
+  }
+  napi_create_array_with_length(env, k, &out);
+  for (uint32_t i = 0; i < k; i++) {
+    napi_value v = take(env, &res[i]);
+    if (!v) break;
+    napi_set_element(env, out, i, v);
+  }
+  free(res);
+  free(st);
+  return out;
+}
+
+static napi_value init(napi_env env, napi_value exports) {
+  napi_property_descriptor props[] = {
+      {"encode", 0, js_encode, 0, 0, 0, napi_default, 0},
+      {"decode", 0, js_decode, 0, 0, 0, napi_default, 0},
+      {"decodedSize", 0, js_decoded_size, 0, 0, 0, napi_default, 0},
+      {"encoderNew", 0, js_encoder_new, 0, 0, 0, napi_default, 0},
+      {"encoderUpdate", 0, js_encoder_update, 0, 0, 0, napi_default, 0},
+      {"encoderFinish", 0, js_encoder_finish, 0, 0, 0, napi_default, 0},
+      {"encodeBatch", 0, js_encode_batch, 0, 0, 0, napi_default, 0},
+  };
+  napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
+  return exports;
+}
+
+NAPI_MODULE(NODE_GYP_MODULE_NAME, init)

@@ -1,0 +1,79 @@
+'use strict'
+// brotli_amd for Node: the public surface of countertype/brotli-lib (package.json:7-23)
+// over the MI355X engine.  Argument handling and error messages follow the reference:
+//   brotliEncode(input, {quality, lgwin, mode, sizeHint})    src/encode/encode.ts:50-90
+//   new BrotliEncoder(options).update(chunk) / .finish()     src/encode/encode.ts:290-409
+//   brotliDecode(data, {maxOutputSize, customDictionary} | outputSize)
+//                                                            src/decode/decode.ts:18-65
+//   brotliDecodedSize(data)                                  src/decode/decode.ts:9-11
+//   EncoderMode                                              src/encode/enc-constants.ts:56-60
+// The addon (brotli_amd.node) is built by __graft_entry__.build(); there is no JavaScript
+// fallback, a missing GPU throws.
+const path = require('path')
+const native = require(path.join(__dirname, 'brotli_amd.node'))
+
+const EncoderMode = Object.freeze({ GENERIC: 0, TEXT: 1, FONT: 2 })
+
+function clampOptions(options) {
+  const o = options || {}
+  let quality = 11
+  let lgwin = 22
+  let mode = EncoderMode.GENERIC
+  if (o.quality !== undefined) quality = Math.max(0, Math.min(11, o.quality))
+  if (o.lgwin !== undefined) lgwin = Math.max(10, Math.min(24, o.lgwin))
+  if (o.mode !== undefined) mode = o.mode
+  return [quality | 0, lgwin | 0, mode | 0]
+}
+
+function toU8(b) {
+  return new Uint8Array(b.buffer, b.byteOffset, b.byteLength)
+}
+
+function brotliEncode(input, options) {
+  const [q, lg, m] = clampOptions(options)
+  return toU8(native.encode(input, q, lg, m))
+}
+
+class BrotliEncoder {
+  constructor(options) {
+    const [q, lg, m] = clampOptions(options)
+    this._h = native.encoderNew(q, lg, m)
+  }
+  update(input) {
+    return toU8(native.encoderUpdate(this._h, input))
+  }
+  finish() {
+    return toU8(native.encoderFinish(this._h))
+  }
+}
+
+function brotliDecodedSize(buffer) {
+  return native.decodedSize(buffer)
+}
+
+function brotliDecode(buffer, options) {
+  let exact = -1
+  let maxOutputSize
+  let dict = null
+  if (typeof options === 'number') {
+    exact = options
+  } else if (options) {
+    maxOutputSize = options.maxOutputSize
+    const d = options.customDictionary
+    if (d) dict = d instanceof Uint8Array ? d : new Uint8Array(d.buffer, d.byteOffset, d.byteLength)
+  }
+  try {
+    return toU8(native.decode(buffer, maxOutputSize === undefined ? -1 : maxOutputSize, exact, dict))
+  } catch (e) {
+    if (e && e.size !== undefined) throw new Error(`Decompressed size ${e.size} exceeds limit ${maxOutputSize}`)
+    throw e
+  }
+}
+
+// batch entry point of this engine: independent buffers in one GPU launch sequence
+function brotliEncodeBatch(inputs, options) {
+  const [q, lg, m] = clampOptions(options)
+  return native.encodeBatch(inputs, q, lg, m).map(toU8)
+}
+
+module.exports = { brotliEncode, BrotliEncoder, brotliDecode, brotliDecodedSize, EncoderMode, brotliEncodeBatch }

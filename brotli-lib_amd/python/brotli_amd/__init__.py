@@ -194,8 +194,7 @@ def brotliDecode(buffer, options=None):
     buf = _Buf()
     rc = _L().mib_decode(data, len(data), dic, len(dic) if dic is not None else 0, max_out, exact, ctypes.byref(buf))
     if rc == -103:   # MIB_E_OUTPUT_LIMIT: the reference's wrapper message
-        size = exact if exact >= 0 else brotliDecodedSize(data)
-        raise BrotliError('Decompressed size %d exceeds limit %d' % (size, max_out), rc)
+        raise BrotliError('Decompressed size %d exceeds limit %d' % (buf.size, max_out), rc)
     if rc:
         raise _err(rc)
     return _take(buf)

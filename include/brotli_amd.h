@@ -63,7 +63,9 @@ int mib_encode(const uint8_t *in, size_t n, const mib_enc_opts *o, mib_buf *out)
 
 /* brotliDecode (decode.ts:18-65).  exact_out >= 0: the legacy numeric `outputSize`
  * signature (truncate / zero-pad to it); -1: none.  max_out: `maxOutputSize`, -1 = none.
- * dict: `customDictionary` (compound-dictionary semantics, engine.ts:142-159), may be NULL. */
+ * dict: `customDictionary` (compound-dictionary semantics, engine.ts:142-159), may be NULL.
+ * On MIB_E_OUTPUT_LIMIT no data is returned and out->size holds the size that exceeded
+ * the limit (the header's size before decoding, the decoded length after). */
 int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, int64_t max_out,
                int64_t exact_out, mib_buf *out);
 

@@ -1,0 +1,107 @@
+'use strict'
+// Node-API drop-in check (runs on the GPU box through tests/test_gpu_node.py): the
+// brotli-lib surface exported by brotli-lib_amd/node/index.js against the committed
+// fixtures -- canonical vectors, the reference decoder's error corpus (exact messages),
+// option semantics, streaming, batch.  Prints one line per group and exits non-zero on
+// the first mismatch.
+const fs = require('fs')
+const path = require('path')
+const assert = require('assert')
+const root = path.join(__dirname, '..', '..')
+const lib = require(path.join(root, 'brotli-lib_amd', 'node', 'index.js'))
+const G = path.join(root, 'tests', 'golden')
+
+function eq(a, b, what) {
+  assert.strictEqual(Buffer.compare(Buffer.from(a), Buffer.from(b)), 0, what)
+}
+
+// canonical vectors decode bit-exactly
+let n = 0
+for (const name of fs.readdirSync(path.join(G, 'vectors')).sort()) {
+  if (!name.includes('.compressed')) continue
+  const comp = fs.readFileSync(path.join(G, 'vectors', name))
+  const exp = fs.readFileSync(path.join(G, 'vectors', name.split('.compressed')[0]))
+  eq(lib.brotliDecode(new Uint8Array(comp)), exp, name)
+  n++
+}
+console.log('vectors', n)
+
+// the reference decoder's error corpus: same outcome, same message (or the same bytes)
+const errs = JSON.parse(fs.readFileSync(path.join(G, 'decode_errors.json'))).cases
+const crypto = require('crypto')
+let ok = 0
+for (const c of errs) {
+  if (c.hang) continue
+  const input = new Uint8Array(Buffer.from(c.in_b64, 'base64'))
+  let got
+  try {
+    got = crypto.createHash('sha256').update(lib.brotliDecode(input)).digest('hex')
+  } catch (e) {
+    got = e.message
+  }
+  if (c.error !== undefined) {
+    if (!c.error.startsWith('Brotli error code')) continue   // JS engine errors (RangeError ...)
+    assert.strictEqual(got, c.error, c.in_b64.slice(0, 40))
+  } else {
+    assert.strictEqual(got, c.sha256, c.in_b64.slice(0, 40))
+  }
+  ok++
+}
+console.log('error corpus', ok)
+
+// round trips, options, modes
+const text = fs.readFileSync(path.join(G, 'vectors', 'alice29.txt'))
+for (const q of [0, 1, 5, 9, 10, 11]) {
+  for (const lgwin of [10, 16, 22, 24]) {
+    const enc = lib.brotliEncode(new Uint8Array(text), { quality: q, lgwin })
+    eq(lib.brotliDecode(enc), text, `q${q} lgwin${lgwin}`)
+  }
+}
+const font = fs.readFileSync(path.join(G, 'bench', 'enc-ttf.bin'))
+const encFont = lib.brotliEncode(new Uint8Array(font), { mode: lib.EncoderMode.FONT })
+eq(lib.brotliDecode(encFont), font, 'font')
+assert.strictEqual(lib.brotliDecodedSize(encFont), font.length)
+console.log('round trips ok, font', font.length, '->', encFont.length)
+
+// empty input: the reference's 1-byte-header stream, then decode
+const e0 = lib.brotliEncode(new Uint8Array(0))
+assert.deepStrictEqual(Array.from(e0), [0xa1, 0x01])
+assert.strictEqual(lib.brotliDecode(e0).length, 0)
+
+// legacy numeric output size: truncate / zero-pad
+const small = lib.brotliEncode(new Uint8Array(Buffer.from('hello hello hello hello')))
+assert.strictEqual(lib.brotliDecode(small, 5).length, 5)
+assert.strictEqual(lib.brotliDecode(small, 40).length, 40)
+
+// maxOutputSize message
+assert.throws(() => lib.brotliDecode(small, { maxOutputSize: 3 }), /^Error: Decompressed size 23 exceeds limit 3$/)
+
+// streaming: random chunking at every quality (brotli.test.ts:285-310 style)
+let seed = 0x12345678
+function next() {
+  seed ^= seed << 13; seed >>>= 0
+  seed ^= seed >>> 17
+  seed ^= seed << 5; seed >>>= 0
+  return seed
+}
+for (let q = 0; q <= 11; q++) {
+  const enc = new lib.BrotliEncoder({ quality: q })
+  const parts = []
+  let pos = 0
+  while (pos < text.length) {
+    const len = 1 + (next() % 4099)
+    parts.push(enc.update(new Uint8Array(text.subarray(pos, pos + len))))
+    pos += len
+  }
+  parts.push(enc.finish())
+  eq(lib.brotliDecode(new Uint8Array(Buffer.concat(parts.map((p) => Buffer.from(p))))), text, 'stream q' + q)
+}
+console.log('streaming ok')
+
+// batch
+const bufs = []
+for (let i = 0; i < 32; i++) bufs.push(new Uint8Array(text.subarray(i * 1000, i * 1000 + 5000 + i)))
+const outs = lib.brotliEncodeBatch(bufs, { quality: 11 })
+for (let i = 0; i < bufs.length; i++) eq(lib.brotliDecode(outs[i]), bufs[i], 'batch ' + i)
+console.log('batch ok')
+console.log('ALL OK')
