@@ -106,7 +106,7 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
     import brotli_amd
-    from brotli_amd import datagen
+    from brotli_amd import datagen, shard
 
     k, size = args.streams, args.size
     total = k * size
@@ -117,7 +117,6 @@ def main():
     dec = torch.empty(total + 64, dtype=torch.uint8, device=dev)
     ctx = brotli_amd.DeviceContext(local, profiling=True)
     opts = {'quality': args.quality, 'lgwin': args.lgwin}
-    gathered = None
 
     def step(times):
         out_off = ctx.encode(data.data_ptr(), in_off, comp.data_ptr(), cap, opts)
@@ -126,19 +125,9 @@ def main():
             t[0] += ms
             t[1] += n
         if world > 1 and not args.no_gather:
-            # RCCL gather of the variable-length compressed shards to rank 0
-            nbytes = torch.tensor([out_off[-1]], dtype=torch.int64, device=dev)
-            allsz = [torch.zeros_like(nbytes) for _ in range(world)]
-            dist.all_gather(allsz, nbytes)
-            mx = int(max(int(s) for s in allsz))
-            send = comp[:mx]
-            if rank == 0:
-                nonlocal gathered
-                if gathered is None or gathered.numel() < world * mx:
-                    gathered = torch.empty(world * mx, dtype=torch.uint8, device=dev)
-                dist.gather(send, [gathered[i * mx:(i + 1) * mx] for i in range(world)], dst=0)
-            else:
-                dist.gather(send, None, dst=0)
+            # the one collective: RCCL gather of the variable-length compressed shards to rank 0
+            lens = [out_off[i + 1] - out_off[i] for i in range(k)]
+            shard.gather_shards(comp[:out_off[-1]], lens, dst=0)
         sizes, status = ctx.decode(comp.data_ptr(), out_off, dec.data_ptr(), in_off)
         for name, (ms, n) in ctx.kernel_times().items():
             t = times.setdefault(name, [0.0, 0])
