@@ -170,7 +170,9 @@ def main():
         dec_ms = times.get('decode_streams_kernel', [0.0, 1])[0] / args.steps
         dom = max(times.items(), key=lambda kv: kv[1][0])
         dom_name, (dom_ms, dom_n) = dom[0], dom[1]
-        launch_bytes = total + comp_bytes   # every launch of every kernel covers the whole shard
+        # a kernel launched L times per step covers 1/L of the shard per launch
+        launches_per_step = max(1, dom_n // args.steps)
+        launch_bytes = (total + comp_bytes) // launches_per_step
         avg_ms = dom_ms / max(1, dom_n)
         achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
         res = {

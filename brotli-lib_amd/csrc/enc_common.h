@@ -12,6 +12,7 @@ namespace enc {
 constexpr uint32_t kSegBits = 16;
 constexpr uint32_t kSeg = 1u << kSegBits;     // 64 KiB parse segments
 constexpr int kMaxMatches = 6;                // staircase entries kept per position
+constexpr uint32_t kMatchLenSat = 255;        // a match is (length:8 | distance:24); 255 = "255 or more"
 constexpr int kRing = 256;                    // DP node window (> kLongCopy + staged batch)
 constexpr int kLongCopy = 200;                // copies longer than this are taken outright (the
                                               // reference's MAX_ZOPFLI_LEN is 325 at q11, 150 at q10,
@@ -139,6 +140,12 @@ __device__ __forceinline__ uint32_t dist_prefix(uint32_t dcode, int ndirect, int
   return (nbits << 10) | (16 + (uint32_t)ndirect + ((2 * (nbits - 1) + prefix) << npostfix) + postfix);
 }
 
+__device__ __forceinline__ uint32_t pack_match(uint32_t dist, uint32_t len) {
+  return (min(len, kMatchLenSat) << 24) | dist;   // distances are below 2^24 (lgwin <= 24)
+}
+__device__ __forceinline__ uint32_t match_dist(uint32_t m) { return m & 0xFFFFFFu; }
+__device__ __forceinline__ uint32_t match_length(uint32_t m) { return m >> 24; }
+
 __device__ __forceinline__ uint32_t load_u32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
@@ -206,10 +213,10 @@ __device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Cmd &c, 
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys,
                       uint32_t *vals);
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
-                         int depth, uint64_t *matches, uint8_t *nmatch);
+                         int depth, uint32_t *matches, uint8_t *nmatch);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
-               const uint64_t *matches, const uint8_t *nmatch, uint64_t *choice);
+               const uint32_t *matches, const uint8_t *nmatch, uint64_t *choice);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const RawCmd *raw, Cmd *cmds,

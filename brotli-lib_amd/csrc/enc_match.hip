@@ -43,7 +43,7 @@ __device__ __forceinline__ uint64_t load_prefix8(const uint8_t *p, uint32_t avai
 
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *sorted_keys,
                                                              const uint32_t *sorted_vals, uint32_t total, int depth,
-                                                             uint64_t *matches, uint8_t *nmatch) {
+                                                             uint32_t *matches, uint8_t *nmatch) {
   __shared__ uint32_t skey[kTile + kBack];
   __shared__ uint32_t spos[kTile + kBack];
   __shared__ uint64_t spre[kTile + kBack];
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     const uint8_t *cur = jb.data + p;
     const uint64_t mine = spre[me];
     uint32_t best = 3;
-    uint64_t local[kMaxMatches];
+    uint32_t local[kMaxMatches];
     const int dmax = min(depth, kBack);
     for (int t = 1; t <= dmax; t++) {
       const int e = me - t;
@@ -99,15 +99,14 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
         len = 8 + match_len(cur + 8, cand + 8, limit > 8 ? limit - 8 : 0);
         len = min(len, limit);
       }
-      len = min(len, 65535u);   // copy lengths travel as u16 through the parse
       if (len > best) {
         best = len;
         if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
           for (int q = 1; q < kMaxMatches; q++) local[q - 1] = local[q];
           cnt--;
         }
-        local[cnt++] = ((uint64_t)d << 32) | len;
-        if (len >= limit || len >= 4096) break;
+        local[cnt++] = pack_match(d, len);
+        if (len >= limit || len >= kMatchLenSat) break;   // the parse measures a long copy itself
       }
     }
     for (int q = 0; q < cnt; q++) matches[(uint64_t)g * kMaxMatches + q] = local[q];
@@ -135,7 +134,7 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, keys, vals);
 }
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
-                         int depth, uint64_t *matches, uint8_t *nmatch) {
+                         int depth, uint32_t *matches, uint8_t *nmatch) {
   hipLaunchKernelGGL(find_matches_kernel, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, skeys, svals, total,
                      depth, matches, nmatch);
 }

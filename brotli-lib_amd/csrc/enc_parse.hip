@@ -40,21 +40,21 @@ __device__ __forceinline__ uint64_t node_choice(uint64_t m) {   // (distance << 
 }
 
 struct Staged {   // one position's parse inputs, loaded ahead
-  uint64_t m[kMaxMatches];
+  uint32_t m[kMaxMatches];
   uint32_t nm;
   uint32_t lit;
 };
-__device__ __forceinline__ void load_staged(Staged &st, const uint64_t *matches, const uint8_t *nmatch, const uint8_t *data,
+__device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches, const uint8_t *nmatch, const uint8_t *data,
                                             uint32_t g, uint32_t p) {
   st.nm = nmatch[g];
   st.lit = data[p];
-  const uint64_t *src = matches + (uint64_t)g * kMaxMatches;
+  const uint32_t *src = matches + (uint64_t)g * kMaxMatches;
 #pragma unroll
   for (int q = 0; q < kMaxMatches; q++) st.m[q] = src[q];   // entries past nm are ignored
 }
 
 __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_histo,
-                                                const uint64_t *matches, const uint8_t *nmatch,
+                                                const uint32_t *matches, const uint8_t *nmatch,
                                                 uint64_t *choice /* per position+1 */) {
   // per-group rows are padded so the 4 groups' same-offset accesses fall in different banks
   __shared__ float cost[kG][kRing + 1];
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
   __shared__ float distc[128];
   __shared__ float blit[kG][kBatch + 1];
   __shared__ uint8_t bnm[kG][kBatch + 4];
-  __shared__ uint64_t bmt[kG][kBatch * kMaxMatches + 1];   // (distance << 32) | length
+  __shared__ uint32_t bmt[kG][kBatch * kMaxMatches + 1];   // pack_match(distance, length)
   __shared__ float bmc[kG][kBatch * kMaxMatches + 1];      // distance symbol cost + extra bits
   const int lane = threadIdx.x, g = lane / kGL, sl = lane % kGL;
   const int s = blockIdx.x * kG + g;
@@ -143,9 +143,9 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
 #pragma unroll
         for (int q = 0; q < kMaxMatches; q++) {
           if (q < nm) {
-            const uint64_t m = cur.m[q];
+            const uint32_t m = cur.m[q];
             uint32_t extra;
-            const uint32_t dp = dist_prefix((uint32_t)(m >> 32) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
+            const uint32_t dp = dist_prefix(match_dist(m) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
             bmt[g][sl * kMaxMatches + q] = m;
             bmc[g][sl * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
           }
@@ -167,9 +167,9 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
     float mc[kMaxMatches];
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
-      const uint64_t m = q < nm ? bmt[g][off * kMaxMatches + q] : 0ull;
-      md[q] = (uint32_t)(m >> 32);
-      mL[q] = min((uint32_t)m, limit);
+      const uint32_t m = q < nm ? bmt[g][off * kMaxMatches + q] : 0u;
+      md[q] = match_dist(m);
+      mL[q] = min(match_length(m), limit);
       mc[q] = q < nm ? bmc[g][off * kMaxMatches + q] : 0.f;
     }
     wave_sync();
@@ -198,6 +198,31 @@ __global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs
         const int cmd = combine_codes(ic, cc, last);
         fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (last ? (cmd < 128 ? 0.f : distc[0]) : mc[q]);
       }
+    }
+    if (fl == kMatchLenSat && limit > kMatchLenSat) {
+      // a saturated match: measure the copy (the group's lanes compare kGL bytes a step)
+      const uint8_t *cur = data + i, *src = data + i - fd;
+      const uint32_t cap = min(limit, 65535u);
+      for (;;) {
+        const uint32_t x = fl + sl;
+        const bool eq = x < cap && cur[x] == src[x];
+        const uint64_t ok = (__ballot(eq) >> (kGL * g)) & ((kGL == 64) ? ~0ull : ((1ull << kGL) - 1));
+        if (ok == ((kGL == 64) ? ~0ull : ((1ull << kGL) - 1))) {
+          fl += kGL;
+          continue;
+        }
+        fl += __ffsll((unsigned long long)~ok) - 1;
+        break;
+      }
+      fl = min(fl, cap);
+      const int cc = copy_code(fl);
+      const bool last = fd == ld;
+      const int cmd = combine_codes(ic, cc, last);
+      float dc = 0.f;
+#pragma unroll
+      for (int q = 0; q < kMaxMatches; q++)
+        if (q < nm && md[q] == fd) dc = mc[q];
+      fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (last ? (cmd < 128 ? 0.f : distc[0]) : dc);
     }
     if (fl) {
       // store the batch's finished nodes, abandon every pending node, resume at the copy's end
@@ -361,7 +386,7 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
 
 
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
-               const uint64_t *matches, const uint8_t *nmatch, uint64_t *choice) {
+               const uint32_t *matches, const uint8_t *nmatch, uint64_t *choice) {
   hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kG - 1) / kG), dim3(64), 0, st, jobs, segs, nsegs, lit_h, matches, nmatch,
                      choice);
 }

@@ -204,7 +204,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
                                         (uint32_t *)nullptr, (int)total, 0, 32, st));
   size_t need = 64 * 256;
   need += 4 * (size_t)total * 4 + sort_tmp;
-  need += (size_t)total * kMaxMatches * 8 + total;
+  need += (size_t)total * kMaxMatches * 4 + total;
   need += ((size_t)total + 1) * 8;
   need += cmd_total * (sizeof(RawCmd) + sizeof(Cmd) + 4);
   need += k * (sizeof(Job) + 1024 + 8) + ns1 * sizeof(Seg) + seg_job.size() * 4;
@@ -228,7 +228,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   uint32_t *keys = ar.take<uint32_t>(total), *vals = ar.take<uint32_t>(total);
   uint32_t *skeys = ar.take<uint32_t>(total), *svals = ar.take<uint32_t>(total);
   void *sort_ws = ar.take<uint8_t>(sort_tmp);
-  uint64_t *matches = ar.take<uint64_t>((size_t)total * kMaxMatches);
+  uint32_t *matches = ar.take<uint32_t>((size_t)total * kMaxMatches);
   uint8_t *nmatch = ar.take<uint8_t>(total);
   uint64_t *choice = ar.take<uint64_t>((size_t)total + 1);
   RawCmd *raw = ar.take<RawCmd>(cmd_total);
@@ -323,8 +323,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   return 0;
 }
 
-// workspace bytes per input byte are ~90: groups of at most this many positions
-constexpr uint64_t kGroupPositions = 1ull << 28;
+// workspace is ~65 bytes per position (keys 16, matches 25, choice 8, commands ~16): groups
+// of at most this many positions (~70 GB)
+constexpr uint64_t kGroupPositions = 1ull << 30;
 constexpr size_t kGroupStreams = 16384;   // job index must fit the 15-bit key field
 
 // Split k streams into groups and encode them back to back into d_out.
