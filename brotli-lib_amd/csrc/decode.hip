@@ -79,6 +79,8 @@ struct Dec {
   int rings[10], dist_rb_idx;
   int32_t *lit_group, *cmd_group, *dist_group;   // LDS when the metablock's codes fit, else HBM scratch
   int32_t *tab_lds, *tab_hbm;
+  uint8_t *ring_scratch;   // the block's HBM ring
+  int direct;              // ring == out: a single-metablock stream decodes in place
   uint8_t *ctx_modes, *ctx_map, *dist_ctx_map;   // HBM scratch
   int trivial_lit_ctx, lit_tree_idx, cmd_tree_idx;
   int j, insert_len, copy_len, dist_code, distance;
@@ -495,6 +497,15 @@ __device__ void lit_block_switch(Dec &s) {
   s.clo2 = s.clo1 + 256;
 }
 
+// back to the block's own ring: its content so far is the output's first ring_size bytes
+__device__ void leave_direct(Dec &s) {
+  const int n = s.ring_size + 37;
+  for (int k = s.lane; k < n; k += 64) s.ring_scratch[k] = k < s.out_cap ? s.out[k] : 0;
+  wave_sync();
+  s.ring = s.ring_scratch;
+  s.direct = 0;
+}
+
 __device__ void maybe_realloc_ring(Dec &s) {   // :608-630 (the scratch slice is max-sized; copy semantics kept)
   int new_size = s.max_ring;
   if (new_size > s.expected_total) {
@@ -503,6 +514,15 @@ __device__ void maybe_realloc_ring(Dec &s) {   // :608-630 (the scratch slice is
     if (!s.input_end && new_size < 16384 && s.max_ring >= 16384) new_size = 16384;
   }
   if (new_size <= s.ring_size) return;
+  // A stream announced as one final metablock whose ring fits the output buffer decodes
+  // straight into the output: the ring's bytes [0, pos) are then exactly the output's,
+  // so every flush is an identity and the ring -> output copy disappears.
+  if (s.ring_size == 0 && s.input_end && s.out_flushed == 0 && (int64_t)new_size + 37 + 64 <= s.out_cap) {
+    s.ring = s.out;
+    s.direct = 1;
+  } else if (s.direct && (int64_t)new_size + 37 + 64 > s.out_cap) {
+    leave_direct(s);
+  }
   // a fresh Uint8Array: bytes beyond the old size are zero
   for (int k = s.ring_size + s.lane; k < new_size + 37; k += 64) s.ring[k] = 0;
   wave_sync();
@@ -738,8 +758,10 @@ __device__ int write_ring(Dec &s) {
     if (s.out_flushed + n > s.out_cap) return MIB_E_NEED_SPACE;
     uint8_t *dst = s.out + s.out_flushed;
     const uint8_t *src = s.ring + s.rb_written;
-    for (int64_t k = s.lane; k < n; k += 64) dst[k] = src[k];
-    wave_sync();
+    if (dst != src) {   // (decoding in place: nothing to move)
+      for (int64_t k = s.lane; k < n; k += 64) dst[k] = src[k];
+      wave_sync();
+    }
     s.out_flushed += n;
     s.rb_written += (int)n;
   }
@@ -1277,6 +1299,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         if ((r = write_ring(s)) != 0) return r;
         if (s.pos >= s.max_back) s.max_dist = s.max_back;
         if (s.pos >= s.ring_size) {
+          if (s.direct && (s.next_running != ST_FINISHED || s.pos > s.ring_size)) leave_direct(s);
           if (s.pos > s.ring_size) {
             int extra = s.pos - s.ring_size;
             uint8_t v = 0;
@@ -1350,6 +1373,8 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     for (int i = 0; i < 10; i++) s.rings[i] = 0;
     s.rings[0] = 16; s.rings[1] = 15; s.rings[2] = 11; s.rings[3] = 4;
     s.dist_rb_idx = 3;
+    s.ring_scratch = ring;
+    s.direct = 0;
     s.tab_lds = ltab;
     s.tab_hbm = tables;
     s.lit_group = tables;

@@ -385,7 +385,12 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     if (dict_n) hipMemcpy(d_dict, dict, dict_n, hipMemcpyHostToDevice);
   }
   for (;;) {
-    if (hipMalloc(&d_out, cap + 64) != hipSuccess) {
+    // room for the ring of a one-metablock stream (a power of two >= its size, + slack), so
+    // the kernel can decode in place instead of through its scratch ring
+    uint64_t alloc = 1;
+    while (alloc < cap) alloc <<= 1;
+    alloc += 4096;
+    if (hipMalloc(&d_out, alloc) != hipSuccess) {
       rc = MIB_E_OUT_OF_MEMORY;
       break;
     }
@@ -395,7 +400,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     j.in = d_in;
     j.in_len = n;
     j.out = d_out;
-    j.out_cap = cap;
+    j.out_cap = known ? alloc : cap;   // unknown size: cap is the growth step's limit
     j.out_size = known ? out_size : -1;
     j.dict = d_dict;
     j.dict_len = dict ? dict_n : 0;
