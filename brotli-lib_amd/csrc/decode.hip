@@ -54,6 +54,11 @@ constexpr int kBlockTreesCap = 3091;   // engine.ts:163 Int32Array(3091)
 // LDS working set of one stream (one wave).
 constexpr int kLdsTableInts = 4096;   // 16 KiB of prefix-code tables in LDS (one tree per alphabet fits)
 
+typedef __attribute__((address_space(1))) uint8_t GU8;          // HBM
+typedef const __attribute__((address_space(1))) int32_t GI32;
+typedef const __attribute__((address_space(3))) uint8_t LU8;    // LDS
+typedef const __attribute__((address_space(3))) int32_t LI32;
+
 struct Lds {
   uint8_t win[4160 + 64];    // byteBuffer (4160) + read slack
   int lens[1080];            // code lengths scratch
@@ -938,12 +943,22 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         // The command / literal / copy loop runs on registers: the bit reader, positions,
         // lengths and block counters are loaded from `s` once, saved back around every
         // cold call (refill, block switch) and on every exit.
+        // Memory is addressed through address-space-typed pointers: LDS reads then wait only
+        // on LDS (lgkmcnt) and never on the outstanding HBM stores of the output, which a
+        // generic (flat) access would have to drain first.
         int phase = s.running;
-        uint8_t *ring = s.ring;
-        const uint8_t *win = s.l->win;
+        GU8 *ring = (GU8 *)s.ring;
+        LU8 *win = (LU8 *)s.l->win;
+        LI32 *ctb = (LI32 *)s.l->ctx_tree_base;
         const int ring_cap = s.ring_cap, npostfix = s.npostfix, ndirect = s.ndirect, max_back = s.max_back;
-        const int32_t *cmd_g = s.cmd_group, *dist_g = s.dist_group, *lit_g = s.lit_group;
+        const bool tab_lds = s.lit_group == s.tab_lds;
+        LI32 *cmd_l = (LI32 *)(tab_lds ? s.cmd_group : s.tab_lds), *dist_l = (LI32 *)(tab_lds ? s.dist_group : s.tab_lds),
+             *lit_l = (LI32 *)(tab_lds ? s.lit_group : s.tab_lds);
+        GI32 *cmd_h = (GI32 *)s.cmd_group, *dist_h = (GI32 *)s.dist_group, *lit_h = (GI32 *)s.lit_group;
         const int lane = s.lane;
+        const uint64_t guard_limit = s.guard_limit;
+        int trivial = s.trivial_lit_ctx, lit_tree = s.lit_tree_idx;
+        int dr0, dr1, dr2, dr3, dridx;   // the distance ring (rings[0..3], dist_rb_idx)
         uint32_t acc;
         int bo, ho, pos, j, mbl, insert_len, copy_len, dist_code, distance, cmd_blen, lit_blen, dist_blen, max_dist;
         uint64_t guard;
@@ -952,12 +967,15 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
     acc = s.acc; bo = s.bo; ho = s.ho; pos = s.pos; j = s.j; mbl = s.mbl; insert_len = s.insert_len;    \
     copy_len = s.copy_len; dist_code = s.dist_code; distance = s.distance; cmd_blen = s.cmd_blen;       \
     lit_blen = s.lit_blen; dist_blen = s.dist_blen; max_dist = s.max_dist; guard = s.guard;              \
+    dr0 = s.rings[0]; dr1 = s.rings[1]; dr2 = s.rings[2]; dr3 = s.rings[3]; dridx = s.dist_rb_idx;       \
+    trivial = s.trivial_lit_ctx; lit_tree = s.lit_tree_idx;                                              \
   } while (0)
 #define HOT_SAVE()                                                                                      \
   do {                                                                                                  \
     s.acc = acc; s.bo = bo; s.ho = ho; s.pos = pos; s.j = j; s.mbl = mbl; s.insert_len = insert_len;    \
     s.copy_len = copy_len; s.dist_code = dist_code; s.distance = distance; s.cmd_blen = cmd_blen;       \
     s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist; s.guard = guard;              \
+    s.rings[0] = dr0; s.rings[1] = dr1; s.rings[2] = dr2; s.rings[3] = dr3; s.dist_rb_idx = dridx;       \
   } while (0)
 #define LHALF(h) (((h) < 0 || (h) >= 2080) ? 0u : ((uint32_t)win[2 * (h)] | ((uint32_t)win[2 * (h) + 1] << 8)))
 #define LFILL16()                                     \
@@ -990,7 +1008,8 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
           bo -= 16;
           return lo | (lbits(n - 16) << 16);
         };
-        auto lsym = [&](const int32_t *g, int idx) -> int {   // read_symbol on registers
+        auto dr_get = [&](int i) -> int { return i == 0 ? dr0 : i == 1 ? dr1 : i == 2 ? dr2 : dr3; };
+        auto lsym = [&](auto g, int idx) -> int {   // read_symbol on registers
           int off = g[idx];
           uint32_t v = acc >> (bo & 31);
           off += (int)(v & 0xFF);
@@ -1010,7 +1029,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         uint32_t dtrees = 0;   // the 4 distance trees of the current distance block type
         for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
         for (;;) {
-          if (++guard > s.guard_limit) {
+          if (++guard > guard_limit) {
             HOT_SAVE();
             return MIB_E_NO_PROGRESS;
           }
@@ -1029,7 +1048,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
             }
             cmd_blen--;
             LFILL16();
-            const int sym = lsym(cmd_g, cmd_tree_idx);
+            const int sym = __builtin_amdgcn_readfirstlane(tab_lds ? lsym(cmd_l, cmd_tree_idx) : lsym(cmd_h, cmd_tree_idx));
             const int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
             dist_code = kCmdLut[4 * sym + 3];
             LFILL16();
@@ -1058,56 +1077,61 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               if (d <= 0 && batch <= 0 && a > 0 && b > 0 && c2 > 0) batch = 1;   // Bug J fix
               lit_blen -= batch;
               const int end = j + batch;
-              if (s.trivial_lit_ctx) {
-                const int root = lit_g[s.lit_tree_idx];
-                while (j < end) {
-                  LFILL16();
-                  const uint32_t v = acc >> (bo & 31);
-                  int off = root + (int)(v & 0xFF);
-                  const int e0 = lit_g[off];
-                  const int nb = e0 >> 16;
-                  int val;
-                  if (nb <= 8) {
-                    bo += nb;
-                    val = e0 & 0xFFFF;
-                  } else {
-                    off += e0 & 0xFFFF;
-                    off += (int)((v & ((1u << nb) - 1u)) >> 8);
-                    const int e1 = lit_g[off];
-                    bo += (e1 >> 16) + 8;
-                    val = e1 & 0xFFFF;
+              auto lit_run = [&](auto g) {
+                if (trivial) {
+                  const int root = g[lit_tree];
+                  while (j < end) {
+                    LFILL16();
+                    const uint32_t v = acc >> (bo & 31);
+                    int off = root + (int)(v & 0xFF);
+                    const int e0 = g[off];
+                    const int nb = e0 >> 16;
+                    int val;
+                    if (nb <= 8) {
+                      bo += nb;
+                      val = e0 & 0xFFFF;
+                    } else {
+                      off += e0 & 0xFFFF;
+                      off += (int)((v & ((1u << nb) - 1u)) >> 8);
+                      const int e1 = g[off];
+                      bo += (e1 >> 16) + 8;
+                      val = e1 & 0xFFFF;
+                    }
+                    if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)val;
+                    pos++;
+                    j++;
                   }
-                  if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)val;
-                  pos++;
-                  j++;
-                }
-              } else {
-                int p1 = ring[(pos - 1) & rmask], p2 = ring[(pos - 2) & rmask];
-                const int32_t *ctb = s.l->ctx_tree_base;
-                const int clo1 = s.clo1, clo2 = s.clo2;
-                while (j < end) {
-                  const int ctx = kRfcContextLut[clo1 + p1] | kRfcContextLut[clo2 + p2];
-                  p2 = p1;
-                  LFILL16();
-                  int off = ctb[ctx];
-                  const uint32_t v = acc >> (bo & 31);
-                  off += (int)(v & 0xFF);
-                  const int e0 = lit_g[off], nb = e0 >> 16;
-                  if (nb <= 8) {
-                    bo += nb;
-                    p1 = e0 & 0xFFFF;
-                  } else {
-                    off += e0 & 0xFFFF;
-                    off += (int)((v & ((1u << nb) - 1u)) >> 8);
-                    const int e1 = lit_g[off];
-                    bo += (e1 >> 16) + 8;
-                    p1 = e1 & 0xFFFF;
+                } else {
+                  int p1 = __builtin_amdgcn_readfirstlane(ring[(pos - 1) & rmask]);
+                  int p2 = __builtin_amdgcn_readfirstlane(ring[(pos - 2) & rmask]);
+                  const int clo1 = s.clo1, clo2 = s.clo2;
+                  while (j < end) {
+                    const int ctx = kRfcContextLut[clo1 + p1] | kRfcContextLut[clo2 + p2];
+                    p2 = p1;
+                    LFILL16();
+                    int off = ctb[ctx];
+                    const uint32_t v = acc >> (bo & 31);
+                    off += (int)(v & 0xFF);
+                    const int e0 = g[off], nb = e0 >> 16;
+                    if (nb <= 8) {
+                      bo += nb;
+                      p1 = e0 & 0xFFFF;
+                    } else {
+                      off += e0 & 0xFFFF;
+                      off += (int)((v & ((1u << nb) - 1u)) >> 8);
+                      const int e1 = g[off];
+                      bo += (e1 >> 16) + 8;
+                      p1 = e1 & 0xFFFF;
+                    }
+                    p1 = __builtin_amdgcn_readfirstlane(p1);
+                    if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)p1;
+                    pos++;
+                    j++;
                   }
-                  if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)p1;
-                  pos++;
-                  j++;
                 }
-              }
+              };
+              if (tab_lds) lit_run(lit_l);
+              else lit_run(lit_h);
               wave_sync();
               if (pos >= fence) {
                 s.next_running = ST_INSERT_LOOP;
@@ -1124,7 +1148,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
             }
             int dc = dist_code;
             if (dc < 0) {
-              distance = s.rings[s.dist_rb_idx];
+              distance = dr_get(dridx);
             } else {
               LREFILL();
               if (dist_blen == 0) {
@@ -1137,11 +1161,12 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               }
               dist_blen--;
               LFILL16();
-              dc = lsym(dist_g, (int)((dtrees >> (8 * dc)) & 0xFF));
+              const int dtree = (int)((dtrees >> (8 * dc)) & 0xFF);
+              dc = __builtin_amdgcn_readfirstlane(tab_lds ? lsym(dist_l, dtree) : lsym(dist_h, dtree));
               if (dc < 16) {
                 // short codes: ring slot and value offsets (kDistIdxOff / kDistValOff, packed)
-                const int idx = (s.dist_rb_idx + (int)((0xfff0006cu >> (2 * dc)) & 3)) & 3;
-                distance = s.rings[idx] + (int)((0xc298b0a626dbull >> (3 * dc)) & 7) - 3;
+                const int idx = (dridx + (int)((0xfff0006cu >> (2 * dc)) & 3)) & 3;
+                distance = dr_get(idx) + (int)((0xc298b0a626dbull >> (3 * dc)) & 7) - 3;
                 if (distance < 0) {
                   HOT_SAVE();
                   return ERR(s, -12);
@@ -1175,8 +1200,11 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               break;
             }
             if (dc > 0) {
-              s.dist_rb_idx = (s.dist_rb_idx + 1) & 3;
-              s.rings[s.dist_rb_idx] = distance;
+              dridx = (dridx + 1) & 3;
+              if (dridx == 0) dr0 = distance;
+              else if (dridx == 1) dr1 = distance;
+              else if (dridx == 2) dr2 = distance;
+              else dr3 = distance;
             }
             if (copy_len > mbl) {
               HOT_SAVE();
