@@ -106,6 +106,10 @@ struct Dec {
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
+#ifdef MIB_PROF   // timing experiment: cycles in command / literal / distance / copy, literal and command counts
+__device__ unsigned long long g_prof[6];
+#endif
+
 // A block is one wave: a wave's LDS and global accesses are performed in order, so the
 // lanes only need a compiler fence at wavefront scope between dependent steps.  (A
 // workgroup barrier would also wait for every outstanding ring store, once per command.)
@@ -962,13 +966,15 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         uint32_t acc;
         int bo, ho, pos, j, mbl, insert_len, copy_len, dist_code, distance, cmd_blen, lit_blen, dist_blen, max_dist;
         uint64_t guard;
+#define U(x) __builtin_amdgcn_readfirstlane(x)   /* the decoder state is wave-uniform: keep it scalar */
 #define HOT_LOAD()                                                                                      \
   do {                                                                                                  \
-    acc = s.acc; bo = s.bo; ho = s.ho; pos = s.pos; j = s.j; mbl = s.mbl; insert_len = s.insert_len;    \
-    copy_len = s.copy_len; dist_code = s.dist_code; distance = s.distance; cmd_blen = s.cmd_blen;       \
-    lit_blen = s.lit_blen; dist_blen = s.dist_blen; max_dist = s.max_dist; guard = s.guard;              \
-    dr0 = s.rings[0]; dr1 = s.rings[1]; dr2 = s.rings[2]; dr3 = s.rings[3]; dridx = s.dist_rb_idx;       \
-    trivial = s.trivial_lit_ctx; lit_tree = s.lit_tree_idx;                                              \
+    acc = U(s.acc); bo = U(s.bo); ho = U(s.ho); pos = U(s.pos); j = U(s.j); mbl = U(s.mbl);             \
+    insert_len = U(s.insert_len); copy_len = U(s.copy_len); dist_code = U(s.dist_code);                 \
+    distance = U(s.distance); cmd_blen = U(s.cmd_blen); lit_blen = U(s.lit_blen);                       \
+    dist_blen = U(s.dist_blen); max_dist = U(s.max_dist); guard = s.guard;                              \
+    dr0 = U(s.rings[0]); dr1 = U(s.rings[1]); dr2 = U(s.rings[2]); dr3 = U(s.rings[3]);                 \
+    dridx = U(s.dist_rb_idx); trivial = U(s.trivial_lit_ctx); lit_tree = U(s.lit_tree_idx);             \
   } while (0)
 #define HOT_SAVE()                                                                                      \
   do {                                                                                                  \
@@ -977,7 +983,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
     s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist; s.guard = guard;              \
     s.rings[0] = dr0; s.rings[1] = dr1; s.rings[2] = dr2; s.rings[3] = dr3; s.dist_rb_idx = dridx;       \
   } while (0)
-#define LHALF(h) (((h) < 0 || (h) >= 2080) ? 0u : ((uint32_t)win[2 * (h)] | ((uint32_t)win[2 * (h) + 1] << 8)))
+#define LHALF(h) (((h) < 0 || (h) >= 2080) ? 0u : (uint32_t)U((int)((uint32_t)win[2 * (h)] | ((uint32_t)win[2 * (h) + 1] << 8))))
 #define LFILL16()                                     \
   do {                                                \
     if (bo >= 16) {                                   \
@@ -1010,10 +1016,10 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         };
         auto dr_get = [&](int i) -> int { return i == 0 ? dr0 : i == 1 ? dr1 : i == 2 ? dr2 : dr3; };
         auto lsym = [&](auto g, int idx) -> int {   // read_symbol on registers
-          int off = g[idx];
+          int off = U(g[idx]);
           uint32_t v = acc >> (bo & 31);
           off += (int)(v & 0xFF);
-          int e0 = g[off];
+          int e0 = U(g[off]);
           int nb = e0 >> 16;
           if (nb <= 8) {
             bo += nb;
@@ -1021,13 +1027,26 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
           }
           off += e0 & 0xFFFF;
           off += (int)((v & ((1u << nb) - 1u)) >> 8);
-          int e1 = g[off];
+          int e1 = U(g[off]);
           bo += (e1 >> 16) + 8;
           return e1 & 0xFFFF;
         };
-        int cmd_tree_idx = s.cmd_tree_idx;
+        int cmd_tree_idx = __builtin_amdgcn_readfirstlane(s.cmd_tree_idx);
         uint32_t dtrees = 0;   // the 4 distance trees of the current distance block type
         for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
+        dtrees = U(dtrees);
+#ifdef MIB_PROF
+        uint64_t prof[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#define PMARK(slot)                                      \
+  do {                                                   \
+    uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+    prof[slot] += t_ - pt0;                              \
+    pt0 = t_;                                            \
+  } while (0)
+#else
+#define PMARK(slot) do {} while (0)
+#endif
         for (;;) {
           if (++guard > guard_limit) {
             HOT_SAVE();
@@ -1044,7 +1063,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               s.cmd_blen = decode_block_type_and_length(s, 1, s.n_cmd_types);
               s.cmd_tree_idx = s.rings[7];
               HOT_LOAD();
-              cmd_tree_idx = s.cmd_tree_idx;
+              cmd_tree_idx = U(s.cmd_tree_idx);
             }
             cmd_blen--;
             LFILL16();
@@ -1059,6 +1078,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
             copy_len = copy_off + (cb <= 16 ? lbits(cb) : lmany(cb));
             j = 0;
             phase = ST_INSERT_LOOP;
+            PMARK(0);
           }
           if (phase <= ST_INSERT_LOOP) {   // literals (:1154-1276)
             int stop = 0;
@@ -1079,12 +1099,15 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               const int end = j + batch;
               auto lit_run = [&](auto g) {
                 if (trivial) {
-                  const int root = g[lit_tree];
+                  const int root = U(g[lit_tree]);
                   while (j < end) {
+                    acc = (uint32_t)U((int)acc);
+                    bo = U(bo);
+                    ho = U(ho);
                     LFILL16();
                     const uint32_t v = acc >> (bo & 31);
                     int off = root + (int)(v & 0xFF);
-                    const int e0 = g[off];
+                    const int e0 = U(g[off]);
                     const int nb = e0 >> 16;
                     int val;
                     if (nb <= 8) {
@@ -1093,11 +1116,11 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                     } else {
                       off += e0 & 0xFFFF;
                       off += (int)((v & ((1u << nb) - 1u)) >> 8);
-                      const int e1 = g[off];
+                      const int e1 = U(g[off]);
                       bo += (e1 >> 16) + 8;
                       val = e1 & 0xFFFF;
                     }
-                    if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)val;
+                    if (pos < ring_cap) ring[pos] = (uint8_t)val;   // every lane: same byte, one transaction
                     pos++;
                     j++;
                   }
@@ -1109,22 +1132,22 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                     const int ctx = kRfcContextLut[clo1 + p1] | kRfcContextLut[clo2 + p2];
                     p2 = p1;
                     LFILL16();
-                    int off = ctb[ctx];
+                    int off = U(ctb[ctx]);
                     const uint32_t v = acc >> (bo & 31);
                     off += (int)(v & 0xFF);
-                    const int e0 = g[off], nb = e0 >> 16;
+                    const int e0 = U(g[off]), nb = e0 >> 16;
                     if (nb <= 8) {
                       bo += nb;
                       p1 = e0 & 0xFFFF;
                     } else {
                       off += e0 & 0xFFFF;
                       off += (int)((v & ((1u << nb) - 1u)) >> 8);
-                      const int e1 = g[off];
+                      const int e1 = U(g[off]);
                       bo += (e1 >> 16) + 8;
                       p1 = e1 & 0xFFFF;
                     }
                     p1 = __builtin_amdgcn_readfirstlane(p1);
-                    if (lane == 0 && pos < ring_cap) ring[pos] = (uint8_t)p1;
+                    if (pos < ring_cap) ring[pos] = (uint8_t)p1;
                     pos++;
                     j++;
                   }
@@ -1141,6 +1164,10 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               }
             }
             if (stop) break;
+            PMARK(1);
+#ifdef MIB_PROF
+            prof[4] += insert_len;
+#endif
             mbl -= insert_len;   // distance (:1277-1377)
             if (mbl <= 0) {
               s.running = ST_BLOCK_START;
@@ -1158,6 +1185,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                 HOT_LOAD();
                 dtrees = 0;
                 for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
+                dtrees = U(dtrees);
               }
               dist_blen--;
               LFILL16();
@@ -1212,6 +1240,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
             }
             j = 0;
             phase = ST_COPY_LOOP;
+            PMARK(2);
           }
           {   // copy (:1379-1433)
             const int dist = distance, cl = copy_len - j;
@@ -1265,8 +1294,17 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               if (cut) break;
             }
             phase = ST_MAIN_LOOP;
+            PMARK(3);
+#ifdef MIB_PROF
+            prof[5]++;
+#endif
           }
         }
+#ifdef MIB_PROF
+        if (lane == 0)
+          for (int q = 0; q < 6; q++) atomicAdd(&g_prof[q], (unsigned long long)prof[q]);
+#endif
+#undef PMARK
         HOT_SAVE();
         s.cmd_tree_idx = cmd_tree_idx;
 #undef HOT_LOAD
@@ -1274,6 +1312,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
 #undef LHALF
 #undef LFILL16
 #undef LREFILL
+#undef U
         continue;
       }
       case ST_USE_DICTIONARY:
@@ -1489,3 +1528,12 @@ extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t 
   hipLaunchKernelGGL(mib::peek_heads_kernel, dim3((k + 255) / 256), dim3(256), 0, stream, d_in, d_offsets, k, d_heads);
   return hipGetLastError();
 }
+
+#ifdef MIB_PROF
+extern "C" int mib_debug_read_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_prof), sizeof(unsigned long long) * 6);
+  unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(mib::g_prof), z, sizeof(z));
+  return 0;
+}
+#endif

@@ -242,9 +242,9 @@ class DeviceContext:
         _L().mib_ctx_set_profiling(self._c, 1 if profiling else 0)
 
     def close(self):
-        if self._c:
-            _L().mib_ctx_free(self._c)
-            self._c = None
+        if getattr(self, '_c', None) and _lib is not None:
+            _lib.mib_ctx_free(self._c)
+        self._c = None
 
     def __del__(self):
         self.close()

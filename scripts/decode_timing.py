@@ -19,7 +19,15 @@ comp = torch.empty(cap, dtype=torch.uint8, device=dev)
 off = ctx.encode(data.data_ptr(), [i * size for i in range(k + 1)], comp.data_ptr(), cap, {'quality': 11})
 slot = size + 4096
 dec = torch.empty(k * slot, dtype=torch.uint8, device=dev)
+import ctypes  # noqa: E402
+lib = brotli_amd._L()
+prof = (ctypes.c_ulonglong * 6)()
+has_prof = hasattr(lib, 'mib_debug_read_prof')
 for it in range(3):
     sizes, st = ctx.decode(comp.data_ptr(), off, dec.data_ptr(), [i * slot for i in range(k + 1)])
     print(it, ctx.kernel_times(), 'ok' if torch.equal(dec.view(k, slot)[:, :size], data.view(k, size)) else 'MISMATCH',
           flush=True)
+    if has_prof:
+        lib.mib_debug_read_prof(prof)
+        names = ['cmd', 'literals', 'distance', 'copy', 'n_literals', 'n_commands']
+        print({n: v / k for n, v in zip(names, prof)}, flush=True)
