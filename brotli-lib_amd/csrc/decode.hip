@@ -65,6 +65,7 @@ struct Lds {
   uint16_t sorted[1080];
   int32_t cl_table[33];
   int32_t ctx_tree_base[64];
+  uint8_t ctx_lut[512];        // the current literal context mode's slice of the RFC lookup table
   uint8_t mtf[256];
   int32_t block_trees[kBlockTreesCap + 1];
 };
@@ -494,6 +495,7 @@ __device__ int decode_block_type_and_length(Dec &s, int tree_type, int ntypes) {
 }
 __device__ void build_ctx_tree_base(Dec &s) {
   if (s.lane < 64) s.l->ctx_tree_base[s.lane] = s.lit_group[s.ctx_map[s.ctx_map_slice + s.lane]];
+  for (int k = s.lane; k < 512; k += 64) s.l->ctx_lut[k] = kRfcContextLut[s.clo1 + k];
   wave_sync();
 }
 __device__ void lit_block_switch(Dec &s) {
@@ -1127,9 +1129,9 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                 } else {
                   int p1 = __builtin_amdgcn_readfirstlane(ring[(pos - 1) & rmask]);
                   int p2 = __builtin_amdgcn_readfirstlane(ring[(pos - 2) & rmask]);
-                  const int clo1 = s.clo1, clo2 = s.clo2;
+                  LU8 *clut = (LU8 *)s.l->ctx_lut;
                   while (j < end) {
-                    const int ctx = kRfcContextLut[clo1 + p1] | kRfcContextLut[clo2 + p2];
+                    const int ctx = U((int)(clut[p1] | clut[256 + p2]));
                     p2 = p1;
                     LFILL16();
                     int off = U(ctb[ctx]);

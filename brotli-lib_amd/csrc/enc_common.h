@@ -6,6 +6,11 @@
 
 #include "common.h"
 
+#ifndef RFC_CONST
+#define RFC_CONST static __device__ const
+#endif
+#include "rfc_tables.h"
+
 namespace mib {
 namespace enc {
 
@@ -19,8 +24,12 @@ constexpr int kLongCopy = 200;                // copies longer than this are tak
                                               // enc-constants.ts:32-33)
 constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
 constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
-constexpr int kHdrBytes = 64;                 // metablock header (without trees)
+constexpr int kHdrBytes = 512;                // metablock header + context maps (without the trees)
 constexpr int kTreeBytes = 1024;              // one serialised prefix code
+constexpr int kLitCtx = 64;                   // literal contexts (RFC 7932 section 7.1)
+constexpr int kDistCtx = 4;                   // distance contexts (copy length 2, 3, 4, >4)
+constexpr int kTreeSlots = kLitCtx + 1 + kDistCtx;   // literal clusters | command | distance clusters
+constexpr int kCmdSlot = kLitCtx;
 constexpr int kBlock = 256;                   // threads of the per-segment entropy / emit blocks
 
 struct Job {                // one stream (or streaming chunk) to encode
@@ -37,6 +46,7 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint32_t hdr_lgwin;       // window bits written before the first metablock, 0 = none
   uint32_t final_;          // last chunk of the stream: ISLAST metablock (else a byte-aligning flush)
   int32_t dc_in[4];         // the decoder's distance ring at the start (streaming continues it)
+  uint32_t prev_bytes;      // the two bytes before data[0] (streaming: the previous chunk's tail), p1 | p2 << 8
   int32_t dc_out[4];        // and after the last command
   uint64_t out_off;         // byte offset of its scratch output slice
   uint64_t out_cap;
@@ -58,13 +68,17 @@ struct Seg {
   uint64_t bits;              // sizes
 };
 
-struct Mb {                   // one metablock (storeMetaBlockTrivial layout, metablock.ts:290-389)
+struct Mb {                   // one metablock: one block type per category, literal and
+                              // distance context modelling (storeMetaBlock, metablock.ts:504-761)
   uint32_t job, start, end;   // stream-local
   uint32_t first_seg, nseg;
   uint32_t is_last;
-  uint32_t hdr_bits;          // header bits before the prefix codes
-  uint32_t tree_bits[3];      // literal, command, distance code
-  uint32_t pad;
+  uint32_t hdr_bits;          // header bits before the prefix codes (incl. context maps)
+  uint32_t ctx_mode;          // literal context mode (chooseContextMode, context.ts:180-227)
+  uint32_t nlit, ndist;       // literal / distance prefix codes (clusters)
+  uint8_t lit_cmap[kLitCtx];  // context -> literal code
+  uint8_t dist_cmap[kDistCtx];
+  uint32_t tree_bits[kTreeSlots];
   uint64_t bit_off;           // of the header, stream-relative
 };
 
@@ -77,13 +91,13 @@ struct Cmd {                  // one command with its prefix codes (command.ts:2
 
 struct RawCmd { uint32_t ins, len, dist; };
 
-struct Codes {   // per metablock Huffman codes
-  uint8_t ld[256];
-  uint16_t lc[256];
+struct Codes {   // per metablock Huffman codes, literal and distance ones per cluster
+  uint8_t ld[kLitCtx][256];
+  uint16_t lc[kLitCtx][256];
   uint8_t cd[704];
   uint16_t cc[704];
-  uint8_t dd[128];
-  uint16_t dcd[128];
+  uint8_t dd[kDistCtx][128];
+  uint16_t dcd[kDistCtx][128];
 };
 
 // ---------------------------------------------------------------- coding helpers (command.ts)
@@ -198,14 +212,31 @@ __device__ __forceinline__ void put_window_bits(BitW &w, int lg) {
   else w.put(7, (uint32_t)(((lg - 8) << 4) | 1));
 }
 
-// Bits of one command: prefix code, extra bits, literals, distance (storeCommandExtra /
-// BlockEncoder, metablock.ts:273-287,392-501).
-__device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Cmd &c, const uint8_t *lits) {
+// the two bytes before stream position p (p1 | p2 << 8): the decoder's ring holds them
+__device__ __forceinline__ uint32_t prev2(const Job &jb, uint32_t p) {
+  const uint32_t b1 = p >= 1 ? jb.data[p - 1] : (jb.prev_bytes & 0xFF);
+  const uint32_t b2 = p >= 2 ? jb.data[p - 2] : (p == 1 ? (jb.prev_bytes & 0xFF) : (jb.prev_bytes >> 8) & 0xFF);
+  return b1 | (b2 << 8);
+}
+// distance context of a copy (RFC 7932 section 7.2; metablock.ts:621)
+__device__ __forceinline__ int dist_ctx(uint32_t copy_len) { return copy_len > 4 ? 3 : (int)copy_len - 2; }
+
+// Bits of one command: prefix code, extra bits, literals under their contexts, distance
+// (storeCommandExtra / storeSymbolWithContext, metablock.ts:273-287,392-501,720-745).
+// lut = the context mode's 512-entry slice of the RFC context lookup table.
+__device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Mb &mb, const uint8_t *lut, const Cmd &c,
+                                                 const uint8_t *lits, uint32_t p12) {
   const int ic = ins_code(c.ins);
   const int cc = copy_code(c.copy ? c.copy : 2);
   uint32_t bits = cd.cd[c.cmd_prefix] + kInsExtra[ic] + kCopyExtra[cc];
-  for (uint32_t k = 0; k < c.ins; k++) bits += cd.ld[lits[k]];
-  if (c.copy && c.cmd_prefix >= 128) bits += cd.dd[c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
+  uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
+  for (uint32_t k = 0; k < c.ins; k++) {
+    const uint32_t lit = lits[k];
+    bits += cd.ld[mb.lit_cmap[lut[p1] | lut[256 + p2]]][lit];
+    p2 = p1;
+    p1 = lit;
+  }
+  if (c.copy && c.cmd_prefix >= 128) bits += cd.dd[mb.dist_cmap[dist_ctx(c.copy)]][c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
   return bits;
 }
 
@@ -219,13 +250,15 @@ void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, cons
                const uint32_t *matches, const uint8_t *nmatch, uint64_t *choice);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
-void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const RawCmd *raw, Cmd *cmds,
+void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd);
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds);
+void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs);
+void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd);
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr);
-void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Cmd *cmds, const uint32_t *cmd_pos,
-                  const Codes *codes);
+void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
+                  const uint32_t *cmd_pos, const Codes *codes);
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out);
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
                  const uint32_t *cmd_pos, const Codes *codes, const uint8_t *trees, const uint8_t *hdr, uint8_t *out);

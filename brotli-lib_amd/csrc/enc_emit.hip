@@ -46,7 +46,8 @@ struct Acc {   // lane-private bit accumulator writing 32-bit words; edge words 
 };
 
 
-// metablock header + its three prefix codes, lane per metablock
+// metablock header (with its context maps) + its prefix codes in stream order: literal
+// clusters, command code, distance clusters.  Lane per metablock.
 __global__ void headers_kernel(const Job *jobs, const Mb *mbs, int nmbs, const uint8_t *hdr, const uint8_t *trees,
                                uint8_t *out) {
   int m = blockIdx.x * blockDim.x + threadIdx.x;
@@ -56,9 +57,9 @@ __global__ void headers_kernel(const Job *jobs, const Mb *mbs, int nmbs, const u
   if (jb.uncompressed) return;
   Acc a;
   a.init(reinterpret_cast<uint32_t *>(out + jb.out_off), mb.bit_off);
-  for (int part = 0; part < 4; part++) {
-    const uint8_t *src = part == 0 ? hdr + (size_t)m * kHdrBytes : trees + ((size_t)m * 3 + part - 1) * kTreeBytes;
-    const uint64_t nbits = part == 0 ? mb.hdr_bits : mb.tree_bits[part - 1];
+  for (int part = -1; part < kTreeSlots; part++) {
+    const uint8_t *src = part < 0 ? hdr + (size_t)m * kHdrBytes : trees + ((size_t)m * kTreeSlots + part) * kTreeBytes;
+    const uint64_t nbits = part < 0 ? mb.hdr_bits : mb.tree_bits[part];
     uint64_t i = 0;
     for (; i + 8 <= nbits; i += 8) a.put(8, src[i >> 3]);
     if (i < nbits) a.put((int)(nbits - i), src[i >> 3]);
@@ -96,20 +97,26 @@ struct OrW {
 };
 
 template <class W>
-__device__ __forceinline__ void write_command(W &wr, const Codes &cd, const Cmd &k, const uint8_t *lits) {
+__device__ __forceinline__ void write_command(W &wr, const Codes &cd, const Mb &mb, const uint8_t *lut, const Cmd &k,
+                                              const uint8_t *lits, uint32_t p12) {
   wr.put(cd.cd[k.cmd_prefix], cd.cc[k.cmd_prefix]);
   const int ic = ins_code(k.ins);
   wr.put((int)kInsExtra[ic], k.ins - kInsBase[ic]);
   const uint32_t clen = k.copy ? k.copy : 2;
   const int cc = copy_code(clen);
   wr.put((int)kCopyExtra[cc], clen - kCopyBase[cc]);
+  uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
   for (uint32_t t = 0; t < k.ins; t++) {
-    const uint8_t lit = lits[t];
-    wr.put(cd.ld[lit], cd.lc[lit]);
+    const uint32_t lit = lits[t];
+    const int tree = mb.lit_cmap[lut[p1] | lut[256 + p2]];
+    wr.put(cd.ld[tree][lit], cd.lc[tree][lit]);
+    p2 = p1;
+    p1 = lit;
   }
   if (k.copy && k.cmd_prefix >= 128) {
     const uint32_t dcode = k.dist_prefix & 0x3FF;
-    wr.put(cd.dd[dcode], cd.dcd[dcode]);
+    const int tree = mb.dist_cmap[dist_ctx(k.copy)];
+    wr.put(cd.dd[tree][dcode], cd.dcd[tree][dcode]);
     wr.put(k.dist_prefix >> 10, k.dist_extra);
   }
 }
@@ -119,7 +126,7 @@ __device__ __forceinline__ void write_command(W &wr, const Codes &cd, const Cmd 
 // last word are ORed: neighbours share them).  A command that does not fit the window (an
 // insert of tens of thousands of literals) is ORed straight into global memory.
 constexpr int kWinWords = 8192;   // 32 KiB = 262144 bits
-__global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg *segs, const Cmd *cmds,
+__global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                       const uint32_t *cmd_pos, const Codes *codes, uint8_t *out) {
   typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
@@ -130,6 +137,8 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
   const Codes &cd = codes[sg.mb];
+  const Mb &mb = mbs[sg.mb];
+  const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
   uint32_t *words = reinterpret_cast<uint32_t *>(out + jb.out_off);
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
@@ -141,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
     uint32_t bits = 0;
     if (q < n) {
       k = c[q];
-      bits = command_bits(cd, k, jb.data + cp[q]);
+      bits = command_bits(cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]));
     }
     uint32_t off, total;
     Scan(scan_tmp).ExclusiveSum(bits, off, total);
@@ -156,13 +165,13 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
       if (fits) {
         OrW<false> wr;
         wr.init(win, rel0 + off);
-        write_command(wr, cd, k, jb.data + cp[q]);
+        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]));
         wr.finish();
         atomicMax(&sh_fit_end, rel0 + off + bits);
       } else {
         OrW<true> wr;
         wr.init(words, bitpos + off);
-        write_command(wr, cd, k, jb.data + cp[q]);
+        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]));
         wr.finish();
       }
     }
@@ -248,7 +257,7 @@ __global__ void pack_kernel(const Job *jobs, const uint64_t *dst_off, const uint
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
                  const uint32_t *cmd_pos, const Codes *codes, const uint8_t *trees, const uint8_t *hdr, uint8_t *out) {
   hipLaunchKernelGGL(headers_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, trees, out);
-  hipLaunchKernelGGL(emit_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, cmds, cmd_pos, codes, out);
+  hipLaunchKernelGGL(emit_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, out);
 }
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out) {
   hipLaunchKernelGGL(uncompressed_kernel, dim3((unsigned)njobs), dim3(256), 0, st, jobs, njobs, out);

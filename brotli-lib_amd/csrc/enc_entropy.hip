@@ -41,24 +41,65 @@ __global__ void carry_kernel(Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
   }
 }
 
+// ---------------------------------------------------------------- context mode per metablock
+// chooseContextMode (context.ts:180-227) on the metablock's first min(length, 4096) bytes:
+// up to 1024 samples classified as ASCII / UTF-8 lead / continuation, small-delta pairs.
+// Lane per metablock.  Values: 0 LSB6, 1 MSB6, 2 UTF8, 3 SIGNED (RFC 7932 section 7.1).
+__global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs) {
+  int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nmbs) return;
+  Mb &mb = mbs[m];
+  const Job &jb = jobs[mb.job];
+  if (jb.uncompressed) return;
+  const uint8_t *d = jb.data + mb.start;
+  const int length = (int)min(mb.end - mb.start, 4096u);
+  const int sample = length < 1024 ? length : 1024;
+  const int step = max(1, length / max(sample, 1));
+  int ascii = 0, lead = 0, cont = 0, signed_pat = 0;
+  for (int i = 0; i < length; i += step) {
+    const int byte = d[i];
+    if (byte < 128) {
+      ascii++;
+      if (i > 0) {
+        const int diff = abs(byte - (int)d[i - 1]);
+        if (diff < 16) signed_pat++;
+      }
+    } else if (byte >= 192) {
+      lead++;
+    } else {
+      cont++;
+    }
+  }
+  const int total = ascii + lead + cont;
+  int mode = 0;
+  if (total == 0) mode = 0;
+  else if (lead > 0 && (double)cont > lead * 0.5) mode = 2;
+  else if ((double)signed_pat > total * 0.3) mode = 3;
+  else if ((double)ascii > total * 0.7) mode = 2;
+  mb.ctx_mode = (uint32_t)mode;
+}
+
 // ---------------------------------------------------------------- codes + histograms
 // Block per segment: command prefix codes (getInsertLengthCode / getCopyLengthCode /
 // combineLengthCodes / prefixEncodeCopyDistance, command.ts:29-179), command positions
-// (block scan), and the metablock's literal / command / distance histograms (LDS, then one
-// global atomic per non-zero bin).
-__global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Seg *segs, const RawCmd *raw, Cmd *cmds,
-                                                       uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
+// (block scan), and the metablock's histograms: literals per context (64), commands,
+// distances per distance context (4) -- in LDS, then one global atomic per non-zero bin
+// (the histogram pass of storeMetaBlock, metablock.ts:580-640).
+__global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const RawCmd *raw,
+                                                       Cmd *cmds, uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc,
+                                                       uint32_t *hd) {
   typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
-  __shared__ uint32_t sh_l[256], sh_c[704], sh_d[128];
+  __shared__ uint32_t sh_l[kLitCtx * 256], sh_c[704], sh_d[kDistCtx * 128];
   __shared__ uint32_t sh_run;
   const Seg sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
+  const uint8_t *lut = kRfcContextLut + (mbs[sg.mb].ctx_mode << 9);
   const int t = threadIdx.x;
   for (int i = t; i < 704; i += kBlock) sh_c[i] = 0;
-  for (int i = t; i < 256; i += kBlock) sh_l[i] = 0;
-  if (t < 128) sh_d[t] = 0;
+  for (int i = t; i < kLitCtx * 256; i += kBlock) sh_l[i] = 0;
+  for (int i = t; i < kDistCtx * 128; i += kBlock) sh_d[i] = 0;
   if (t == 0) sh_run = sg.start - sg.carry_in;
   __syncthreads();
   const RawCmd *r = raw + sg.cmd_off;
@@ -97,23 +138,178 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
         c.dist_extra = extra;
         c.dist_prefix = (uint16_t)dp;
         c.cmd_prefix = (uint16_t)combine_codes(ic, copy_code(len), dcode == 0);
-        if (c.cmd_prefix >= 128) atomicAdd(&sh_d[dp & 0x3FF], 1u);
+        if (c.cmd_prefix >= 128) atomicAdd(&sh_d[dist_ctx(len) * 128 + (dp & 0x3FF)], 1u);
       } else {   // insert-only: copy code 0 with the implicit last distance when possible
         c.cmd_prefix = (uint16_t)combine_codes(ic, 0, ic < 8);
       }
       atomicAdd(&sh_c[c.cmd_prefix], 1u);
       out[q] = c;
       outp[q] = pos;
-      for (uint32_t k = 0; k < ins; k++) atomicAdd(&sh_l[jb.data[pos + k]], 1u);
+      const uint32_t p12 = prev2(jb, pos);
+      uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
+      for (uint32_t k = 0; k < ins; k++) {
+        const uint32_t lit = jb.data[pos + k];
+        atomicAdd(&sh_l[(lut[p1] | lut[256 + p2]) * 256 + lit], 1u);
+        p2 = p1;
+        p1 = lit;
+      }
     }
     __syncthreads();
   }
   const uint32_t m = sg.mb;
   for (int i = t; i < 704; i += kBlock)
     if (sh_c[i]) atomicAdd(&hc[m * 704 + i], sh_c[i]);
-  for (int i = t; i < 256; i += kBlock)
-    if (sh_l[i]) atomicAdd(&hl[m * 256 + i], sh_l[i]);
-  if (t < 128 && sh_d[t]) atomicAdd(&hd[m * 128 + t], sh_d[t]);
+  for (int i = t; i < kLitCtx * 256; i += kBlock)
+    if (sh_l[i]) atomicAdd(&hl[(size_t)m * kLitCtx * 256 + i], sh_l[i]);
+  for (int i = t; i < kDistCtx * 128; i += kBlock)
+    if (sh_d[i]) atomicAdd(&hd[(size_t)m * kDistCtx * 128 + i], sh_d[i]);
+}
+
+// ---------------------------------------------------------------- clustering
+// clusterHistograms (cluster.ts:317-377) restated for one block: the metablock's context
+// histograms (64 literal ones over 256 symbols, or 4 distance ones) are merged greedily --
+// always the pair whose merge saves the most estimated bits (populationCost-style: Shannon
+// bits + a prefix-code header estimate, bit-cost.ts:44-135) -- until no merge saves bits.
+// Writes the context map (clusters numbered by first use, as the decoder's IMTF expects
+// nothing of it) and the clustered histograms in place.
+__device__ __forceinline__ float hist_cost(float bits, int nnz) {
+  if (nnz <= 1) return 12.f;
+  if (nnz <= 4) return bits + 20.f + 4.f * nnz;
+  return bits + 40.f + 3.5f * nnz;
+}
+
+__global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
+  constexpr int kMaxH = kLitCtx;
+  __shared__ uint32_t h[kMaxH][256];
+  __shared__ float cost[kMaxH];
+  __shared__ float save[kMaxH][kMaxH];
+  __shared__ int alive[kMaxH], label[kMaxH];
+  __shared__ float red_v[256];
+  __shared__ int red_i[256];
+  __shared__ int sh_best;
+  const int m = blockIdx.x >> 1, kind = blockIdx.x & 1;
+  Mb &mb = mbs[m];
+  const Job &jb = jobs[mb.job];
+  if (jb.uncompressed) return;
+  const int t = threadIdx.x;
+  const int nh = kind == 0 ? kLitCtx : kDistCtx;
+  const int A = kind == 0 ? 256 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
+  const int stride = kind == 0 ? 256 : 128;
+  uint32_t *src = kind == 0 ? hl + (size_t)m * kLitCtx * 256 : hd + (size_t)m * kDistCtx * 128;
+  for (int i = t; i < nh * 256; i += 256) {
+    const int a = i / 256, x = i % 256;
+    h[a][x] = x < A ? src[a * stride + x] : 0u;
+  }
+  __syncthreads();
+  // each histogram's cost, and which contexts are used at all
+  for (int a = t; a < nh; a += 256) {
+    float sum = 0.f, ent = 0.f;
+    int nnz = 0;
+    for (int x = 0; x < A; x++) {
+      const float c = (float)h[a][x];
+      if (c > 0.f) {
+        sum += c;
+        ent -= c * __log2f(c);
+        nnz++;
+      }
+    }
+    if (sum > 0.f) ent += sum * __log2f(sum);
+    cost[a] = hist_cost(ent, nnz);
+    alive[a] = sum > 0.f ? 1 : 0;
+    label[a] = a;
+  }
+  __syncthreads();
+  // savings of every pair
+  auto pair_saving = [&](int a, int b) -> float {
+    float sum = 0.f, ent = 0.f;
+    int nnz = 0;
+    for (int x = 0; x < A; x++) {
+      const float c = (float)(h[a][x] + h[b][x]);
+      if (c > 0.f) {
+        sum += c;
+        ent -= c * __log2f(c);
+        nnz++;
+      }
+    }
+    if (sum > 0.f) ent += sum * __log2f(sum);
+    return cost[a] + cost[b] - hist_cost(ent, nnz);
+  };
+  for (int p = t; p < nh * nh; p += 256) {
+    const int a = p / nh, b = p % nh;
+    save[a][b] = (a < b && alive[a] && alive[b]) ? pair_saving(a, b) : -1e30f;
+  }
+  __syncthreads();
+  for (;;) {
+    // best pair
+    float bv = -1e30f;
+    int bi = -1;
+    for (int p = t; p < nh * nh; p += 256) {
+      const float v = save[p / nh][p % nh];
+      if (v > bv) {
+        bv = v;
+        bi = p;
+      }
+    }
+    red_v[t] = bv;
+    red_i[t] = bi;
+    __syncthreads();
+    for (int o = 128; o; o >>= 1) {
+      if (t < o && (red_v[t + o] > red_v[t] || (red_v[t + o] == red_v[t] && red_i[t + o] >= 0 &&
+                                                 (red_i[t] < 0 || red_i[t + o] < red_i[t])))) {
+        red_v[t] = red_v[t + o];
+        red_i[t] = red_i[t + o];
+      }
+      __syncthreads();
+    }
+    if (t == 0) sh_best = red_v[0] > 0.f ? red_i[0] : -1;
+    __syncthreads();
+    const int best = sh_best;
+    if (best < 0) break;
+    const int a = best / nh, b = best % nh;   // merge b into a
+    for (int x = t; x < A; x += 256) h[a][x] += h[b][x];
+    __syncthreads();
+    if (t == 0) {
+      cost[a] = cost[a] + cost[b] - save[a][b];
+      alive[b] = 0;
+      for (int q = 0; q < nh; q++)
+        if (label[q] == b) label[q] = a;
+    }
+    __syncthreads();
+    // pairs with b die; pairs with a change
+    for (int q = t; q < nh; q += 256) {
+      save[min(q, b)][max(q, b)] = -1e30f;
+      if (q != a) {
+        const int lo = min(q, a), hi = max(q, a);
+        save[lo][hi] = alive[q] ? pair_saving(lo, hi) : -1e30f;
+      }
+    }
+    __syncthreads();
+  }
+  // number the clusters by first use; unused contexts go to cluster 0
+  __shared__ int rep_id[kMaxH];
+  if (t == 0) {
+    for (int a = 0; a < nh; a++) rep_id[a] = -1;
+    int k = 0;
+    for (int q = 0; q < nh; q++)
+      if (alive[label[q]] && rep_id[label[q]] < 0) rep_id[label[q]] = k++;
+    for (int q = 0; q < nh; q++) {
+      const int c = alive[label[q]] ? rep_id[label[q]] : 0;
+      if (kind == 0) mb.lit_cmap[q] = (uint8_t)c;
+      else mb.dist_cmap[q] = (uint8_t)c;
+    }
+    if (k == 0) k = 1;
+    if (kind == 0) mb.nlit = (uint32_t)k;
+    else mb.ndist = (uint32_t)k;
+  }
+  __syncthreads();
+  // clustered histograms, in place: cluster c <- its representative's merged histogram
+  for (int i = t; i < nh * stride; i += 256) src[i] = 0;
+  __syncthreads();
+  for (int i = t; i < nh * 256; i += 256) {
+    const int a = i / 256, x = i % 256;
+    const int c = alive[a] ? rep_id[a] : -1;
+    if (c >= 0 && x < A) src[c * stride + x] = h[a][x];
+  }
 }
 
 // ---------------------------------------------------------------- distance ring after a chunk
@@ -365,9 +561,81 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize) {
   }
 }
 
+// One prefix code: simple form for up to 4 used symbols (zero-length codeword for one),
+// complex form otherwise (buildAndStoreHuffmanTree, context-map.ts:215-347).  `depth`
+// holds the code lengths (computed by the caller for n >= 2); `code` is filled.
+__device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uint8_t *depth, uint16_t *code, int asize) {
+  if (n <= 1) {
+    w.put(4, 1);
+    w.put(max_bits, n ? (uint32_t)nzs[0] : 0u);
+    if (n) depth[nzs[0]] = 0;
+    for (int i = 0; i < asize; i++) code[i] = 0;
+    return;
+  }
+  depths_to_codes(depth, asize, code);
+  if (n <= 4) {
+    int s4[4];
+    for (int i = 0; i < n; i++) s4[i] = nzs[i];
+    for (int i = 1; i < n; i++) {
+      int v = s4[i], k = i;
+      while (k > 0 && depth[s4[k - 1]] > depth[v]) {
+        s4[k] = s4[k - 1];
+        k--;
+      }
+      s4[k] = v;
+    }
+    w.put(2, 1);
+    w.put(2, (uint32_t)(n - 1));
+    for (int i = 0; i < n; i++) w.put(max_bits, (uint32_t)s4[i]);
+    if (n == 4) w.put(1, depth[s4[0]] == 1 ? 1 : 0);
+    return;
+  }
+  store_complex(w, depth, asize);
+}
+
+// serial length-limited Huffman depths for small alphabets (<= 80 symbols)
+__device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *depth) {
+  int16_t sorted[80];
+  uint32_t cnt[2 * 80 + 2];
+  int16_t left[2 * 80 + 2], val[2 * 80 + 2];
+  for (int i = 0; i < len; i++) depth[i] = 0;
+  int n = 0;
+  for (int i = len - 1; i >= 0; i--)
+    if (h[i]) sorted[n++] = (int16_t)i;
+  if (n == 0) return;
+  if (n == 1) {
+    depth[sorted[0]] = 1;
+    return;
+  }
+  for (uint32_t lc = 1;; lc *= 2) {
+    for (int a = 1; a < n; a++) {   // count ascending, symbol descending
+      int16_t v = sorted[a];
+      uint32_t cv = h[v] > lc ? h[v] : lc;
+      int k = a - 1;
+      while (k >= 0) {
+        uint32_t ck = h[sorted[k]] > lc ? h[sorted[k]] : lc;
+        if (ck > cv || (ck == cv && sorted[k] < v)) {
+          sorted[k + 1] = sorted[k];
+          k--;
+        } else {
+          break;
+        }
+      }
+      sorted[k + 1] = v;
+    }
+    bool ok;
+    tree_depths(h, sorted, n, lc, limit, depth, cnt, left, val, &ok);
+    if (ok) return;
+    for (int i = 0; i < len; i++) depth[i] = 0;
+  }
+}
+
+// Block (one wave) per (metablock, code slot): slots 0..63 the literal clusters, 64 the
+// command code, 65..68 the distance clusters; slots beyond the metablock's cluster counts
+// are empty.
 __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                                                      const uint32_t *hc, const uint32_t *hd, Codes *codes,
-                                                     uint8_t *trees, uint8_t *hdr) {
+                                                     uint8_t *trees) {
   __shared__ uint32_t h[704];
   __shared__ int16_t nzs[704];
   __shared__ int16_t sorted[704];
@@ -377,13 +645,20 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ uint16_t code[704];
   __shared__ uint8_t buf[kTreeBytes];
   __shared__ int sh_ok;
-  const int m = blockIdx.x / 3, t = blockIdx.x % 3;
+  const int m = blockIdx.x / kTreeSlots, t = blockIdx.x % kTreeSlots;
   const int lane = threadIdx.x;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
-  const int asize = t == 0 ? 256 : t == 1 ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
-  const uint32_t *src = t == 0 ? hl + m * 256 : t == 1 ? hc + m * 704 : hd + m * 128;
+  const bool lit = t < kCmdSlot, dist = t > kCmdSlot;
+  const int cl = dist ? t - kCmdSlot - 1 : t;
+  if ((lit && cl >= (int)mb.nlit) || (dist && cl >= (int)mb.ndist)) {
+    if (lane == 0) mb.tree_bits[t] = 0;
+    return;
+  }
+  const int asize = lit ? 256 : !dist ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
+  const uint32_t *src = lit ? hl + ((size_t)m * kLitCtx + cl) * 256 : !dist ? hc + (size_t)m * 704
+                                                                          : hd + ((size_t)m * kDistCtx + cl) * 128;
   for (int i = lane; i < asize; i += 64) {
     h[i] = src[i];
     depth[i] = 0;
@@ -430,82 +705,149 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   }
   if (lane == 0) {
     BitW w{buf, 0};
-    if (n <= 1) {   // one symbol (or none): simple code, zero-length codeword
-      w.put(4, 1);
-      w.put(max_bits, n ? (uint32_t)nzs[0] : 0u);
-      if (n) depth[nzs[0]] = 0;
-    } else {
-      depths_to_codes(depth, asize, code);
-      if (n <= 4) {
-        int s4[4];
-        for (int i = 0; i < n; i++) s4[i] = nzs[i];
-        for (int i = 1; i < n; i++) {
-          int v = s4[i], k = i;
-          while (k > 0 && depth[s4[k - 1]] > depth[v]) {
-            s4[k] = s4[k - 1];
-            k--;
-          }
-          s4[k] = v;
-        }
-        w.put(2, 1);
-        w.put(2, (uint32_t)(n - 1));
-        for (int i = 0; i < n; i++) w.put(max_bits, (uint32_t)s4[i]);
-        if (n == 4) w.put(1, depth[s4[0]] == 1 ? 1 : 0);
-      } else {
-        store_complex(w, depth, asize);
-      }
-    }
+    store_code(w, n, nzs, max_bits, depth, code, asize);
     mb.tree_bits[t] = (uint32_t)w.pos;
   }
   wave_sync();
-  uint8_t *dst = trees + ((size_t)m * 3 + t) * kTreeBytes;
+  uint8_t *dst = trees + ((size_t)m * kTreeSlots + t) * kTreeBytes;
   for (int i = lane; i < kTreeBytes; i += 64) dst[i] = buf[i];
   Codes &cd = codes[m];
-  uint8_t *dd = t == 0 ? cd.ld : t == 1 ? cd.cd : cd.dd;
-  uint16_t *cc = t == 0 ? cd.lc : t == 1 ? cd.cc : cd.dcd;
+  uint8_t *dd = lit ? cd.ld[cl] : !dist ? cd.cd : cd.dd[cl];
+  uint16_t *cc = lit ? cd.lc[cl] : !dist ? cd.cc : cd.dcd[cl];
   for (int i = lane; i < asize; i += 64) {
     dd[i] = depth[i];
     cc[i] = code[i];
   }
-  // the metablock header before the codes (storeMetaBlockTrivial, metablock.ts:290-356)
-  if (t == 0 && lane == 0) {
-    uint8_t *hb = hdr + (size_t)m * kHdrBytes;
-    for (int i = 0; i < kHdrBytes; i++) hb[i] = 0;
-    BitW w{hb, 0};
-    if (mb.start == 0 && jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
-    const uint32_t length = mb.end - mb.start;
-    w.put(1, mb.is_last);
-    if (mb.is_last) w.put(1, 0);
-    const int lg = length == 1 ? 1 : 32 - __clz(length - 1);
-    const int mn = (lg < 16 ? 16 : lg + 3) / 4;
-    w.put(2, (uint32_t)(mn - 4));
-    w.put(mn * 4, length - 1);
-    if (!mb.is_last) w.put(1, 0);
-    put_varlen_u8(w, 0);   // NBLTYPESL - 1
-    put_varlen_u8(w, 0);   // NBLTYPESI - 1
-    put_varlen_u8(w, 0);   // NBLTYPESD - 1
-    w.put(2, jb.npostfix);
-    w.put(4, jb.ndirect >> jb.npostfix);
-    w.put(2, 0);           // literal context mode (one tree: contexts unused)
-    put_varlen_u8(w, 0);   // NTREESL - 1
-    put_varlen_u8(w, 0);   // NTREESD - 1
-    mb.hdr_bits = (uint32_t)w.pos;
+}
+
+// encodeContextMap (context-map.ts:114-170): NTREES, then (NTREES > 1) move-to-front, runs
+// of zeros as RLEMAX-prefixed run codes, a prefix code over NTREES + RLEMAX symbols, and the
+// IMTF bit (RFC 7932 section 7.3).  Serial, one lane.
+__device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int ntrees) {
+  put_varlen_u8(w, ntrees - 1);
+  if (ntrees <= 1) return;
+  uint8_t mtf[kLitCtx];
+  for (int i = 0; i < ntrees; i++) mtf[i] = (uint8_t)i;
+  uint8_t v[kLitCtx];
+  for (int i = 0; i < size; i++) {
+    int idx = 0;
+    while (mtf[idx] != cmap[i]) idx++;
+    v[i] = (uint8_t)idx;
+    for (int k = idx; k > 0; k--) mtf[k] = mtf[k - 1];
+    mtf[0] = cmap[i];
   }
+  int maxrun = 0;
+  for (int i = 0; i < size;) {
+    int r = 0;
+    while (i + r < size && v[i + r] == 0) r++;
+    if (r > maxrun) maxrun = r;
+    i += r ? r : 1;
+  }
+  int rlemax = 0;
+  while ((2 << rlemax) <= maxrun && rlemax < 16) rlemax++;   // largest p with 2^p <= maxrun
+  // symbols (code, extra bits, extra)
+  uint8_t sym[kLitCtx], nb[kLitCtx];
+  uint16_t ex[kLitCtx];
+  int ns = 0;
+  for (int i = 0; i < size;) {
+    if (v[i] != 0) {
+      sym[ns] = (uint8_t)(v[i] + rlemax);
+      nb[ns] = 0;
+      ex[ns++] = 0;
+      i++;
+      continue;
+    }
+    int L = 0;
+    while (i + L < size && v[i + L] == 0) L++;
+    i += L;
+    while (L > 0) {
+      if (L == 1 || rlemax == 0) {
+        sym[ns] = 0;
+        nb[ns] = 0;
+        ex[ns++] = 0;
+        L--;
+        continue;
+      }
+      int p = 0;
+      while ((2 << p) <= L && p < rlemax) p++;
+      const int extra = min(L - (1 << p), (1 << p) - 1);
+      sym[ns] = (uint8_t)p;
+      nb[ns] = (uint8_t)p;
+      ex[ns++] = (uint16_t)extra;
+      L -= (1 << p) + extra;
+    }
+  }
+  const int asize = ntrees + rlemax;
+  uint32_t hist[kLitCtx + 16];
+  for (int i = 0; i < asize; i++) hist[i] = 0;
+  for (int k = 0; k < ns; k++) hist[sym[k]]++;
+  w.put(1, rlemax > 0 ? 1 : 0);
+  if (rlemax) w.put(4, (uint32_t)(rlemax - 1));
+  uint8_t depth[kLitCtx + 16];
+  uint16_t code[kLitCtx + 16];
+  int16_t nzs[kLitCtx + 16];
+  int n = 0;
+  for (int i = 0; i < asize; i++)
+    if (hist[i]) nzs[n++] = (int16_t)i;
+  serial_depths(hist, asize, 15, depth);
+  int max_bits = 0;
+  for (int c = asize - 1; c; c >>= 1) max_bits++;
+  store_code(w, n, nzs, max_bits, depth, code, asize);
+  for (int k = 0; k < ns; k++) {
+    w.put(depth[sym[k]], code[sym[k]]);
+    if (nb[k]) w.put(nb[k], ex[k]);
+  }
+  w.put(1, 1);   // IMTF
+}
+
+// The metablock header before the prefix codes, lane per metablock (storeMetaBlock's
+// header part, metablock.ts:690-705; one block type per category).
+__global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hdr) {
+  int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= nmbs) return;
+  Mb &mb = mbs[m];
+  const Job &jb = jobs[mb.job];
+  if (jb.uncompressed) return;
+  uint8_t *hb = hdr + (size_t)m * kHdrBytes;
+  for (int i = 0; i < kHdrBytes; i++) hb[i] = 0;
+  BitW w{hb, 0};
+  if (mb.start == 0 && jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
+  const uint32_t length = mb.end - mb.start;
+  w.put(1, mb.is_last);
+  if (mb.is_last) w.put(1, 0);
+  const int lg = length == 1 ? 1 : 32 - __clz(length - 1);
+  const int mn = (lg < 16 ? 16 : lg + 3) / 4;
+  w.put(2, (uint32_t)(mn - 4));
+  w.put(mn * 4, length - 1);
+  if (!mb.is_last) w.put(1, 0);
+  put_varlen_u8(w, 0);   // NBLTYPESL - 1
+  put_varlen_u8(w, 0);   // NBLTYPESI - 1
+  put_varlen_u8(w, 0);   // NBLTYPESD - 1
+  w.put(2, jb.npostfix);
+  w.put(4, jb.ndirect >> jb.npostfix);
+  w.put(2, mb.ctx_mode);
+  encode_context_map(w, mb.lit_cmap, kLitCtx, (int)mb.nlit);
+  encode_context_map(w, mb.dist_cmap, kDistCtx, (int)mb.ndist);
+  mb.hdr_bits = (uint32_t)w.pos;
 }
 
 // ---------------------------------------------------------------- sizes: block per segment
-__global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *segs, const Cmd *cmds, const uint32_t *cmd_pos,
-                                                       const Codes *codes) {
+__global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
+                                                       const uint32_t *cmd_pos, const Codes *codes) {
   typedef hipcub::BlockReduce<unsigned long long, kBlock> Reduce;
   __shared__ typename Reduce::TempStorage tmp;
   Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
+  const Mb &mb = mbs[sg.mb];
   const Codes &cd = codes[sg.mb];
+  const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
   unsigned long long bits = 0;
-  for (uint32_t q = threadIdx.x; q < n; q += kBlock)
-    bits += command_bits(cd, cmds[sg.cmd_off + q], jb.data + cmd_pos[sg.cmd_off + q]);
+  for (uint32_t q = threadIdx.x; q < n; q += kBlock) {
+    const uint32_t p = cmd_pos[sg.cmd_off + q];
+    bits += command_bits(cd, mb, lut, cmds[sg.cmd_off + q], jb.data + p, prev2(jb, p));
+  }
   unsigned long long total = Reduce(tmp).Sum(bits);
   if (threadIdx.x == 0) sg.bits = total;
 }
@@ -520,7 +862,8 @@ __global__ void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t
   for (uint32_t m = 0; m < jb.nmb; m++) {
     Mb &mb = mbs[jb.mb_base + m];
     mb.bit_off = pos;
-    pos += (uint64_t)mb.hdr_bits + mb.tree_bits[0] + mb.tree_bits[1] + mb.tree_bits[2];
+    pos += mb.hdr_bits;
+    for (int q = 0; q < kTreeSlots; q++) pos += mb.tree_bits[q];
     for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
       segs[s].bit_off = pos;
       pos += segs[s].bits;
@@ -549,20 +892,27 @@ __global__ void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
   hipLaunchKernelGGL(carry_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, mbs);
 }
-void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const RawCmd *raw, Cmd *cmds,
+void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
-  hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, raw, cmds, cmd_pos, hl, hc, hd);
+  hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, hl, hc, hd);
 }
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds) {
   hipLaunchKernelGGL(dist_ring_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, cmds);
 }
+void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
+  hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs);
+}
+void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
+  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2), dim3(256), 0, st, jobs, mbs, nmbs, hl, hd);
+}
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
-  hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * 3), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, hdr);
+  hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * kTreeSlots), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees);
+  hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr);
 }
-void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Cmd *cmds, const uint32_t *cmd_pos,
-                  const Codes *codes) {
-  hipLaunchKernelGGL(sizes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, cmds, cmd_pos, codes);
+void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
+                  const uint32_t *cmd_pos, const Codes *codes) {
+  hipLaunchKernelGGL(sizes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes);
 }
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
   hipLaunchKernelGGL(offsets_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, out);

@@ -118,6 +118,7 @@ struct StreamDesc {
   uint32_t hdr_lgwin;
   uint32_t final_;
   int32_t dc[4];
+  uint32_t prev_bytes;   // p1 | p2 << 8 before data[0] (streaming)
 };
 
 struct Params {
@@ -158,6 +159,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.hdr_lgwin = sd[j].hdr_lgwin;
     jb.final_ = sd[j].final_;
     for (int q = 0; q < 4; q++) jb.dc_in[q] = jb.dc_out[q] = sd[j].dc[q];
+    jb.prev_bytes = sd[j].prev_bytes;
     jb.pos_base = (uint32_t)pos_total;
     jb.seg_base = (uint32_t)segs.size();
     jb.mb_base = (uint32_t)mbs.size();
@@ -208,7 +210,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += ((size_t)total + 1) * 8;
   need += cmd_total * (sizeof(RawCmd) + sizeof(Cmd) + 4);
   need += k * (sizeof(Job) + 1024 + 8) + ns1 * sizeof(Seg) + seg_job.size() * 4;
-  need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + 3 * kTreeBytes + 4 * (256 + 704 + 128));
+  need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + kTreeSlots * kTreeBytes + 4 * (kLitCtx * 256 + 704 + kDistCtx * 128));
   need += out_scratch + 64;
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
@@ -239,12 +241,12 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   Mb *d_mbs = ar.take<Mb>(nm1);
   uint32_t *d_seg_job = ar.take<uint32_t>(seg_job.size());
   uint32_t *lit_h = ar.take<uint32_t>(k * 256);
-  uint32_t *hl = ar.take<uint32_t>(nm1 * 256);
+  uint32_t *hl = ar.take<uint32_t>(nm1 * kLitCtx * 256);
   uint32_t *hc = ar.take<uint32_t>(nm1 * 704);
-  uint32_t *hd = ar.take<uint32_t>(nm1 * 128);
+  uint32_t *hd = ar.take<uint32_t>(nm1 * kDistCtx * 128);
   Codes *codes = ar.take<Codes>(nm1);
   uint8_t *hdr = ar.take<uint8_t>(nm1 * kHdrBytes);
-  uint8_t *trees = ar.take<uint8_t>(nm1 * 3 * kTreeBytes);
+  uint8_t *trees = ar.take<uint8_t>(nm1 * kTreeSlots * kTreeBytes);
   uint64_t *d_dst_off = ar.take<uint64_t>(k + 1);
   uint8_t *oscr = ar.take<uint8_t>(out_scratch + 64);
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
@@ -257,9 +259,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
   if (nsegs) {
     CK(hipMemsetAsync(lit_h, 0, k * 256 * 4, st));
-    CK(hipMemsetAsync(hl, 0, nm1 * 256 * 4, st));
+    CK(hipMemsetAsync(hl, 0, nm1 * kLitCtx * 256 * 4, st));
     CK(hipMemsetAsync(hc, 0, nm1 * 704 * 4, st));
-    CK(hipMemsetAsync(hd, 0, nm1 * 128 * 4, st));
+    CK(hipMemsetAsync(hd, 0, nm1 * kDistCtx * 128 * 4, st));
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
     const int depth = depth_for_quality(prm.quality);
     tm.start("hash_keys");
@@ -282,14 +284,18 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.stop();
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
-    launch_codes(st, d_jobs, d_segs, nsegs, raw, cmds, cmd_pos, hl, hc, hd);
+    launch_context_mode(st, d_jobs, d_mbs, nmbs);
+    launch_codes(st, d_jobs, d_segs, d_mbs, nsegs, raw, cmds, cmd_pos, hl, hc, hd);
     launch_dist_ring(st, d_jobs, (int)k, d_segs, cmds);
+    tm.stop();
+    tm.start("cluster");
+    launch_cluster(st, d_jobs, d_mbs, nmbs, hl, hd);
     tm.stop();
     tm.start("huffman");
     launch_huffman(st, d_jobs, d_mbs, nmbs, hl, hc, hd, codes, trees, hdr);
     tm.stop();
     tm.start("sizes");
-    launch_sizes(st, d_jobs, d_segs, nsegs, cmds, cmd_pos, codes);
+    launch_sizes(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, codes);
     launch_offsets(st, d_jobs, (int)k, d_mbs, d_segs, oscr);
     tm.stop();
     tm.start("emit");
@@ -362,6 +368,7 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
   d.dc[1] = 11;
   d.dc[2] = 15;
   d.dc[3] = 16;
+  d.prev_bytes = 0;
   if (!one_shot) {
     d.hdr_lgwin = (uint32_t)prm.lgwin;
   } else if (n == 0) {
@@ -389,6 +396,7 @@ struct mib_encoder {
   bool started = false;
   bool finished = false;
   int32_t dc[4] = {4, 11, 15, 16};
+  uint32_t prev_bytes = 0;   // the last two bytes handed to the engine (literal contexts)
   uint64_t block = 1 << 16;
 };
 
@@ -447,6 +455,7 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
       sd[i].hdr_lgwin = streaming->started ? 0 : (uint32_t)prm.lgwin;
       sd[i].final_ = final_ ? 1 : 0;
       for (int q = 0; q < 4; q++) sd[i].dc[q] = streaming->dc[q];
+      sd[i].prev_bytes = streaming->prev_bytes;
     }
   }
   std::vector<uint64_t> ooff(k + 1, 0);
@@ -519,6 +528,8 @@ static int encoder_emit(mib_encoder *e, const uint8_t *p, size_t n, bool final_,
   acc.insert(acc.end(), b.data, b.data + b.size);
   mib_buf_free(&b);
   e->started = true;
+  for (size_t i = 0; i < n && i < 2; i++)   // shift in the chunk's last bytes
+    e->prev_bytes = ((e->prev_bytes << 8) & 0xFF00) | p[n - (n < 2 ? n : 2) + i];
   return 0;
 }
 
