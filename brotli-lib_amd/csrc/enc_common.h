@@ -18,7 +18,6 @@ constexpr uint32_t kSegBits = 16;
 constexpr uint32_t kSeg = 1u << kSegBits;     // 64 KiB parse segments
 constexpr int kMaxMatches = 6;                // staircase entries kept per position
 constexpr uint32_t kMatchLenSat = 255;        // a match is (length:8 | distance:24); 255 = "255 or more"
-constexpr int kRing = 256;                    // DP node window (> kLongCopy + staged batch)
 constexpr int kLongCopy = 200;                // copies longer than this are taken outright (the
                                               // reference's MAX_ZOPFLI_LEN is 325 at q11, 150 at q10,
                                               // enc-constants.ts:32-33)

@@ -14,32 +14,62 @@ namespace enc {
 // than kLongCopy is taken outright and the parse jumps to its end, as the reference does
 // (:518-533).
 //
-// One wave runs kG = 2 segments side by side, 32 lanes each: per step every group advances
-// its own segment by one position, its 32 lanes relaxing 32 copy lengths at a time, so the
-// per-position bookkeeping is paid once per 2 positions.  (Measured on MI355X, 1 GiB of
-// text: 1 x 64 lanes 696 ms, 2 x 32 474 ms, 4 x 16 518 ms, 8 x 8 897 ms -- beyond two
-// groups the groups' divergent refills and long-match chunks cost more than they save.)
-// Everything a position needs (its matches with their distance costs, its literal cost) is
-// staged into LDS kBatch positions at a time from registers that were loaded one batch
-// ahead, so the serial loop itself never waits on global memory.
-constexpr int kGL = 32;        // lanes per segment
-constexpr int kG = 64 / kGL;   // segments per wave
-constexpr int kBatch = kGL;    // positions staged per refill (one per lane)
-constexpr int kCache = kGL >= 32 ? 1 : 32 / kGL;   // length chunks whose command costs stay in registers
-constexpr uint32_t kRingMask = kRing - 1;
+// One wave per segment, the pending nodes in REGISTERS: the parse runs in batches of 64
+// positions starting at i0, and lane j of chunk k holds node i0 + 64 k + j.  Relaxing the
+// edge of length l out of i = i0 + off lands in chunk (off + l) / 64, lane (off + l) % 64:
+// every lane relaxes the one length that maps to it -- a lane-local compare/select, no LDS
+// round trip, no shuffle -- and only the chunks holding lengths 0..maxlen are touched.
+// Node i is read with three readlanes from chunk 0.  At a batch end the chunks move down
+// by one (chunk 0 is all consumed nodes).
+//
+// The length-dependent half of a copy's price (copy code, its extra bits, the command
+// code it forms with the insert code, with and without short code 0) comes from an LDS
+// table indexed by (insert code, length), fp16 pairs, built once per workgroup.
+// Per-position inputs (matches, distance costs, literal cost) are staged one lane per
+// position, loaded a batch ahead, and read back with readlanes; the batch's choices are
+// collected the same way and stored as one coalesced write.
+#ifdef MIB_PROF   // timing experiment: cycles in staging / node read / long copies / relaxation; counts
+__device__ unsigned long long g_dp_prof[8];
+#define DPMARK(slot)                                  \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    prof[slot] += t_ - pt0;                           \
+    pt0 = t_;                                         \
+  } while (0)
+#define DPCOUNT(slot, v) prof[slot] += (v)
+#else
+#define DPMARK(slot) do {} while (0)
+#define DPCOUNT(slot, v) do {} while (0)
+#endif
+constexpr int kC = 5;                 // chunks: batch offset (< 64) + longest relaxed length (<= kLongCopy)
+constexpr int kDpWaves = 4;           // segments (waves) per workgroup, sharing the length table
+constexpr int kLenTab = kLongCopy + 1;
 constexpr float kInf = 3.0e38f;
-static_assert(kLongCopy + kBatch < kRing, "a batch's nodes must survive until they are flushed");
+static_assert(63 + kLongCopy < 64 * kC, "every relaxed length must land in a chunk");
 
-// node meta: last distance (32) | copy length that reached it (16, 0 = literal) | insert length (16)
-__device__ __forceinline__ uint64_t pack_node(uint32_t ld, uint32_t clen, uint32_t ins) {
-  return (uint64_t)ld | ((uint64_t)clen << 32) | ((uint64_t)min(ins, 65535u) << 48);
+typedef const __attribute__((address_space(1))) uint8_t GCU8;
+
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
+__device__ __forceinline__ float rdlf(float v, uint32_t l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
 }
-__device__ __forceinline__ uint64_t node_choice(uint64_t m) {   // (distance << 32) | length, 0 = literal
-  uint32_t cl = (uint32_t)(m >> 32) & 0xFFFF;
-  return cl ? (((uint64_t)(uint32_t)m << 32) | cl) : 0ull;
+// kCopyExtra / kInsExtra in closed form (no table loads on the serial path)
+__device__ __forceinline__ uint32_t copy_extra(int cc) { return cc < 8 ? 0u : cc < 18 ? (uint32_t)(cc - 6) >> 1 : cc < 23 ? (uint32_t)(cc - 12) : 24u; }
+__device__ __forceinline__ uint32_t ins_extra(int ic) {
+  return ic < 6 ? 0u : ic < 16 ? (uint32_t)(ic - 4) >> 1 : ic < 21 ? (uint32_t)(ic - 10) : ic == 21 ? 12u : ic == 22 ? 14u : 24u;
+}
+// iteration-0 cost model (zopfli-cost-model.ts: costCmd = log2(11 + code), costDist = log2(20 + code))
+__device__ __forceinline__ float cmd_cost(int cmd) { return __builtin_amdgcn_logf(11.f + (float)cmd); }
+__device__ __forceinline__ float dist_sym_cost(uint32_t code) { return __builtin_amdgcn_logf(20.f + (float)min(code, 127u)); }
+// the length-dependent price of a copy of length l after insert code ic: with an explicit
+// distance (its symbol cost added by the caller), and with short code 0 (complete)
+__device__ __forceinline__ float copy_price(int ic, uint32_t l, bool last, float dist0) {
+  const int cc = copy_code(l);
+  const int cmd = combine_codes(ic, cc, last);
+  return (float)copy_extra(cc) + cmd_cost(cmd) + (last && cmd >= 128 ? dist0 : 0.f);
 }
 
-struct Staged {   // one position's parse inputs, loaded ahead
+struct Staged {   // one position's parse inputs (lane j of a batch = position i0 + j)
   uint32_t m[kMaxMatches];
   uint32_t nm;
   uint32_t lit;
@@ -52,243 +82,251 @@ __device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches,
 #pragma unroll
   for (int q = 0; q < kMaxMatches; q++) st.m[q] = src[q];   // entries past nm are ignored
 }
+__device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (distance << 32) | length, 0 = literal
+  const uint32_t cl = m & 0xFFFF;
+  return cl ? (((uint64_t)d << 32) | cl) : 0ull;
+}
 
-__global__ __launch_bounds__(64) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_histo,
-                                                const uint32_t *matches, const uint8_t *nmatch,
-                                                uint64_t *choice /* per position+1 */) {
-  // per-group rows are padded so the 4 groups' same-offset accesses fall in different banks
-  __shared__ float cost[kG][kRing + 1];
-  __shared__ uint64_t meta[kG][kRing + 1];
-  __shared__ uint16_t litc[kG][256 + 2];   // literal cost x 256
-  __shared__ float cmdc[704];
-  __shared__ float distc[128];
-  __shared__ float blit[kG][kBatch + 1];
-  __shared__ uint8_t bnm[kG][kBatch + 4];
-  __shared__ uint32_t bmt[kG][kBatch * kMaxMatches + 1];   // pack_match(distance, length)
-  __shared__ float bmc[kG][kBatch * kMaxMatches + 1];      // distance symbol cost + extra bits
-  const int lane = threadIdx.x, g = lane / kGL, sl = lane % kGL;
-  const int s = blockIdx.x * kG + g;
-  const bool valid = s < nsegs;
-  const Seg sg = segs[valid ? s : 0];
+__global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5))) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
+                                                           const uint32_t *lit_histo, const uint32_t *matches,
+                                                           const uint8_t *nmatch, uint64_t *choice /* per position+1 */) {
+  __shared__ uint32_t lentab[24 * kLenTab];   // (insert code, length) -> fp16 (explicit distance) | fp16 (short code 0) << 16
+  __shared__ float litc_all[kDpWaves][256];
+  const float dist0 = dist_sym_cost(0);
+  for (int t = threadIdx.x; t < 24 * kLenTab; t += 64 * kDpWaves) {
+    const int ic = t / kLenTab;
+    const uint32_t l = (uint32_t)(t % kLenTab);
+    uint32_t v = 0;
+    if (l >= 4) {
+      const _Float16 a = (_Float16)copy_price(ic, l, false, dist0), b = (_Float16)copy_price(ic, l, true, dist0);
+      v = (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+    }
+    lentab[t] = v;
+  }
+  __syncthreads();
+  // the wave index is wave-uniform: say so, so that everything derived from the segment stays scalar
+  const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int s = blockIdx.x * kDpWaves + (int)w;
+  if (s >= nsegs) return;
+  float *litc = litc_all[w];
+  const Seg sg = segs[s];
   const Job &jb = jobs[sg.job];
   const uint8_t *data = jb.data;
   const uint32_t a = sg.start, b = sg.end, gbase = jb.pos_base;
-  for (int i = lane; i < 704; i += 64) cmdc[i] = log2f(11.f + i);
-  for (int i = lane; i < 128; i += 64) distc[i] = log2f(20.f + i);
+  const int ndirect = (int)jb.ndirect, npostfix = (int)jb.npostfix;
+  if (a >= b) return;
   // literal costs from the stream's order-0 histogram (zopfli-cost-model.ts:163-189)
   {
     uint32_t part = 0;
-    for (int i = sl; i < 256; i += kGL) part += lit_histo[sg.job * 256 + i];
-    for (int o = kGL / 2; o; o >>= 1) part += __shfl_xor(part, o, kGL);
+    for (uint32_t k = lane; k < 256; k += 64) part += lit_histo[sg.job * 256 + k];
+    for (int o = 32; o; o >>= 1) part += __shfl_xor(part, o);
     const float lt = log2f((float)max(part, 1u));
-    for (int i = sl; i < 256; i += kGL) {
-      const uint32_t c = lit_histo[sg.job * 256 + i];
+    for (uint32_t k = lane; k < 256; k += 64) {
+      const uint32_t c = lit_histo[sg.job * 256 + k];
       const float v = c ? lt - log2f((float)c) : lt + 2.f;
-      litc[g][i] = (uint16_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f);
+      litc[k] = (float)(uint32_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f) * (1.f / 256.f);
     }
   }
-  for (int i = sl; i < kRing; i += kGL) {
-    cost[g][i] = kInf;
-    meta[g][i] = 0;
-  }
   wave_sync();
-  if (sl == 0) cost[g][a & kRingMask] = 0.f;
-  // command cost of this lane's lengths in chunks 0 and 1 for the current insert code
-  int ccA[kCache];
-  float cmA[kCache], cmlA[kCache];
+  // the pending nodes: cost, last distance, (copy length that reached it | insert length << 16)
+  float wc[kC];
+  uint32_t wd[kC], wm[kC];
 #pragma unroll
-  for (int c = 0; c < kCache; c++) {
-    ccA[c] = copy_code(max(2u, (uint32_t)(kGL * c + sl)));
-    cmA[c] = cmlA[c] = 0.f;
+  for (int c = 0; c < kC; c++) {
+    wc[c] = kInf;
+    wd[c] = wm[c] = 0;
   }
-  int cached_ic = -1;
-  bool active = valid && a < b;
-  uint32_t i = a, i0 = a, nb = 0;
-  bool flushed = true;   // the current batch's choices are already stored
-  // the batch after the current one, in registers
+  if (lane == 0) wc[0] = 0.f;   // node a
+  // the current batch (registers, lane = position - i0) and the next one
+  uint32_t bm[kMaxMatches], binfo = 0;   // binfo: nm | maxlen << 8 (clipped to the segment)
+  float bmc[kMaxMatches], blc = 0.f;
   Staged pf;
-  uint32_t pf_at = 0xFFFFFFFFu;
-  if (active && a + sl < b) {
-    load_staged(pf, matches, nmatch, data, gbase + a + sl, a + sl);
-    pf_at = a;
-  }
-  wave_sync();
-  for (;;) {
-    // ---- per group: finish a batch (store its choices), finish the segment, or stage
-    if (active && i >= i0 + nb) {
-      if (!flushed && (uint32_t)sl < nb && i0 + sl != a) choice[gbase + i0 + sl] = node_choice(meta[g][(i0 + sl) & kRingMask]);
-      if (i >= b) {
-        if (sl == 0) choice[gbase + b] = node_choice(meta[g][b & kRingMask]);
-        active = false;
-      } else {
-        i0 = i;
-        nb = min((uint32_t)kBatch, b - i0);
-        flushed = false;
-        Staged cur;
-        if (pf_at == i0) {
-          cur = pf;
-        } else if (i0 + sl < b) {   // the parse jumped past the prefetched batch
-          load_staged(cur, matches, nmatch, data, gbase + i0 + sl, i0 + sl);
-        }
-        // prefetch the next batch
-        const uint32_t nx = i0 + nb;
-        if (nx + sl < b) load_staged(pf, matches, nmatch, data, gbase + nx + sl, nx + sl);
-        pf_at = nx;
-        int nm = 0;
-        if ((uint32_t)sl < nb) {
-          nm = (int)cur.nm;
-          blit[g][sl] = (float)litc[g][cur.lit] * (1.f / 256.f);
-        }
-        bnm[g][sl] = (uint8_t)nm;
+  uint32_t pf_at = a;
+  if (a + lane < b) load_staged(pf, matches, nmatch, data, gbase + a + lane, a + lane);
+  uint32_t chd = 0, chm = 0;   // choices of the batch
+  uint32_t i = a, i0 = a;
+#ifdef MIB_PROF
+  uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t pt0 = __builtin_amdgcn_s_memtime();
+#endif
+  // stage the batch starting at i0 (the window's chunk 0 starts there)
+  auto stage = [&]() {
+    Staged cur;
+    if (pf_at == i0) {
+      cur = pf;
+    } else if (i0 + lane < b) {   // the parse jumped past the prefetched batch
+      load_staged(cur, matches, nmatch, data, gbase + i0 + lane, i0 + lane);
+    }
+    const uint32_t nx = i0 + 64;
+    if (nx + lane < b) load_staged(pf, matches, nmatch, data, gbase + nx + lane, nx + lane);
+    pf_at = nx;
+    const uint32_t p = i0 + lane;
+    const uint32_t nm = p < b ? cur.nm : 0u;
+    blc = p < b ? litc[cur.lit] : 0.f;
+    uint32_t maxlen = 0;
 #pragma unroll
-        for (int q = 0; q < kMaxMatches; q++) {
-          if (q < nm) {
-            const uint32_t m = cur.m[q];
-            uint32_t extra;
-            const uint32_t dp = dist_prefix(match_dist(m) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra);
-            bmt[g][sl * kMaxMatches + q] = m;
-            bmc[g][sl * kMaxMatches + q] = (float)(dp >> 10) + distc[min(dp & 0x3FFu, 127u)];
+    for (int q = 0; q < kMaxMatches; q++) {
+      bm[q] = 0;
+      bmc[q] = 0.f;
+      if ((uint32_t)q < nm) {
+        uint32_t extra;
+        const uint32_t ln = min(match_length(cur.m[q]), b - p);
+        const uint32_t dp = dist_prefix(match_dist(cur.m[q]) + 15, ndirect, npostfix, &extra);
+        bm[q] = (ln << 24) | match_dist(cur.m[q]);
+        bmc[q] = (float)(dp >> 10) + dist_sym_cost(dp & 0x3FFu);
+        maxlen = ln;
+      }
+    }
+    binfo = nm | (maxlen << 8);
+    DPCOUNT(6, 1);
+  };
+  stage();
+  DPMARK(0);
+  for (;;) {
+    const uint32_t off = i - i0;
+    // ---- node i
+    const float ci = rdlf(wc[0], off);
+    const uint32_t ld = rdl(wd[0], off), mm = rdl(wm[0], off);
+    chd = lane == off ? ld : chd;
+    chm = lane == off ? mm : chm;
+    if (i == b) break;
+    const uint32_t ins = mm >> 16;
+    const uint32_t info = rdl(binfo, off);
+    const uint32_t nm = info & 0xFF, maxlen = info >> 8;
+    const float litcost = rdlf(blc, off);
+    const int ic = ins_code(ins);
+    const float base = ci + (float)ins_extra(ic);
+    DPMARK(1);
+    DPCOUNT(4, 1);
+    if (maxlen > (uint32_t)kLongCopy) {
+      // forceful long copy (backward-references-hq.ts:518-533): the shortest-distance match
+      // longer than kLongCopy
+      uint32_t fl = 0, fd = 0;
+      float fdc = 0.f;
+#pragma unroll
+      for (int q = kMaxMatches - 1; q >= 0; q--) {
+        if ((uint32_t)q < nm) {
+          const uint32_t m = rdl(bm[q], off);
+          if (match_length(m) > (uint32_t)kLongCopy) {
+            fd = match_dist(m);
+            fl = match_length(m);
+            fdc = rdlf(bmc[q], off);
           }
         }
       }
-    }
-    wave_sync();
-    if (!__ballot(active)) break;
-    if (!active) continue;
-    // ---- one position per group
-    const uint32_t slot = i & kRingMask;
-    const float ci = cost[g][slot];
-    const uint64_t mi = meta[g][slot];
-    const uint32_t ld = (uint32_t)mi, ins_i = (uint32_t)(mi >> 48);
-    const uint32_t off = i - i0, limit = b - i;
-    const float litcost = blit[g][off];
-    const int nm = bnm[g][off];
-    uint32_t md[kMaxMatches], mL[kMaxMatches];
-    float mc[kMaxMatches];
-#pragma unroll
-    for (int q = 0; q < kMaxMatches; q++) {
-      const uint32_t m = q < nm ? bmt[g][off * kMaxMatches + q] : 0u;
-      md[q] = match_dist(m);
-      mL[q] = min(match_length(m), limit);
-      mc[q] = q < nm ? bmc[g][off * kMaxMatches + q] : 0.f;
-    }
-    wave_sync();
-    if (sl == 0) cost[g][slot] = kInf;   // the slot now serves position i + kRing
-    const int ic = ins_code(ins_i);
-    const float base = ci + (float)kInsExtra[ic];
-    if (ic != cached_ic) {
-      cached_ic = ic;
-#pragma unroll
-      for (int c = 0; c < kCache; c++) {
-        cmA[c] = (float)kCopyExtra[ccA[c]] + cmdc[combine_codes(ic, ccA[c], false)];
-        const int cmd = combine_codes(ic, ccA[c], true);
-        cmlA[c] = (float)kCopyExtra[ccA[c]] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-      }
-    }
-    // forceful long copy (backward-references-hq.ts:518-533)
-    uint32_t fl = 0, fd = 0;
-    float fc = 0.f;
-#pragma unroll
-    for (int q = 0; q < kMaxMatches; q++) {
-      if (!fl && q < nm && mL[q] > (uint32_t)kLongCopy) {
-        fd = md[q];
-        fl = mL[q];
-        const int cc = copy_code(fl);
-        const bool last = fd == ld;
-        const int cmd = combine_codes(ic, cc, last);
-        fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (last ? (cmd < 128 ? 0.f : distc[0]) : mc[q]);
-      }
-    }
-    if (fl == kMatchLenSat && limit > kMatchLenSat) {
-      // a saturated match: measure the copy (the group's lanes compare kGL bytes a step)
-      const uint8_t *cur = data + i, *src = data + i - fd;
-      const uint32_t cap = min(limit, 65535u);
-      for (;;) {
-        const uint32_t x = fl + sl;
-        const bool eq = x < cap && cur[x] == src[x];
-        const uint64_t ok = (__ballot(eq) >> (kGL * g)) & ((kGL == 64) ? ~0ull : ((1ull << kGL) - 1));
-        if (ok == ((kGL == 64) ? ~0ull : ((1ull << kGL) - 1))) {
-          fl += kGL;
-          continue;
+      const uint32_t limit = b - i;
+      if (fl == kMatchLenSat && limit > kMatchLenSat) {
+        // a saturated match: measure the copy, 64 bytes a step
+        GCU8 *cp = (GCU8 *)(data + i), *src = (GCU8 *)(data + i - fd);
+        const uint32_t cap = min(limit, 65535u);
+        for (;;) {
+          const uint32_t x = fl + lane;
+          const uint64_t ok = __ballot(x < cap && cp[x] == src[x]);
+          if (ok == ~0ull) {
+            fl += 64;
+            continue;
+          }
+          fl += (uint32_t)__ffsll((unsigned long long)~ok) - 1;
+          break;
         }
-        fl += __ffsll((unsigned long long)~ok) - 1;
-        break;
+        fl = min(fl, cap);
       }
-      fl = min(fl, cap);
       const int cc = copy_code(fl);
       const bool last = fd == ld;
       const int cmd = combine_codes(ic, cc, last);
-      float dc = 0.f;
-#pragma unroll
-      for (int q = 0; q < kMaxMatches; q++)
-        if (q < nm && md[q] == fd) dc = mc[q];
-      fc = base + (float)kCopyExtra[cc] + cmdc[cmd] + (last ? (cmd < 128 ? 0.f : distc[0]) : dc);
-    }
-    if (fl) {
-      // store the batch's finished nodes, abandon every pending node, resume at the copy's end
-      for (uint32_t p = i0 + sl; p <= i; p += kGL)
-        if (p != a) choice[gbase + p] = node_choice(meta[g][p & kRingMask]);
-      wave_sync();
-      for (int t = sl; t < kRing; t += kGL) cost[g][t] = kInf;
-      wave_sync();
-      i += fl;
-      if (sl == 0) {
-        cost[g][i & kRingMask] = fc;
-        meta[g][i & kRingMask] = pack_node(fd, fl, 0);
+      const float fc = base + (float)copy_extra(cc) + cmd_cost(cmd) + (last ? (cmd < 128 ? 0.f : dist0) : fdc);
+      // store the batch's choices up to i; every pending node is abandoned; the parse
+      // resumes at the copy's end with a new batch
+      {
+        const uint32_t p = i0 + lane;
+        if (p <= i && p != a) choice[gbase + p] = choice_of(chd, chm);
       }
-      flushed = true;
-      nb = 0;
+      i += fl;
       i0 = i;
+#pragma unroll
+      for (int c = 0; c < kC; c++) wc[c] = kInf;
+      if (lane == 0) {
+        wc[0] = fc;
+        wd[0] = fd;
+        wm[0] = fl;
+      }
+      stage();
+      DPCOUNT(7, 1);
+      DPMARK(2);
       continue;
     }
-    // relax every edge out of i: lane sl of chunk k takes length kGL k + sl, choosing the
-    // literal (length 1) or the shortest-distance match covering it
-    uint32_t maxlen = 1;
+    // the match staircase of i: lengths (clipped), distances, distance costs
+    uint32_t mL[kMaxMatches], md[kMaxMatches];
+    float mc[kMaxMatches];
 #pragma unroll
-    for (int q = 0; q < kMaxMatches; q++)
-      if (q < nm) maxlen = max(maxlen, mL[q]);
-    for (uint32_t k = 0; kGL * k <= maxlen; k++) {
-      const uint32_t l = kGL * k + sl;
-      float best = kInf;
-      uint64_t bm = 0;
-      if (l == 1) {
-        best = ci + litcost;
-        bm = pack_node(ld, 0, ins_i + 1);
-      } else if (l >= 4 && l <= maxlen) {
-        float cmx = 0.f, cml = 0.f;
-        bool cached = false;
-#pragma unroll
-        for (int c = 0; c < kCache; c++)
-          if (k == (uint32_t)c) {
-            cmx = cmA[c];
-            cml = cmlA[c];
-            cached = true;
-          }
-        if (!cached) {
-          const int cc = copy_code(l);
-          const int cmd = combine_codes(ic, cc, true);
-          cmx = (float)kCopyExtra[cc] + cmdc[combine_codes(ic, cc, false)];
-          cml = (float)kCopyExtra[cc] + cmdc[cmd] + (cmd < 128 ? 0.f : distc[0]);
-        }
-        bool found = false;
-#pragma unroll
-        for (int q = 0; q < kMaxMatches; q++) {
-          if (!found && q < nm && mL[q] >= l) {
-            found = true;
-            best = base + (md[q] == ld ? cml : mc[q] + cmx);
-            bm = pack_node(md[q], l, 0);
-          }
-        }
+    for (int q = 0; q < kMaxMatches; q++) {
+      mL[q] = md[q] = 0;
+      mc[q] = 0.f;
+      if ((uint32_t)q < nm) {
+        const uint32_t m = rdl(bm[q], off);
+        mL[q] = match_length(m);
+        md[q] = match_dist(m);
+        mc[q] = rdlf(bmc[q], off);
       }
-      if (best < kInf) {
-        const uint32_t ts = (i + l) & kRingMask;
-        if (best < cost[g][ts]) {
-          cost[g][ts] = best;
-          meta[g][ts] = bm;
-        }
+    }
+    const uint32_t maxrel = max(1u, maxlen);
+    const uint32_t *trow = lentab + ic * kLenTab;
+    // relax every edge out of i: lane j of chunk k takes length 64 k + j - off
+#pragma unroll
+    for (int c = 0; c < kC; c++) {
+      if (c > 0 && 64u * c > off + maxrel) break;
+      DPCOUNT(5, 1);
+      const uint32_t l = 64u * c + lane - off;   // wraps (huge) for consumed nodes
+      float cand = kInf;
+      uint32_t nd = ld, nmeta = min(ins + 1, 65535u) << 16;
+      if (l == 1) cand = ci + litcost;
+      if (l >= 4 && l <= maxlen) {
+        uint32_t sd = 0;
+        float sc = 0.f;
+#pragma unroll
+        for (int q = kMaxMatches - 1; q >= 0; q--)
+          if (l <= mL[q]) {   // mL = 0 past nm
+            sd = md[q];
+            sc = mc[q];
+          }
+        const uint32_t tv = trow[l];
+        const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
+        const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
+        cand = base + (sd == ld ? pl : pn + sc);
+        nd = sd;
+        nmeta = l;
+      }
+      if (cand < wc[c]) {
+        wc[c] = cand;
+        wd[c] = nd;
+        wm[c] = nmeta;
       }
     }
     i++;
+    if (i - i0 == 64) {
+      // batch end: store its choices, move the window down one chunk, stage the next batch
+      if (i0 + lane != a) choice[gbase + i0 + lane] = choice_of(chd, chm);   // node a belongs to the previous segment
+#pragma unroll
+      for (int c = 0; c + 1 < kC; c++) {
+        wc[c] = wc[c + 1];
+        wd[c] = wd[c + 1];
+        wm[c] = wm[c + 1];
+      }
+      wc[kC - 1] = kInf;
+      wd[kC - 1] = wm[kC - 1] = 0;
+      i0 = i;
+      stage();
+    }
+    DPMARK(3);
+  }
+#ifdef MIB_PROF
+  if (lane == 0)
+    for (int q = 0; q < 8; q++) atomicAdd(&g_dp_prof[q], (unsigned long long)prof[q]);
+#endif
+  // the last batch, through node b
+  {
+    const uint32_t p = i0 + lane;
+    if (p <= b && p != a) choice[gbase + p] = choice_of(chd, chm);
   }
 }
 
@@ -385,9 +423,17 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
 }
 
 
+#ifdef MIB_PROF
+extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dp_prof), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(g_dp_prof), z, sizeof(z));
+  return 0;
+}
+#endif
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                const uint32_t *matches, const uint8_t *nmatch, uint64_t *choice) {
-  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kG - 1) / kG), dim3(64), 0, st, jobs, segs, nsegs, lit_h, matches, nmatch,
+  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kDpWaves - 1) / kDpWaves), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h, matches, nmatch,
                      choice);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {

@@ -19,7 +19,8 @@ __all__ = ['brotliEncode', 'BrotliEncoder', 'brotliDecode', 'brotliDecodedSize',
            'encode_batch', 'decode_batch', 'DeviceContext', 'library_path']
 
 _PKG = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-_LIB_PATH = os.path.join(_PKG, 'libbrotli_amd.so')
+# BROTLI_AMD_LIB: an instrumented build of the same library (timing experiments only)
+_LIB_PATH = os.environ.get('BROTLI_AMD_LIB') or os.path.join(_PKG, 'libbrotli_amd.so')
 
 
 def library_path():
