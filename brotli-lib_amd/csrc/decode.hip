@@ -51,13 +51,17 @@ enum : int {
 
 constexpr int kBlockTreesCap = 3091;   // engine.ts:163 Int32Array(3091)
 
-// LDS working set of one stream (one wave).
-constexpr int kLdsTableInts = 4096;   // 16 KiB of prefix-code tables in LDS (one tree per alphabet fits)
+// LDS working set of one stream (one wave): 40 KiB, so the 4 streams per CU of a
+// 1024-stream batch fit the 160 KiB.  A metablock's prefix-code tables are built in HBM
+// scratch (packed, exact sizes) and, when they fit, copied into kLdsTab 16-bit entries
+// (nbits << 12 | symbol-or-subtable-offset), tree roots resolved to absolute indices.
+constexpr int kLdsTab = 12288;
 
 typedef __attribute__((address_space(1))) uint8_t GU8;          // HBM
 typedef const __attribute__((address_space(1))) int32_t GI32;
 typedef const __attribute__((address_space(3))) uint8_t LU8;    // LDS
 typedef const __attribute__((address_space(3))) int32_t LI32;
+typedef const __attribute__((address_space(3))) uint16_t LU16;
 
 struct Lds {
   uint8_t win[4160 + 64];    // byteBuffer (4160) + read slack
@@ -67,7 +71,7 @@ struct Lds {
   int32_t ctx_tree_base[64];
   uint8_t ctx_lut[512];        // the current literal context mode's slice of the RFC lookup table
   uint8_t mtf[256];
-  int32_t block_trees[kBlockTreesCap + 1];
+  uint16_t ctx_root[2048];     // (p1 << 3 | lut1[p2]) -> root of the literal tree (16-bit tables)
 };
 
 struct Dec {
@@ -83,8 +87,11 @@ struct Dec {
   int mbl, input_end, is_uncompressed, is_metadata;
   int lit_blen, n_lit_types, cmd_blen, n_cmd_types, dist_blen, n_dist_types;
   int rings[10], dist_rb_idx;
-  int32_t *lit_group, *cmd_group, *dist_group;   // LDS when the metablock's codes fit, else HBM scratch
-  int32_t *tab_lds, *tab_hbm;
+  int32_t *lit_group, *cmd_group, *dist_group;   // HBM scratch, packed
+  int32_t *tab_hbm;
+  uint16_t *tab_lds;       // the 16-bit copy of the tables
+  int tab16, cmd_base, dist_base;   // tables in LDS; where the command / distance groups start there
+  int32_t *bt;             // block-type and block-count trees (HBM scratch, cold)
   uint8_t *ring_scratch;   // the block's HBM ring
   int direct;              // ring == out: a single-metablock stream decodes in place
   uint8_t *ctx_modes, *ctx_map, *dist_ctx_map;   // HBM scratch
@@ -108,7 +115,7 @@ struct Dec {
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
 #ifdef MIB_PROF   // timing experiment: cycles in command / literal / distance / copy, literal and command counts
-__device__ unsigned long long g_prof[6];
+__device__ unsigned long long g_prof[8];   // + metablocks with LDS / HBM tables
 #endif
 
 // A block is one wave: a wave's LDS and global accesses are performed in order, so the
@@ -483,8 +490,8 @@ __device__ int read_block_length(Dec &s, const int32_t *g, int idx) {
 __device__ int decode_block_type_and_length(Dec &s, int tree_type, int ntypes) {   // :559-580
   int off = 4 + tree_type * 2;
   fill16(s);
-  int bt = read_symbol(s, s.l->block_trees, kBlockTreesCap, 2 * tree_type);
-  int len = read_block_length(s, s.l->block_trees, 2 * tree_type + 1);
+  int bt = read_symbol(s, s.bt, kBlockTreesCap, 2 * tree_type);
+  int len = read_block_length(s, s.bt, 2 * tree_type + 1);
   if (bt == 1) bt = s.rings[off + 1] + 1;
   else if (bt == 0) bt = s.rings[off];
   else bt -= 2;
@@ -494,8 +501,16 @@ __device__ int decode_block_type_and_length(Dec &s, int tree_type, int ntypes) {
   return len;
 }
 __device__ void build_ctx_tree_base(Dec &s) {
-  if (s.lane < 64) s.l->ctx_tree_base[s.lane] = s.lit_group[s.ctx_map[s.ctx_map_slice + s.lane]];
   for (int k = s.lane; k < 512; k += 64) s.l->ctx_lut[k] = kRfcContextLut[s.clo1 + k];
+  const int tree = s.ctx_map[s.ctx_map_slice + s.lane];
+  if (s.tab16) {
+    // lut0[p1] | lut1[p2] with lut1 < 8 in every mode: one (p1, lut1[p2]) -> root table
+    const int root = s.tab_lds[tree];   // the literal group starts at 0
+    wave_sync();
+    for (int k = s.lane; k < 2048; k += 64) s.l->ctx_root[k] = (uint16_t)__shfl(root, s.l->ctx_lut[k >> 3] | (k & 7));
+  } else {
+    s.l->ctx_tree_base[s.lane] = s.lit_group[tree];
+  }
   wave_sync();
 }
 __device__ void lit_block_switch(Dec &s) {
@@ -598,7 +613,7 @@ __device__ int read_next_mb_header(Dec &s) {   // :631-678
 }
 
 __device__ int read_partition(Dec &s, int tt, int ntypes) {   // :679-704
-  int32_t *bt = s.l->block_trees;
+  int32_t *bt = s.bt;
   int off = bt[2 * tt];
   if (ntypes <= 1) {
     wave_sync();
@@ -624,16 +639,14 @@ __device__ int read_partition(Dec &s, int tt, int ntypes) {   // :679-704
 
 __device__ int decode_tree_group(Dec &s, int amax, int alimit, int n, int32_t *group) {
   int next = n;
-  // tables in LDS must not run past the LDS area (complete codes never do)
-  const int cap = s.lit_group == s.tab_lds ? (int)(s.tab_lds + kLdsTableInts - group) : kNoCap;
   for (int i = 0; i < n; i++) {
     if (s.lane == 0) group[i] = next;
     wave_sync();
-    int r = read_huffman_code(s, amax, alimit, group, cap, i);
+    int r = read_huffman_code(s, amax, alimit, group, kNoCap, i);
     if (r < 0) return r;
     next += r;
   }
-  return 0;
+  return next;   // the group's size in ints: its n roots and its tables
 }
 
 __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
@@ -674,14 +687,35 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
   // groups live back to back: literal, command, distance.  A metablock with few prefix
   // codes (the common case: one tree per alphabet) gets them in LDS, so every symbol
   // lookup is an LDS read instead of a dependent HBM load.
-  const int need = nlit_trees * (1 + 630) + s.n_cmd_types * (1 + 1080) + ndist_trees * (1 + 1080);
-  s.lit_group = need <= kLdsTableInts ? s.tab_lds : s.tab_hbm;
-  s.cmd_group = s.lit_group + (size_t)nlit_trees * (1 + 630);
+  s.lit_group = s.tab_hbm;
   if ((r = decode_tree_group(s, 256, 256, nlit_trees, s.lit_group)) < 0) return r;
-  s.dist_group = s.cmd_group + (size_t)s.n_cmd_types * (1 + 1080);
+  s.cmd_group = s.lit_group + r;
   if ((r = decode_tree_group(s, 704, 704, s.n_cmd_types, s.cmd_group)) < 0) return r;
+  s.dist_group = s.cmd_group + r;
   int dmax = 16 + s.ndirect + 2 * (24 << s.npostfix);
   if ((r = decode_tree_group(s, dmax, dmax, ndist_trees, s.dist_group)) < 0) return r;
+  // tables that fit go to LDS as 16-bit entries, roots made absolute
+  const int cmd_base = (int)(s.cmd_group - s.lit_group), dist_base = (int)(s.dist_group - s.lit_group);
+  const int total = dist_base + r;
+  s.tab16 = total <= kLdsTab;
+#ifdef MIB_PROF
+  if (s.lane == 0) atomicAdd(&g_prof[s.tab16 ? 6 : 7], 1ull);
+#endif
+  s.cmd_base = cmd_base;
+  s.dist_base = dist_base;
+  if (s.tab16) {
+    const int32_t *src = s.lit_group;
+    for (int k = s.lane; k < total; k += 64) {
+      const int v = src[k];
+      int o;
+      if (k < nlit_trees) o = v;
+      else if (k >= cmd_base && k < cmd_base + s.n_cmd_types) o = v + cmd_base;
+      else if (k >= dist_base && k < dist_base + ndist_trees) o = v + dist_base;
+      else o = ((v >> 16) << 12) | (v & 0xFFF);
+      s.tab_lds[k] = (uint16_t)o;
+    }
+    wave_sync();
+  }
   // calculateDistanceLut (:705-726), lane 0
   if (s.lane == 0) {
     int np = s.npostfix, nd = s.ndirect, postfix = 1 << np, b = 1, half = 0, k = 16;
@@ -954,16 +988,23 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         // generic (flat) access would have to drain first.
         int phase = s.running;
         GU8 *ring = (GU8 *)s.ring;
-        LU8 *win = (LU8 *)s.l->win;
+        LU16 *win16 = (LU16 *)s.l->win;
         LI32 *ctb = (LI32 *)s.l->ctx_tree_base;
         const int ring_cap = s.ring_cap, npostfix = s.npostfix, ndirect = s.ndirect, max_back = s.max_back;
-        const bool tab_lds = s.lit_group == s.tab_lds;
-        LI32 *cmd_l = (LI32 *)(tab_lds ? s.cmd_group : s.tab_lds), *dist_l = (LI32 *)(tab_lds ? s.dist_group : s.tab_lds),
-             *lit_l = (LI32 *)(tab_lds ? s.lit_group : s.tab_lds);
+        const bool tab_lds = s.tab16 != 0;
+        LU16 *t16 = (LU16 *)s.tab_lds;
+        LU16 *croot = (LU16 *)s.l->ctx_root;
+        const int cmd_base = __builtin_amdgcn_readfirstlane(s.cmd_base), dist_base = __builtin_amdgcn_readfirstlane(s.dist_base);
         GI32 *cmd_h = (GI32 *)s.cmd_group, *dist_h = (GI32 *)s.dist_group, *lit_h = (GI32 *)s.lit_group;
         const int lane = s.lane;
         const uint64_t guard_limit = s.guard_limit;
         int trivial = s.trivial_lit_ctx, lit_tree = s.lit_tree_idx;
+        const int ring_size = s.ring_size;
+        LU8 *clut = (LU8 *)s.l->ctx_lut;
+        // The last two output bytes (the literal context) live in registers: reading them
+        // back from the ring would wait for every outstanding ring store (vmcnt is in order).
+        int c1 = __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 1) & rmask]);
+        int c2b = __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 2) & rmask]);
         int dr0, dr1, dr2, dr3, dridx;   // the distance ring (rings[0..3], dist_rb_idx)
         uint32_t acc;
         int bo, ho, pos, j, mbl, insert_len, copy_len, dist_code, distance, cmd_blen, lit_blen, dist_blen, max_dist;
@@ -985,7 +1026,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
     s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist; s.guard = guard;              \
     s.rings[0] = dr0; s.rings[1] = dr1; s.rings[2] = dr2; s.rings[3] = dr3; s.dist_rb_idx = dridx;       \
   } while (0)
-#define LHALF(h) (((h) < 0 || (h) >= 2080) ? 0u : (uint32_t)U((int)((uint32_t)win[2 * (h)] | ((uint32_t)win[2 * (h) + 1] << 8))))
+#define LHALF(h) (((h) < 0 || (h) >= 2080) ? 0u : (uint32_t)U((int)win16[h]))
 #define LFILL16()                                     \
   do {                                                \
     if (bo >= 16) {                                   \
@@ -1017,6 +1058,20 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
           return lo | (lbits(n - 16) << 16);
         };
         auto dr_get = [&](int i) -> int { return i == 0 ? dr0 : i == 1 ? dr1 : i == 2 ? dr2 : dr3; };
+        auto lsym16 = [&](int root) -> int {   // read_symbol on a 16-bit LDS table with an absolute root
+          uint32_t v = acc >> (bo & 31);
+          int off = root + (int)(v & 0xFF);
+          const int e0 = U((int)t16[off]);
+          const int nb = e0 >> 12;
+          if (nb <= 8) {
+            bo += nb;
+            return e0 & 0xFFF;
+          }
+          off += (e0 & 0xFFF) + (int)((v & ((1u << nb) - 1u)) >> 8);
+          const int e1 = U((int)t16[off]);
+          bo += (e1 >> 12) + 8;
+          return e1 & 0xFFF;
+        };
         auto lsym = [&](auto g, int idx) -> int {   // read_symbol on registers
           int off = U(g[idx]);
           uint32_t v = acc >> (bo & 31);
@@ -1037,6 +1092,17 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         uint32_t dtrees = 0;   // the 4 distance trees of the current distance block type
         for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
         dtrees = U(dtrees);
+        // 16-bit tables: the command root and the 4 distance roots, absolute
+        int cmd_root = tab_lds ? U((int)t16[cmd_base + cmd_tree_idx]) : 0;
+        uint32_t droot01 = 0, droot23 = 0;
+        auto dist_roots = [&]() {
+          if (!tab_lds) return;
+          const int r0 = t16[dist_base + (dtrees & 0xFF)], r1 = t16[dist_base + ((dtrees >> 8) & 0xFF)];
+          const int r2 = t16[dist_base + ((dtrees >> 16) & 0xFF)], r3 = t16[dist_base + (dtrees >> 24)];
+          droot01 = U((int)((uint32_t)r0 | ((uint32_t)r1 << 16)));
+          droot23 = U((int)((uint32_t)r2 | ((uint32_t)r3 << 16)));
+        };
+        dist_roots();
 #ifdef MIB_PROF
         uint64_t prof[6] = {0, 0, 0, 0, 0, 0};
         uint64_t pt0 = __builtin_amdgcn_s_memtime();
@@ -1066,10 +1132,11 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               s.cmd_tree_idx = s.rings[7];
               HOT_LOAD();
               cmd_tree_idx = U(s.cmd_tree_idx);
+              if (tab_lds) cmd_root = U((int)t16[cmd_base + cmd_tree_idx]);
             }
             cmd_blen--;
             LFILL16();
-            const int sym = __builtin_amdgcn_readfirstlane(tab_lds ? lsym(cmd_l, cmd_tree_idx) : lsym(cmd_h, cmd_tree_idx));
+            const int sym = __builtin_amdgcn_readfirstlane(tab_lds ? lsym16(cmd_root) : lsym(cmd_h, cmd_tree_idx));
             const int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
             dist_code = kCmdLut[4 * sym + 3];
             LFILL16();
@@ -1099,6 +1166,53 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               if (d <= 0 && batch <= 0 && a > 0 && b > 0 && c2 > 0) batch = 1;   // Bug J fix
               lit_blen -= batch;
               const int end = j + batch;
+              // 16-bit LDS tables: the context's root is one lookup, (p1 << 3 | lut1[p2]),
+              // and lut1 of the literal just decoded is fetched beside it for the next one
+              auto lit_run16 = [&]() {
+                if (trivial) {
+                  const int root = U((int)t16[lit_tree]);
+                  while (j < end) {
+                    acc = (uint32_t)U((int)acc);
+                    bo = U(bo);
+                    ho = U(ho);
+                    j = U(j);
+                    pos = U(pos);
+                    LFILL16();
+                    const int val = lsym16(root);
+                    if (pos < ring_cap) ring[pos] = (uint8_t)val;
+                    pos++;
+                    j++;
+                    c2b = c1;
+                    c1 = val;
+                  }
+                  c1 = U(c1);
+                  c2b = U(c2b);
+                } else {
+                  int p1 = c1;
+                  const int p2 = c2b;
+                  LU8 *lut1 = clut + 256;
+                  int q2 = U((int)lut1[p2]);
+                  while (j < end) {
+                    acc = (uint32_t)U((int)acc);
+                    bo = U(bo);
+                    ho = U(ho);
+                    j = U(j);
+                    pos = U(pos);
+                    p1 = U(p1);
+                    q2 = U(q2);
+                    const int root = U((int)croot[(p1 << 3) | q2]);
+                    q2 = U((int)lut1[p1]);
+                    LFILL16();
+                    c2b = p1;
+                    p1 = U(lsym16(root));
+                    if (pos < ring_cap) ring[pos] = (uint8_t)p1;
+                    pos++;
+                    j++;
+                  }
+                  c1 = U(p1);
+                  c2b = U(c2b);
+                }
+              };
               auto lit_run = [&](auto g) {
                 if (trivial) {
                   const int root = U(g[lit_tree]);
@@ -1125,11 +1239,14 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                     if (pos < ring_cap) ring[pos] = (uint8_t)val;   // every lane: same byte, one transaction
                     pos++;
                     j++;
+                    c2b = c1;
+                    c1 = val;
                   }
+                  c1 = U(c1);
+                  c2b = U(c2b);
                 } else {
-                  int p1 = __builtin_amdgcn_readfirstlane(ring[(pos - 1) & rmask]);
-                  int p2 = __builtin_amdgcn_readfirstlane(ring[(pos - 2) & rmask]);
-                  LU8 *clut = (LU8 *)s.l->ctx_lut;
+                  int p1 = c1;
+                  int p2 = c2b;
                   while (j < end) {
                     const int ctx = U((int)(clut[p1] | clut[256 + p2]));
                     p2 = p1;
@@ -1153,9 +1270,11 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                     pos++;
                     j++;
                   }
+                  c1 = U(p1);
+                  c2b = U(p2);
                 }
               };
-              if (tab_lds) lit_run(lit_l);
+              if (tab_lds) lit_run16();
               else lit_run(lit_h);
               wave_sync();
               if (pos >= fence) {
@@ -1188,11 +1307,13 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                 dtrees = 0;
                 for (int q = 0; q < 4; q++) dtrees |= (uint32_t)s.dist_ctx_map[s.dist_ctx_map_slice + q] << (8 * q);
                 dtrees = U(dtrees);
+                dist_roots();
               }
               dist_blen--;
               LFILL16();
               const int dtree = (int)((dtrees >> (8 * dc)) & 0xFF);
-              dc = __builtin_amdgcn_readfirstlane(tab_lds ? lsym(dist_l, dtree) : lsym(dist_h, dtree));
+              const uint32_t dpair = dc < 2 ? droot01 : droot23;
+              dc = __builtin_amdgcn_readfirstlane(tab_lds ? lsym16((int)((dpair >> (16 * (dc & 1))) & 0xFFFF)) : lsym(dist_h, dtree));
               if (dc < 16) {
                 // short codes: ring slot and value offsets (kDistIdxOff / kDistValOff, packed)
                 const int idx = (dridx + (int)((0xfff0006cu >> (2 * dc)) & 3)) & 3;
@@ -1248,16 +1369,28 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
             const int dist = distance, cl = copy_len - j;
             const int src = (pos - dist) & rmask;
             if (src + cl < rmask && pos + cl < rmask) {
+              int lastv = 0;   // each lane's last copied byte: lanes (cl - 1) & 63, (cl - 2) & 63 end the copy
               if (dist >= cl) {
-                for (int k = lane; k < cl; k += 64) ring[pos + k] = ring[src + k];
+                for (int k = lane; k < cl; k += 64) {
+                  lastv = ring[src + k];
+                  ring[pos + k] = (uint8_t)lastv;
+                }
               } else {
                 int q = lane % dist;
                 const int qstep = 64 % dist;
                 for (int k = lane; k < cl; k += 64) {
-                  ring[pos + k] = ring[src + q];
+                  lastv = ring[src + q];
+                  ring[pos + k] = (uint8_t)lastv;
                   q += qstep;
                   if (q >= dist) q -= dist;
                 }
+              }
+              if (cl >= 2) {
+                c1 = __builtin_amdgcn_readlane(lastv, (cl - 1) & 63);
+                c2b = __builtin_amdgcn_readlane(lastv, (cl - 2) & 63);
+              } else if (cl == 1) {
+                c2b = c1;
+                c1 = __builtin_amdgcn_readlane(lastv, 0);
               }
               wave_sync();
               j = copy_len;
@@ -1270,8 +1403,8 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                 const int rem = copy_len - j;
                 const int room = fence - pos;
                 int chunk = rem < 4096 ? rem : 4096;
-                if (dist >= s.ring_size - 4096) chunk = rem < 64 ? rem : 64;
-                if (dist >= s.ring_size - 64) chunk = 1;
+                if (dist >= ring_size - 4096) chunk = rem < 64 ? rem : 64;
+                if (dist >= ring_size - 64) chunk = 1;
                 if (room < chunk) chunk = room;
                 if (chunk < 1) chunk = 1;
                 // byte p copies the byte dist back, or (overlap) its periodic image before pos
@@ -1294,6 +1427,8 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               }
               if (j < copy_len) cut = 1;
               if (cut) break;
+              c1 = __builtin_amdgcn_readfirstlane(ring[(pos - 1) & rmask]);
+              c2b = __builtin_amdgcn_readfirstlane(ring[(pos - 2) & rmask]);
             }
             phase = ST_MAIN_LOOP;
             PMARK(3);
@@ -1402,7 +1537,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
 __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int njobs, uint8_t *scratch,
                                                             uint64_t per_block, uint64_t ring_bytes) {
   __shared__ Lds lds;
-  __shared__ int32_t ltab[kLdsTableInts];
+  __shared__ uint16_t ltab[kLdsTab];
   uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
   uint8_t *ring = base;
   int32_t *tables = reinterpret_cast<int32_t *>(base + ring_bytes);
@@ -1410,6 +1545,7 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
   int8_t *dist_extra = reinterpret_cast<int8_t *>(ctx + kDecodeCtxBytes);
   int32_t *dist_offset = reinterpret_cast<int32_t *>(dist_extra + 1152);
   int32_t *ctxmap_table = dist_offset + 1152;
+  int32_t *block_trees = ctxmap_table + 1100;
   const int lane = threadIdx.x;
   for (int jb = blockIdx.x; jb < njobs; jb += gridDim.x) {
     DecJob job = jobs[jb];
@@ -1445,6 +1581,8 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     s.ring_scratch = ring;
     s.direct = 0;
     s.tab_lds = ltab;
+    s.tab16 = s.cmd_base = s.dist_base = 0;
+    s.bt = block_trees;
     s.tab_hbm = tables;
     s.lit_group = tables;
     s.cmd_group = tables;
@@ -1472,9 +1610,9 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     s.guard_limit = 64ull * (job.in_len + 64) * 8 + 4ull * job.out_cap + (1ull << 26);
     // initState (:160-178): fresh zeroed byteBuffer (its stale tail is observable) and block trees
     for (int i = lane; i < (int)sizeof(lds.win); i += 64) lds.win[i] = 0;
-    for (int i = lane; i <= kBlockTreesCap; i += 64) lds.block_trees[i] = 0;
+    for (int i = lane; i <= kBlockTreesCap; i += 64) block_trees[i] = 0;
     __syncthreads();
-    if (lane == 0) lds.block_trees[0] = 7;
+    if (lane == 0) block_trees[0] = 7;
     __syncthreads();
     int rc = prepare(s);
     if (rc >= 0) {
@@ -1533,8 +1671,8 @@ extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t 
 
 #ifdef MIB_PROF
 extern "C" int mib_debug_read_prof(unsigned long long *out) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_prof), sizeof(unsigned long long) * 6);
-  unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_prof), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   hipMemcpyToSymbol(HIP_SYMBOL(mib::g_prof), z, sizeof(z));
   return 0;
 }

@@ -278,7 +278,7 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
   for (auto &j : jobs) max_log = std::max(max_log, j.max_ring_log);
   uint64_t ring_bytes = ((uint64_t)1 << max_log) + 37 + 256;
   ring_bytes = (ring_bytes + 255) & ~(uint64_t)255;
-  uint64_t per_block = ring_bytes + mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4;
+  uint64_t per_block = ring_bytes + mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4 + 3092 * 4;   // ... ctx-map table, block trees
   per_block = (per_block + 255) & ~(uint64_t)255;
   int grid = (int)std::min<size_t>(k, 2048);
   int rc;
