@@ -17,18 +17,29 @@ namespace enc {
 constexpr uint32_t kSegBits = 16;
 constexpr uint32_t kSeg = 1u << kSegBits;     // 64 KiB parse segments
 constexpr int kMaxMatches = 6;                // staircase entries kept per position
+constexpr int kMatchRec = 8;                  // u32 per position record: 6 matches, count, 0 (one 32 B sector)
 constexpr uint32_t kMatchLenSat = 255;        // a match is (length:8 | distance:24); 255 = "255 or more"
 constexpr int kLongCopy = 200;                // copies longer than this are taken outright (the
                                               // reference's MAX_ZOPFLI_LEN is 325 at q11, 150 at q10,
                                               // enc-constants.ts:32-33)
 constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
 constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
-constexpr int kHdrBytes = 512;                // metablock header + context maps (without the trees)
+constexpr int kHdrBytes = 2048;               // metablock header: block-switch codes, context maps (not the trees)
 constexpr int kTreeBytes = 1024;              // one serialised prefix code
 constexpr int kLitCtx = 64;                   // literal contexts (RFC 7932 section 7.1)
 constexpr int kDistCtx = 4;                   // distance contexts (copy length 2, 3, 4, >4)
-constexpr int kTreeSlots = kLitCtx + 1 + kDistCtx;   // literal clusters | command | distance clusters
-constexpr int kCmdSlot = kLitCtx;
+// Block splitting (block-splitter.ts): up to kMaxBT block types per category, decided per
+// metablock over 8 KiB units of commands (kSubBits), kSubPerSeg units per parse segment.
+constexpr int kMaxBT = 4;
+constexpr uint32_t kSubBits = 13;
+constexpr int kSubPerSeg = 1 << (kSegBits - kSubBits);
+constexpr int kSubHist = 256 + 704 + 128;      // a unit's literal | command | distance-code histograms
+constexpr int kMaxLitTrees = 64;              // literal prefix codes per metablock (decoder tables stay in LDS)
+// code slots: literal (type, cluster) | command (type) | distance (type, cluster)
+constexpr int kLitSlots = kMaxBT * kLitCtx;
+constexpr int kCmdSlot = kLitSlots;
+constexpr int kDistSlot = kCmdSlot + kMaxBT;
+constexpr int kTreeSlots = kDistSlot + kMaxBT * kDistCtx;
 constexpr int kBlock = 256;                   // threads of the per-segment entropy / emit blocks
 
 struct Job {                // one stream (or streaming chunk) to encode
@@ -67,18 +78,30 @@ struct Seg {
   uint64_t bits;              // sizes
 };
 
-struct Mb {                   // one metablock: one block type per category, literal and
+struct Mb {                   // one metablock: block types per category, literal and
                               // distance context modelling (storeMetaBlock, metablock.ts:504-761)
   uint32_t job, start, end;   // stream-local
   uint32_t first_seg, nseg;
   uint32_t is_last;
   uint32_t hdr_bits;          // header bits before the prefix codes (incl. context maps)
   uint32_t ctx_mode;          // literal context mode (chooseContextMode, context.ts:180-227)
-  uint32_t nlit, ndist;       // literal / distance prefix codes (clusters)
-  uint8_t lit_cmap[kLitCtx];  // context -> literal code
-  uint8_t dist_cmap[kDistCtx];
+  uint32_t nbt[3];            // block types: literal, command, distance
+  uint32_t first_count[3];    // symbols in the first block of each category
+  uint32_t nlit_t[kMaxBT], ndist_t[kMaxBT];   // prefix codes (clusters) per literal / distance block type
+  uint8_t lit_cmap[kLitSlots];             // (type, context) -> literal code slot (type * 64 + cluster)
+  uint8_t dist_cmap[kMaxBT * kDistCtx];    // (type, context) -> distance code slot (type * 4 + cluster)
   uint32_t tree_bits[kTreeSlots];
   uint64_t bit_off;           // of the header, stream-relative
+};
+
+struct Unit {                 // one block-split unit: the commands of 8 KiB of a segment
+  uint32_t nsym[3];           // symbols: literals, commands, distance codes
+  uint32_t first[3];          // segment-relative index of its first command with a literal /
+                              // any / with a distance code (~0u: none)
+  uint32_t sw_count[3];       // block switch before that symbol: the new block's count (0: none)
+  uint8_t type[3];            // block type per category
+  uint8_t sw_code[3];         // the switch's block type code (RFC 7932 section 6)
+  uint16_t pad;
 };
 
 struct Cmd {                  // one command with its prefix codes (command.ts:29-208)
@@ -90,14 +113,28 @@ struct Cmd {                  // one command with its prefix codes (command.ts:2
 
 struct RawCmd { uint32_t ins, len, dist; };
 
-struct Codes {   // per metablock Huffman codes, literal and distance ones per cluster
-  uint8_t ld[kLitCtx][256];
-  uint16_t lc[kLitCtx][256];
-  uint8_t cd[704];
-  uint16_t cc[704];
-  uint8_t dd[kDistCtx][128];
-  uint16_t dcd[kDistCtx][128];
+struct Codes {   // per metablock Huffman codes by slot, and the block-switch codes
+  uint8_t ld[kLitSlots][256];
+  uint16_t lc[kLitSlots][256];
+  uint8_t cd[kMaxBT][704];
+  uint16_t cc[kMaxBT][704];
+  uint8_t dd[kMaxBT * kDistCtx][128];
+  uint16_t dcd[kMaxBT * kDistCtx][128];
+  uint8_t btd[3][kMaxBT + 2];   // block type codes
+  uint16_t btc[3][kMaxBT + 2];
+  uint8_t bcd[3][26];           // block count codes
+  uint16_t bcc[3][26];
 };
+
+// block count prefix codes (RFC 7932 section 6; engine.ts kBlockLengthOffset / NBits)
+static __device__ __constant__ uint32_t kBlkOff[26] = {1,   5,   9,   13,  17,  25,   33,   41,   49,   65,   81,    97,    113,
+                                                       145, 177, 209, 241, 305, 369, 497, 753, 1265, 2289, 4337, 8433, 16625};
+static __device__ __constant__ uint32_t kBlkBits[26] = {2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 7, 8, 9, 10, 11, 12, 13, 24};
+__device__ __forceinline__ int block_count_code(uint32_t count) {
+  int c = 0;
+  while (c < 25 && kBlkOff[c + 1] <= count) c++;
+  return c;
+}
 
 // ---------------------------------------------------------------- coding helpers (command.ts)
 __device__ __forceinline__ int log2floor_u(uint32_t v) { return 31 - __clz(v); }
@@ -220,22 +257,42 @@ __device__ __forceinline__ uint32_t prev2(const Job &jb, uint32_t p) {
 // distance context of a copy (RFC 7932 section 7.2; metablock.ts:621)
 __device__ __forceinline__ int dist_ctx(uint32_t copy_len) { return copy_len > 4 ? 3 : (int)copy_len - 2; }
 
-// Bits of one command: prefix code, extra bits, literals under their contexts, distance
-// (storeCommandExtra / storeSymbolWithContext, metablock.ts:273-287,392-501,720-745).
-// lut = the context mode's 512-entry slice of the RFC context lookup table.
+// the unit of command q (segment-relative position p of its insert): 8 KiB slices of the segment
+__device__ __forceinline__ uint32_t unit_of(const Seg &sg, uint32_t p) {
+  const uint32_t c = p < sg.start ? sg.start : (p >= sg.end ? sg.end - 1 : p);
+  return (c - sg.start) >> kSubBits;
+}
+// a block switch: block type code, block count code and its extra bits (storeBlockSwitch,
+// metablock.ts:204-220)
+__device__ __forceinline__ uint32_t switch_bits(const Codes &cd, int cat, const Unit &u) {
+  const int bc = block_count_code(u.sw_count[cat]);
+  return cd.btd[cat][u.sw_code[cat]] + cd.bcd[cat][bc] + kBlkBits[bc];
+}
+__device__ __forceinline__ bool switch_at(const Unit &u, int cat, uint32_t q) { return u.sw_count[cat] && q == u.first[cat]; }
+
+// Bits of command q of a segment: block switches, prefix code, extra bits, literals under
+// their contexts, distance (storeCommandExtra / storeSymbolWithContext / BlockEncoder,
+// metablock.ts:273-287,392-501,720-745).  lut = the context mode's 512-entry slice of the
+// RFC context lookup table; u = the command's block-split unit.
 __device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Mb &mb, const uint8_t *lut, const Cmd &c,
-                                                 const uint8_t *lits, uint32_t p12) {
+                                                 const uint8_t *lits, uint32_t p12, const Unit &u, uint32_t q) {
   const int ic = ins_code(c.ins);
   const int cc = copy_code(c.copy ? c.copy : 2);
-  uint32_t bits = cd.cd[c.cmd_prefix] + kInsExtra[ic] + kCopyExtra[cc];
+  const uint8_t *lmap = mb.lit_cmap + u.type[0] * kLitCtx;
+  uint32_t bits = cd.cd[u.type[1]][c.cmd_prefix] + kInsExtra[ic] + kCopyExtra[cc];
+  if (switch_at(u, 1, q)) bits += switch_bits(cd, 1, u);
+  if (switch_at(u, 0, q)) bits += switch_bits(cd, 0, u);
   uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
   for (uint32_t k = 0; k < c.ins; k++) {
     const uint32_t lit = lits[k];
-    bits += cd.ld[mb.lit_cmap[lut[p1] | lut[256 + p2]]][lit];
+    bits += cd.ld[lmap[lut[p1] | lut[256 + p2]]][lit];
     p2 = p1;
     p1 = lit;
   }
-  if (c.copy && c.cmd_prefix >= 128) bits += cd.dd[mb.dist_cmap[dist_ctx(c.copy)]][c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
+  if (c.copy && c.cmd_prefix >= 128) {
+    if (switch_at(u, 2, q)) bits += switch_bits(cd, 2, u);
+    bits += cd.dd[mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(c.copy)]][c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
+  }
   return bits;
 }
 
@@ -243,24 +300,28 @@ __device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Mb &mb, 
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys,
                       uint32_t *vals);
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
-                         int depth, uint32_t *matches, uint8_t *nmatch);
+                         int depth, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
-               const uint32_t *matches, const uint8_t *nmatch, uint64_t *choice);
+               const uint32_t *matches, uint64_t *choice);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
-                  uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd);
+                  uint32_t *cmd_pos, Unit *units, uint32_t *unit_h);
+void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes);
+void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
+                  const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd);
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds);
 void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs);
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd);
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr);
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
-                  const uint32_t *cmd_pos, const Codes *codes);
+                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units);
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out);
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
-                 const uint32_t *cmd_pos, const Codes *codes, const uint8_t *trees, const uint8_t *hdr, uint8_t *out);
+                 const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint8_t *trees, const uint8_t *hdr,
+                 uint8_t *out);
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out);
 void launch_pack(hipStream_t st, const Job *jobs, int njobs, const uint64_t *dst_off, const uint8_t *src, uint8_t *dst);
 

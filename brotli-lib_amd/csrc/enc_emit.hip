@@ -96,26 +96,43 @@ struct OrW {
   }
 };
 
+// a block switch: block type code, block count code, count extra bits (storeBlockSwitch,
+// metablock.ts:204-220)
+template <class W>
+__device__ __forceinline__ void put_switch(W &wr, const Codes &cd, int cat, const Unit &u) {
+  const int code = u.sw_code[cat], bc = block_count_code(u.sw_count[cat]);
+  wr.put(cd.btd[cat][code], cd.btc[cat][code]);
+  wr.put(cd.bcd[cat][bc], cd.bcc[cat][bc]);
+  wr.put((int)kBlkBits[bc], u.sw_count[cat] - kBlkOff[bc]);
+}
+
+// command q of its segment, with the block switches its unit places on it (same bits as
+// command_bits)
 template <class W>
 __device__ __forceinline__ void write_command(W &wr, const Codes &cd, const Mb &mb, const uint8_t *lut, const Cmd &k,
-                                              const uint8_t *lits, uint32_t p12) {
-  wr.put(cd.cd[k.cmd_prefix], cd.cc[k.cmd_prefix]);
+                                              const uint8_t *lits, uint32_t p12, const Unit &u, uint32_t q) {
+  if (switch_at(u, 1, q)) put_switch(wr, cd, 1, u);
+  const int ct = u.type[1];
+  wr.put(cd.cd[ct][k.cmd_prefix], cd.cc[ct][k.cmd_prefix]);
   const int ic = ins_code(k.ins);
   wr.put((int)kInsExtra[ic], k.ins - kInsBase[ic]);
   const uint32_t clen = k.copy ? k.copy : 2;
   const int cc = copy_code(clen);
   wr.put((int)kCopyExtra[cc], clen - kCopyBase[cc]);
+  if (switch_at(u, 0, q)) put_switch(wr, cd, 0, u);
+  const uint8_t *lmap = mb.lit_cmap + u.type[0] * kLitCtx;
   uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
   for (uint32_t t = 0; t < k.ins; t++) {
     const uint32_t lit = lits[t];
-    const int tree = mb.lit_cmap[lut[p1] | lut[256 + p2]];
+    const int tree = lmap[lut[p1] | lut[256 + p2]];
     wr.put(cd.ld[tree][lit], cd.lc[tree][lit]);
     p2 = p1;
     p1 = lit;
   }
   if (k.copy && k.cmd_prefix >= 128) {
+    if (switch_at(u, 2, q)) put_switch(wr, cd, 2, u);
     const uint32_t dcode = k.dist_prefix & 0x3FF;
-    const int tree = mb.dist_cmap[dist_ctx(k.copy)];
+    const int tree = mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(k.copy)];
     wr.put(cd.dd[tree][dcode], cd.dcd[tree][dcode]);
     wr.put(k.dist_prefix >> 10, k.dist_extra);
   }
@@ -127,7 +144,8 @@ __device__ __forceinline__ void write_command(W &wr, const Codes &cd, const Mb &
 // insert of tens of thousands of literals) is ORed straight into global memory.
 constexpr int kWinWords = 8192;   // 32 KiB = 262144 bits
 __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
-                                                      const uint32_t *cmd_pos, const Codes *codes, uint8_t *out) {
+                                                      const uint32_t *cmd_pos, const Codes *codes, const Unit *units,
+                                                      uint8_t *out) {
   typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t win[kWinWords];
@@ -143,14 +161,17 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   uint64_t bitpos = sg.bit_off;
   for (uint32_t base = 0; base < n; base += kBlock) {
     const uint32_t q = base + t;
     Cmd k;
+    Unit u;
     uint32_t bits = 0;
     if (q < n) {
       k = c[q];
-      bits = command_bits(cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]));
+      u = un[unit_of(sg, cp[q])];
+      bits = command_bits(cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]), u, q);
     }
     uint32_t off, total;
     Scan(scan_tmp).ExclusiveSum(bits, off, total);
@@ -165,13 +186,13 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
       if (fits) {
         OrW<false> wr;
         wr.init(win, rel0 + off);
-        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]));
+        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]), u, q);
         wr.finish();
         atomicMax(&sh_fit_end, rel0 + off + bits);
       } else {
         OrW<true> wr;
         wr.init(words, bitpos + off);
-        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]));
+        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]), u, q);
         wr.finish();
       }
     }
@@ -255,9 +276,10 @@ __global__ void pack_kernel(const Job *jobs, const uint64_t *dst_off, const uint
 
 
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
-                 const uint32_t *cmd_pos, const Codes *codes, const uint8_t *trees, const uint8_t *hdr, uint8_t *out) {
+                 const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint8_t *trees, const uint8_t *hdr,
+                 uint8_t *out) {
   hipLaunchKernelGGL(headers_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, trees, out);
-  hipLaunchKernelGGL(emit_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, out);
+  hipLaunchKernelGGL(emit_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, out);
 }
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out) {
   hipLaunchKernelGGL(uncompressed_kernel, dim3((unsigned)njobs), dim3(256), 0, st, jobs, njobs, out);

@@ -79,27 +79,28 @@ __global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs) {
   mb.ctx_mode = (uint32_t)mode;
 }
 
-// ---------------------------------------------------------------- codes + histograms
+// ---------------------------------------------------------------- codes + unit histograms
 // Block per segment: command prefix codes (getInsertLengthCode / getCopyLengthCode /
 // combineLengthCodes / prefixEncodeCopyDistance, command.ts:29-179), command positions
-// (block scan), and the metablock's histograms: literals per context (64), commands,
-// distances per distance context (4) -- in LDS, then one global atomic per non-zero bin
-// (the histogram pass of storeMetaBlock, metablock.ts:580-640).
+// (block scan), and per block-split unit (8 KiB of the segment's commands) its order-0
+// literal, command and distance-code histograms, symbol counts and first commands -- the
+// symbol streams splitBlock works on (block-splitter.ts:394-464).
 __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const RawCmd *raw,
-                                                       Cmd *cmds, uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc,
-                                                       uint32_t *hd) {
+                                                       Cmd *cmds, uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
   typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
-  __shared__ uint32_t sh_l[kLitCtx * 256], sh_c[704], sh_d[kDistCtx * 128];
+  __shared__ uint32_t sh_h[kSubPerSeg * kSubHist];
+  __shared__ uint32_t sh_n[kSubPerSeg][3], sh_first[kSubPerSeg][3];
   __shared__ uint32_t sh_run;
   const Seg sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
-  const uint8_t *lut = kRfcContextLut + (mbs[sg.mb].ctx_mode << 9);
   const int t = threadIdx.x;
-  for (int i = t; i < 704; i += kBlock) sh_c[i] = 0;
-  for (int i = t; i < kLitCtx * 256; i += kBlock) sh_l[i] = 0;
-  for (int i = t; i < kDistCtx * 128; i += kBlock) sh_d[i] = 0;
+  for (int i = t; i < kSubPerSeg * kSubHist; i += kBlock) sh_h[i] = 0;
+  if (t < kSubPerSeg * 3) {
+    sh_n[t / 3][t % 3] = 0;
+    sh_first[t / 3][t % 3] = ~0u;
+  }
   if (t == 0) sh_run = sg.start - sg.carry_in;
   __syncthreads();
   const RawCmd *r = raw + sg.cmd_off;
@@ -131,6 +132,8 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
       c.dist_extra = 0;
       c.dist_prefix = 0;
       const int ic = ins_code(ins);
+      const uint32_t u = unit_of(sg, pos);
+      uint32_t *hu = sh_h + u * kSubHist;
       if (len) {
         const uint32_t dcode = d == prevd ? 0 : d + 15;
         uint32_t extra;
@@ -138,31 +141,107 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
         c.dist_extra = extra;
         c.dist_prefix = (uint16_t)dp;
         c.cmd_prefix = (uint16_t)combine_codes(ic, copy_code(len), dcode == 0);
-        if (c.cmd_prefix >= 128) atomicAdd(&sh_d[dist_ctx(len) * 128 + (dp & 0x3FF)], 1u);
+        if (c.cmd_prefix >= 128) {
+          atomicAdd(&hu[256 + 704 + (dp & 0x3FF)], 1u);
+          atomicAdd(&sh_n[u][2], 1u);
+          atomicMin(&sh_first[u][2], q);
+        }
       } else {   // insert-only: copy code 0 with the implicit last distance when possible
         c.cmd_prefix = (uint16_t)combine_codes(ic, 0, ic < 8);
       }
-      atomicAdd(&sh_c[c.cmd_prefix], 1u);
+      atomicAdd(&hu[256 + c.cmd_prefix], 1u);
+      atomicAdd(&sh_n[u][1], 1u);
+      atomicMin(&sh_first[u][1], q);
+      if (ins) {
+        atomicAdd(&sh_n[u][0], ins);
+        atomicMin(&sh_first[u][0], q);
+      }
       out[q] = c;
       outp[q] = pos;
-      const uint32_t p12 = prev2(jb, pos);
+      for (uint32_t k = 0; k < ins; k++) atomicAdd(&hu[jb.data[pos + k]], 1u);
+    }
+    __syncthreads();
+  }
+  const uint32_t u0 = blockIdx.x * kSubPerSeg;
+  uint32_t *gh = unit_h + (size_t)u0 * kSubHist;
+  for (int i = t; i < kSubPerSeg * kSubHist; i += kBlock) gh[i] = sh_h[i];
+  if (t < kSubPerSeg) {
+    Unit un;
+    for (int c = 0; c < 3; c++) {
+      un.nsym[c] = sh_n[t][c];
+      un.first[c] = sh_first[t][c];
+      un.sw_count[c] = 0;
+      un.type[c] = 0;
+      un.sw_code[c] = 0;
+    }
+    un.pad = 0;
+    units[u0 + t] = un;
+  }
+}
+
+// ---------------------------------------------------------------- histograms by block type
+// Block per segment, after the split: literal histograms per (block type, context), command
+// histograms per block type, distance-code histograms per (block type, distance context),
+// accumulated in LDS (literals one block type at a time) and added to the metablock's with
+// one global atomic per non-zero bin (the histogram pass of storeMetaBlock, metablock.ts:580-640).
+__global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
+                                                       const uint32_t *cmd_pos, const Unit *units, uint32_t *hl,
+                                                       uint32_t *hc, uint32_t *hd) {
+  __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
+  __shared__ uint8_t ut[kSubPerSeg][3];
+  uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
+  const Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  if (jb.uncompressed) return;
+  const Mb &mb = mbs[sg.mb];
+  const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
+  const int t = threadIdx.x;
+  const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
+  if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
+  for (int i = t; i < kMaxBT * 704; i += kBlock) sh_c[i] = 0;
+  for (int i = t; i < kMaxBT * kDistCtx * 128; i += kBlock) sh_d[i] = 0;
+  __syncthreads();
+  const Cmd *c = cmds + sg.cmd_off;
+  const uint32_t *cp = cmd_pos + sg.cmd_off;
+  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  for (uint32_t q = t; q < n; q += kBlock) {
+    const Cmd k = c[q];
+    const uint32_t u = unit_of(sg, cp[q]);
+    atomicAdd(&sh_c[ut[u][1] * 704 + k.cmd_prefix], 1u);
+    if (k.copy && k.cmd_prefix >= 128) atomicAdd(&sh_d[(ut[u][2] * kDistCtx + dist_ctx(k.copy)) * 128 + (k.dist_prefix & 0x3FF)], 1u);
+  }
+  const uint32_t m = sg.mb;
+  __syncthreads();
+  for (int i = t; i < kMaxBT * 704; i += kBlock)
+    if (sh_c[i]) atomicAdd(&hc[(size_t)m * kMaxBT * 704 + i], sh_c[i]);
+  for (int i = t; i < kMaxBT * kDistCtx * 128; i += kBlock)
+    if (sh_d[i]) atomicAdd(&hd[(size_t)m * kMaxBT * kDistCtx * 128 + i], sh_d[i]);
+  __syncthreads();
+  uint32_t present = 0;   // literal block types used by this segment
+  for (int u = 0; u < kSubPerSeg; u++) present |= 1u << ut[u][0];
+  for (int ty = 0; ty < kMaxBT; ty++) {
+    if (!(present >> ty & 1)) continue;
+    for (int i = t; i < kLitCtx * 256; i += kBlock) sh_l[i] = 0;
+    __syncthreads();
+    for (uint32_t q = t; q < n; q += kBlock) {
+      const uint32_t p = cp[q];
+      if (ut[unit_of(sg, p)][0] != ty) continue;
+      const Cmd k = c[q];
+      const uint32_t p12 = prev2(jb, p);
       uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
-      for (uint32_t k = 0; k < ins; k++) {
-        const uint32_t lit = jb.data[pos + k];
+      for (uint32_t x = 0; x < k.ins; x++) {
+        const uint32_t lit = jb.data[p + x];
         atomicAdd(&sh_l[(lut[p1] | lut[256 + p2]) * 256 + lit], 1u);
         p2 = p1;
         p1 = lit;
       }
     }
     __syncthreads();
+    uint32_t *dst = hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256;
+    for (int i = t; i < kLitCtx * 256; i += kBlock)
+      if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
+    __syncthreads();
   }
-  const uint32_t m = sg.mb;
-  for (int i = t; i < 704; i += kBlock)
-    if (sh_c[i]) atomicAdd(&hc[m * 704 + i], sh_c[i]);
-  for (int i = t; i < kLitCtx * 256; i += kBlock)
-    if (sh_l[i]) atomicAdd(&hl[(size_t)m * kLitCtx * 256 + i], sh_l[i]);
-  for (int i = t; i < kDistCtx * 128; i += kBlock)
-    if (sh_d[i]) atomicAdd(&hd[(size_t)m * kDistCtx * 128 + i], sh_d[i]);
 }
 
 // ---------------------------------------------------------------- clustering
@@ -178,6 +257,9 @@ __device__ __forceinline__ float hist_cost(float bits, int nnz) {
   return bits + 40.f + 3.5f * nnz;
 }
 
+// Block per (metablock, literal | distance, block type): the type's context histograms.  A
+// literal block type may keep at most kMaxLitTrees / (literal block types) codes: past that
+// cap the cheapest merge is taken even when it costs bits.
 __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
   constexpr int kMaxH = kLitCtx;
   __shared__ uint32_t h[kMaxH][256];
@@ -186,16 +268,26 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
   __shared__ int alive[kMaxH], label[kMaxH];
   __shared__ float red_v[256];
   __shared__ int red_i[256];
-  __shared__ int sh_best;
-  const int m = blockIdx.x >> 1, kind = blockIdx.x & 1;
+  __shared__ int sh_best, sh_alive;
+  const int m = blockIdx.x / (2 * kMaxBT), kind = (blockIdx.x / kMaxBT) & 1, ty = blockIdx.x % kMaxBT;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
+  const int nbt = (int)(kind == 0 ? mb.nbt[0] : mb.nbt[2]);
+  if (ty >= nbt) {
+    if (t == 0) {
+      if (kind == 0) mb.nlit_t[ty] = 0;
+      else mb.ndist_t[ty] = 0;
+    }
+    return;
+  }
   const int nh = kind == 0 ? kLitCtx : kDistCtx;
+  const int cap = kind == 0 ? kMaxLitTrees / nbt : kDistCtx;
   const int A = kind == 0 ? 256 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
   const int stride = kind == 0 ? 256 : 128;
-  uint32_t *src = kind == 0 ? hl + (size_t)m * kLitCtx * 256 : hd + (size_t)m * kDistCtx * 128;
+  uint32_t *src = kind == 0 ? hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256
+                            : hd + ((size_t)m * kMaxBT * kDistCtx + ty * kDistCtx) * 128;
   for (int i = t; i < nh * 256; i += 256) {
     const int a = i / 256, x = i % 256;
     h[a][x] = x < A ? src[a * stride + x] : 0u;
@@ -219,6 +311,11 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
     label[a] = a;
   }
   __syncthreads();
+  if (t == 0) {
+    int na = 0;
+    for (int a = 0; a < nh; a++) na += alive[a];
+    sh_alive = na;
+  }
   // savings of every pair
   auto pair_saving = [&](int a, int b) -> float {
     float sum = 0.f, ent = 0.f;
@@ -261,7 +358,7 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
       }
       __syncthreads();
     }
-    if (t == 0) sh_best = red_v[0] > 0.f ? red_i[0] : -1;
+    if (t == 0) sh_best = (red_v[0] > 0.f || (sh_alive > cap && red_v[0] > -1e29f)) ? red_i[0] : -1;
     __syncthreads();
     const int best = sh_best;
     if (best < 0) break;
@@ -271,6 +368,7 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
     if (t == 0) {
       cost[a] = cost[a] + cost[b] - save[a][b];
       alive[b] = 0;
+      sh_alive--;
       for (int q = 0; q < nh; q++)
         if (label[q] == b) label[q] = a;
     }
@@ -294,12 +392,12 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
       if (alive[label[q]] && rep_id[label[q]] < 0) rep_id[label[q]] = k++;
     for (int q = 0; q < nh; q++) {
       const int c = alive[label[q]] ? rep_id[label[q]] : 0;
-      if (kind == 0) mb.lit_cmap[q] = (uint8_t)c;
-      else mb.dist_cmap[q] = (uint8_t)c;
+      if (kind == 0) mb.lit_cmap[ty * kLitCtx + q] = (uint8_t)(ty * kLitCtx + c);
+      else mb.dist_cmap[ty * kDistCtx + q] = (uint8_t)(ty * kDistCtx + c);
     }
     if (k == 0) k = 1;
-    if (kind == 0) mb.nlit = (uint32_t)k;
-    else mb.ndist = (uint32_t)k;
+    if (kind == 0) mb.nlit_t[ty] = (uint32_t)k;
+    else mb.ndist_t[ty] = (uint32_t)k;
   }
   __syncthreads();
   // clustered histograms, in place: cluster c <- its representative's merged histogram
@@ -630,9 +728,8 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
   }
 }
 
-// Block (one wave) per (metablock, code slot): slots 0..63 the literal clusters, 64 the
-// command code, 65..68 the distance clusters; slots beyond the metablock's cluster counts
-// are empty.
+// Block (one wave) per (metablock, code slot): literal (block type, cluster), command (block
+// type), distance (block type, cluster); slots beyond the metablock's counts are empty.
 __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                                                      const uint32_t *hc, const uint32_t *hd, Codes *codes,
                                                      uint8_t *trees) {
@@ -650,15 +747,18 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
-  const bool lit = t < kCmdSlot, dist = t > kCmdSlot;
-  const int cl = dist ? t - kCmdSlot - 1 : t;
-  if ((lit && cl >= (int)mb.nlit) || (dist && cl >= (int)mb.ndist)) {
+  const bool lit = t < kCmdSlot, dist = t >= kDistSlot;
+  const int cl = lit ? t : dist ? t - kDistSlot : t - kCmdSlot;   // slot within its alphabet
+  const bool used = lit ? (cl / kLitCtx < (int)mb.nbt[0] && cl % kLitCtx < (int)mb.nlit_t[cl / kLitCtx])
+                        : dist ? (cl / kDistCtx < (int)mb.nbt[2] && cl % kDistCtx < (int)mb.ndist_t[cl / kDistCtx])
+                               : cl < (int)mb.nbt[1];
+  if (!used) {
     if (lane == 0) mb.tree_bits[t] = 0;
     return;
   }
   const int asize = lit ? 256 : !dist ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
-  const uint32_t *src = lit ? hl + ((size_t)m * kLitCtx + cl) * 256 : !dist ? hc + (size_t)m * 704
-                                                                          : hd + ((size_t)m * kDistCtx + cl) * 128;
+  const uint32_t *src = lit ? hl + ((size_t)m * kLitSlots + cl) * 256 : !dist ? hc + ((size_t)m * kMaxBT + cl) * 704
+                                                                          : hd + ((size_t)m * kMaxBT * kDistCtx + cl) * 128;
   for (int i = lane; i < asize; i += 64) {
     h[i] = src[i];
     depth[i] = 0;
@@ -712,12 +812,274 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   uint8_t *dst = trees + ((size_t)m * kTreeSlots + t) * kTreeBytes;
   for (int i = lane; i < kTreeBytes; i += 64) dst[i] = buf[i];
   Codes &cd = codes[m];
-  uint8_t *dd = lit ? cd.ld[cl] : !dist ? cd.cd : cd.dd[cl];
-  uint16_t *cc = lit ? cd.lc[cl] : !dist ? cd.cc : cd.dcd[cl];
+  uint8_t *dd = lit ? cd.ld[cl] : !dist ? cd.cd[cl] : cd.dd[cl];
+  uint16_t *cc = lit ? cd.lc[cl] : !dist ? cd.cc[cl] : cd.dcd[cl];
   for (int i = lane; i < asize; i += 64) {
     dd[i] = depth[i];
     cc[i] = code[i];
   }
+}
+
+
+// ---------------------------------------------------------------- block split: block per (metablock, category)
+// splitByteVector / findBlocks / clusterBlocks (block-splitter.ts:117-464) restated over
+// block-split units (8 KiB of commands) instead of single symbols: kMaxBT block types are
+// seeded as contiguous runs of units, then refined kSplitIters times -- type histograms,
+// per-symbol bit costs (log2 total - log2 count, block-splitter.ts:150-160), each unit's cost
+// under every type, and a shortest path over the units with the reference's block switch
+// cost (26.0 bits literals, 28.1 commands / distances, :431-459).  The split is kept when it
+// beats one block type by more than its header cost.  Types are renumbered by first use (the
+// first block is type 0), then the block switches are laid out: each switch sits before the
+// first symbol of its unit and carries the type code (second-to-last / last + 1 / explicit,
+// RFC 7932 section 6) and the count of the new block; the block type and count prefix codes
+// are built here (serial, <= 26 symbols).
+constexpr int kMaxUnits = (int)(kMaxMetablock >> kSubBits);
+constexpr int kSplitIters = 4;
+__device__ __forceinline__ float sym_bits(uint32_t c, float log_total) {
+  return c ? log_total - __log2f((float)c) : log_total + 2.f;
+}
+__global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h,
+                                                    Codes *codes) {
+  __shared__ uint32_t th[kMaxBT][704];
+  __shared__ float bc[kMaxBT][704];
+  __shared__ float ucost[kMaxUnits][kMaxBT];
+  __shared__ uint8_t asg[kMaxUnits], bp[kMaxUnits];
+  __shared__ uint32_t ns[kMaxUnits];   // the units' symbol counts (the serial steps read them from LDS)
+  __shared__ uint32_t tot[kMaxBT];
+  __shared__ float red[256];
+  __shared__ int sh_ne, sh_keep;
+  const int m = blockIdx.x / 3, cat = blockIdx.x % 3;
+  Mb &mb = mbs[m];
+  const Job &jb = jobs[mb.job];
+  if (jb.uncompressed) return;
+  const int t = threadIdx.x;
+  const int A = cat == 0 ? 256 : cat == 1 ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
+  const int hoff = cat == 0 ? 0 : cat == 1 ? 256 : 256 + 704;
+  const float sw_cost = cat == 0 ? 26.0f : 28.1f;
+  const uint32_t u0 = mb.first_seg * kSubPerSeg;
+  const int nu = (int)mb.nseg * kSubPerSeg;
+  Unit *U = units + u0;
+  const uint32_t *H = unit_h + (size_t)u0 * kSubHist + hoff;
+  for (int i = t; i < nu; i += 256) ns[i] = U[i].nsym[cat];
+  __syncthreads();
+  // seed: the non-empty units in kMaxBT contiguous runs
+  if (t == 0) {
+    int ne = 0;
+    for (int i = 0; i < nu; i++) ne += ns[i] ? 1 : 0;
+    int r = 0;
+    for (int i = 0; i < nu; i++) {
+      asg[i] = (uint8_t)(ne ? (r * kMaxBT) / ne : 0);
+      if (ns[i]) r++;
+    }
+    sh_ne = ne;
+  }
+  __syncthreads();
+  const int ne = sh_ne;
+  int keep = 0;
+  if (ne >= 2 * kMaxBT) {
+    float base_cost = 0.f;
+    for (int it = 0; it <= kSplitIters; it++) {
+      // type histograms (it == kSplitIters: of the final assignment); one type = all units
+      for (int x = t; x < A; x += 256) {
+        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        for (int i = 0; i < nu; i++) {
+          const uint32_t v = H[(size_t)i * kSubHist + x];
+          const int a = asg[i];
+          s0 += a == 0 ? v : 0u;
+          s1 += a == 1 ? v : 0u;
+          s2 += a == 2 ? v : 0u;
+          s3 += a == 3 ? v : 0u;
+        }
+        th[0][x] = s0;
+        th[1][x] = s1;
+        th[2][x] = s2;
+        th[3][x] = s3;
+      }
+      __syncthreads();
+      if (t < kMaxBT) {
+        uint32_t s = 0;
+        for (int x = 0; x < A; x++) s += th[t][x];
+        tot[t] = s;
+      }
+      __syncthreads();
+      if (it == 0) {   // the one-type baseline: entropy of the merged histogram + one code's header
+        float part = 0.f;
+        const uint32_t all = tot[0] + tot[1] + tot[2] + tot[3];
+        const float la = __log2f((float)all);
+        int nz = 0;
+        for (int x = t; x < A; x += 256) {
+          const uint32_t c = th[0][x] + th[1][x] + th[2][x] + th[3][x];
+          if (c) {
+            part += (float)c * (la - __log2f((float)c));
+            nz++;
+          }
+        }
+        red[t] = part + 3.5f * (float)nz;
+        __syncthreads();
+        for (int o = 128; o; o >>= 1) {
+          if (t < o) red[t] += red[t + o];
+          __syncthreads();
+        }
+        base_cost = red[0] + 40.f;
+        __syncthreads();
+      }
+      for (int x = t; x < A; x += 256)
+        for (int q = 0; q < kMaxBT; q++) bc[q][x] = tot[q] ? sym_bits(th[q][x], __log2f((float)tot[q])) : 1e9f;
+      __syncthreads();
+      if (it == kSplitIters) break;
+      // every unit's bits under every type: a wave per unit, lanes over the symbols
+      for (int i = t >> 6; i < nu; i += 4) {
+        float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+        if (ns[i]) {
+          const uint32_t *h = H + (size_t)i * kSubHist;
+          for (int x = t & 63; x < A; x += 64) {
+            const float v = (float)h[x];
+            c0 += v * bc[0][x];
+            c1 += v * bc[1][x];
+            c2 += v * bc[2][x];
+            c3 += v * bc[3][x];
+          }
+          for (int o = 32; o; o >>= 1) {
+            c0 += __shfl_xor(c0, o);
+            c1 += __shfl_xor(c1, o);
+            c2 += __shfl_xor(c2, o);
+            c3 += __shfl_xor(c3, o);
+          }
+        }
+        if ((t & 63) == 0) {
+          ucost[i][0] = c0;
+          ucost[i][1] = c1;
+          ucost[i][2] = c2;
+          ucost[i][3] = c3;
+        }
+      }
+      __syncthreads();
+      // shortest path over the non-empty units with the switch cost (findBlocks' DP)
+      if (t == 0) {
+        float dp[kMaxBT] = {0.f, 0.f, 0.f, 0.f};
+        int last = -1;
+        for (int i = 0; i < nu; i++) {
+          if (!ns[i]) continue;
+          float best = 1e30f;
+          int bq = 0;
+          for (int q = 0; q < kMaxBT; q++)
+            if (dp[q] < best) {
+              best = dp[q];
+              bq = q;
+            }
+          uint8_t b = 0;
+          float nd[kMaxBT];
+          for (int q = 0; q < kMaxBT; q++) {
+            const float stay = dp[q], sw = best + sw_cost;
+            const bool s = last >= 0 && sw < stay;
+            nd[q] = (s ? sw : stay) + ucost[i][q];
+            if (s) b |= (uint8_t)(1 << q);
+          }
+          bp[i] = (uint8_t)(b | (bq << 4));
+          for (int q = 0; q < kMaxBT; q++) dp[q] = nd[q];
+          last = i;
+        }
+        int cur = 0;
+        for (int q = 1; q < kMaxBT; q++)
+          if (dp[q] < dp[cur]) cur = q;
+        for (int i = nu - 1; i >= 0; i--) {
+          if (!ns[i]) continue;
+          asg[i] = (uint8_t)cur;
+          if (bp[i] >> cur & 1) cur = bp[i] >> 4;
+        }
+        int prev = asg[0];
+        for (int i = 0; i < nu; i++) {   // empty units follow their predecessor
+          if (!ns[i]) asg[i] = (uint8_t)prev;
+          prev = asg[i];
+        }
+      }
+      __syncthreads();
+    }
+    // the split's cost: unit bits under the final histograms, switches, one code header per type
+    float part = 0.f;
+    for (int i = t >> 6; i < nu; i += 4) {
+      if (!ns[i]) continue;
+      const uint32_t *h = H + (size_t)i * kSubHist;
+      const int q = asg[i];
+      for (int x = t & 63; x < A; x += 64) part += (float)h[x] * bc[q][x];
+    }
+    for (int x = t; x < A; x += 256)
+      for (int q = 0; q < kMaxBT; q++) part += th[q][x] ? 3.5f : 0.f;
+    red[t] = part;
+    __syncthreads();
+    for (int o = 128; o; o >>= 1) {
+      if (t < o) red[t] += red[t + o];
+      __syncthreads();
+    }
+    if (t == 0) {
+      int nsw = 0, used = 0, prev = -1;
+      for (int i = 0; i < nu; i++) {
+        if (!ns[i]) continue;
+        if (prev >= 0 && asg[i] != prev) nsw++;
+        prev = asg[i];
+      }
+      for (int q = 0; q < kMaxBT; q++) used += tot[q] ? 1 : 0;
+      const float split_cost = red[0] + 40.f * (float)used + sw_cost * (float)nsw + 60.f;
+      sh_keep = (used > 1 && split_cost < base_cost) ? 1 : 0;
+    }
+    __syncthreads();
+    keep = sh_keep;
+  }
+  if (t != 0) return;
+  Codes &cd = codes[m];
+  if (!keep) {
+    for (int i = 0; i < nu; i++) {
+      U[i].type[cat] = 0;
+      U[i].sw_count[cat] = 0;
+    }
+    mb.nbt[cat] = 1;
+    mb.first_count[cat] = 0;
+    return;
+  }
+  // renumber by first use
+  int map[kMaxBT] = {-1, -1, -1, -1}, nt = 0;
+  for (int i = 0; i < nu; i++)
+    if (ns[i] && map[asg[i]] < 0) map[asg[i]] = nt++;
+  // lay out the switches
+  uint32_t hcode[kMaxBT + 2] = {0, 0, 0, 0, 0, 0}, hcount[26];
+  for (int q = 0; q < 26; q++) hcount[q] = 0;
+  int cur = 0, last = 0, second = 1, open = -1;   // open: unit of the current block's switch (-1: the header's)
+  uint32_t count = 0;
+  bool started = false;
+  for (int i = 0; i < nu; i++) {
+    Unit &u = U[i];
+    u.sw_count[cat] = 0;
+    const uint32_t nsy = ns[i];
+    if (!nsy) {
+      u.type[cat] = (uint8_t)cur;
+      continue;
+    }
+    const int ty = map[asg[i]];
+    if (started && ty != cur) {
+      if (open < 0) mb.first_count[cat] = count;
+      else U[open].sw_count[cat] = count;
+      hcount[block_count_code(count)]++;
+      const int code = ty == second ? 0 : ty == (last + 1) % nt ? 1 : ty + 2;
+      u.sw_code[cat] = (uint8_t)code;
+      hcode[code]++;
+      second = last;
+      last = ty;
+      cur = ty;
+      open = i;
+      count = 0;
+    }
+    started = true;
+    u.type[cat] = (uint8_t)ty;
+    count += nsy;
+  }
+  if (open < 0) mb.first_count[cat] = count;
+  else U[open].sw_count[cat] = count;
+  hcount[block_count_code(count)]++;
+  mb.nbt[cat] = (uint32_t)nt;
+  serial_depths(hcode, nt + 2, 15, cd.btd[cat]);
+  depths_to_codes(cd.btd[cat], nt + 2, cd.btc[cat]);
+  serial_depths(hcount, 26, 15, cd.bcd[cat]);
+  depths_to_codes(cd.bcd[cat], 26, cd.bcc[cat]);
 }
 
 // encodeContextMap (context-map.ts:114-170): NTREES, then (NTREES > 1) move-to-front, runs
@@ -726,9 +1088,9 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
 __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int ntrees) {
   put_varlen_u8(w, ntrees - 1);
   if (ntrees <= 1) return;
-  uint8_t mtf[kLitCtx];
+  uint8_t mtf[kMaxLitTrees];
   for (int i = 0; i < ntrees; i++) mtf[i] = (uint8_t)i;
-  uint8_t v[kLitCtx];
+  uint8_t v[kLitSlots];
   for (int i = 0; i < size; i++) {
     int idx = 0;
     while (mtf[idx] != cmap[i]) idx++;
@@ -746,8 +1108,8 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
   int rlemax = 0;
   while ((2 << rlemax) <= maxrun && rlemax < 16) rlemax++;   // largest p with 2^p <= maxrun
   // symbols (code, extra bits, extra)
-  uint8_t sym[kLitCtx], nb[kLitCtx];
-  uint16_t ex[kLitCtx];
+  uint8_t sym[kLitSlots], nb[kLitSlots];
+  uint16_t ex[kLitSlots];
   int ns = 0;
   for (int i = 0; i < size;) {
     if (v[i] != 0) {
@@ -778,14 +1140,14 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
     }
   }
   const int asize = ntrees + rlemax;
-  uint32_t hist[kLitCtx + 16];
+  uint32_t hist[kMaxLitTrees + 16];
   for (int i = 0; i < asize; i++) hist[i] = 0;
   for (int k = 0; k < ns; k++) hist[sym[k]]++;
   w.put(1, rlemax > 0 ? 1 : 0);
   if (rlemax) w.put(4, (uint32_t)(rlemax - 1));
-  uint8_t depth[kLitCtx + 16];
-  uint16_t code[kLitCtx + 16];
-  int16_t nzs[kLitCtx + 16];
+  uint8_t depth[kMaxLitTrees + 16];
+  uint16_t code[kMaxLitTrees + 16];
+  int16_t nzs[kMaxLitTrees + 16];
   int n = 0;
   for (int i = 0; i < asize; i++)
     if (hist[i]) nzs[n++] = (int16_t)i;
@@ -800,9 +1162,31 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
   w.put(1, 1);   // IMTF
 }
 
+// NBLTYPES and, for a split category, its block type and block count prefix codes and the
+// first block count (storeBlockSwitch's header part, metablock.ts:150-220)
+__device__ void put_block_split(BitW &w, int nbt, uint8_t *td, uint16_t *tc, uint8_t *cdp, uint16_t *cc, uint32_t first) {
+  put_varlen_u8(w, nbt - 1);
+  if (nbt <= 1) return;
+  int16_t nzs[26];
+  int n = 0;
+  const int ta = nbt + 2;
+  for (int i = 0; i < ta; i++)
+    if (td[i]) nzs[n++] = (int16_t)i;
+  int mb_bits = 0;
+  for (int c = ta - 1; c; c >>= 1) mb_bits++;
+  store_code(w, n, nzs, mb_bits, td, tc, ta);
+  n = 0;
+  for (int i = 0; i < 26; i++)
+    if (cdp[i]) nzs[n++] = (int16_t)i;
+  store_code(w, n, nzs, 5, cdp, cc, 26);
+  const int bc = block_count_code(first);
+  w.put(cdp[bc], cc[bc]);
+  w.put((int)kBlkBits[bc], first - kBlkOff[bc]);
+}
+
 // The metablock header before the prefix codes, lane per metablock (storeMetaBlock's
-// header part, metablock.ts:690-705; one block type per category).
-__global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hdr) {
+// header part, metablock.ts:690-705).
+__global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hdr, Codes *codes) {
   int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nmbs) return;
   Mb &mb = mbs[m];
@@ -820,20 +1204,31 @@ __global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hd
   w.put(2, (uint32_t)(mn - 4));
   w.put(mn * 4, length - 1);
   if (!mb.is_last) w.put(1, 0);
-  put_varlen_u8(w, 0);   // NBLTYPESL - 1
-  put_varlen_u8(w, 0);   // NBLTYPESI - 1
-  put_varlen_u8(w, 0);   // NBLTYPESD - 1
+  Codes &cd = codes[m];
+  for (int c = 0; c < 3; c++) put_block_split(w, (int)mb.nbt[c], cd.btd[c], cd.btc[c], cd.bcd[c], cd.bcc[c], mb.first_count[c]);
   w.put(2, jb.npostfix);
   w.put(4, jb.ndirect >> jb.npostfix);
-  w.put(2, mb.ctx_mode);
-  encode_context_map(w, mb.lit_cmap, kLitCtx, (int)mb.nlit);
-  encode_context_map(w, mb.dist_cmap, kDistCtx, (int)mb.ndist);
+  for (uint32_t ty = 0; ty < mb.nbt[0]; ty++) w.put(2, mb.ctx_mode);
+  // context maps over dense code indices (slots of type ty start at the codes of the types before it)
+  uint8_t map[kLitSlots];
+  int base = 0;
+  for (uint32_t ty = 0; ty < mb.nbt[0]; ty++) {
+    for (int q = 0; q < kLitCtx; q++) map[ty * kLitCtx + q] = (uint8_t)(base + mb.lit_cmap[ty * kLitCtx + q] - ty * kLitCtx);
+    base += (int)mb.nlit_t[ty];
+  }
+  encode_context_map(w, map, (int)mb.nbt[0] * kLitCtx, base);
+  base = 0;
+  for (uint32_t ty = 0; ty < mb.nbt[2]; ty++) {
+    for (int q = 0; q < kDistCtx; q++) map[ty * kDistCtx + q] = (uint8_t)(base + mb.dist_cmap[ty * kDistCtx + q] - ty * kDistCtx);
+    base += (int)mb.ndist_t[ty];
+  }
+  encode_context_map(w, map, (int)mb.nbt[2] * kDistCtx, base);
   mb.hdr_bits = (uint32_t)w.pos;
 }
 
 // ---------------------------------------------------------------- sizes: block per segment
 __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
-                                                       const uint32_t *cmd_pos, const Codes *codes) {
+                                                       const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
   typedef hipcub::BlockReduce<unsigned long long, kBlock> Reduce;
   __shared__ typename Reduce::TempStorage tmp;
   Seg &sg = segs[blockIdx.x];
@@ -843,10 +1238,11 @@ __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *seg
   const Codes &cd = codes[sg.mb];
   const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   unsigned long long bits = 0;
   for (uint32_t q = threadIdx.x; q < n; q += kBlock) {
     const uint32_t p = cmd_pos[sg.cmd_off + q];
-    bits += command_bits(cd, mb, lut, cmds[sg.cmd_off + q], jb.data + p, prev2(jb, p));
+    bits += command_bits(cd, mb, lut, cmds[sg.cmd_off + q], jb.data + p, prev2(jb, p), un[unit_of(sg, p)], q);
   }
   unsigned long long total = Reduce(tmp).Sum(bits);
   if (threadIdx.x == 0) sg.bits = total;
@@ -893,8 +1289,15 @@ void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs
   hipLaunchKernelGGL(carry_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, mbs);
 }
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
-                  uint32_t *cmd_pos, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
-  hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, hl, hc, hd);
+                  uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
+  hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
+}
+void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes) {
+  hipLaunchKernelGGL(split_kernel, dim3(nmbs * 3), dim3(256), 0, st, jobs, mbs, nmbs, units, unit_h, codes);
+}
+void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
+                  const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
+  hipLaunchKernelGGL(histo_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, units, hl, hc, hd);
 }
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds) {
   hipLaunchKernelGGL(dist_ring_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, cmds);
@@ -903,16 +1306,16 @@ void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
   hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs);
 }
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
-  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2), dim3(256), 0, st, jobs, mbs, nmbs, hl, hd);
+  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(256), 0, st, jobs, mbs, nmbs, hl, hd);
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
   hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * kTreeSlots), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees);
-  hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr);
+  hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
-                  const uint32_t *cmd_pos, const Codes *codes) {
-  hipLaunchKernelGGL(sizes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes);
+                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
+  hipLaunchKernelGGL(sizes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
 }
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
   hipLaunchKernelGGL(offsets_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, out);

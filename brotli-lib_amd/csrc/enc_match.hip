@@ -31,10 +31,13 @@ constexpr int kTile = 256;
 constexpr int kBack = 64;
 
 __device__ __forceinline__ uint64_t load_prefix8(const uint8_t *p, uint32_t avail) {
-  if (avail >= 8) {
-    uint64_t v = 0;
-    for (int i = 0; i < 8; i++) v |= (uint64_t)p[i] << (8 * i);
-    return v;
+  if (avail >= 12) {   // three aligned words (all inside the stream) and two funnel shifts
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    return ((uint64_t)hi << 32) | lo;
   }
   uint64_t v = 0;
   for (uint32_t i = 0; i < avail; i++) v |= (uint64_t)p[i] << (8 * i);
@@ -43,7 +46,7 @@ __device__ __forceinline__ uint64_t load_prefix8(const uint8_t *p, uint32_t avai
 
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *sorted_keys,
                                                              const uint32_t *sorted_vals, uint32_t total, int depth,
-                                                             uint32_t *matches, uint8_t *nmatch) {
+                                                             uint32_t *matches) {
   __shared__ uint32_t skey[kTile + kBack];
   __shared__ uint32_t spos[kTile + kBack];
   __shared__ uint64_t spre[kTile + kBack];
@@ -96,7 +99,9 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       } else {
         const uint8_t *cand = cur - d;
         if (best >= 8 && cur[best] != cand[best]) continue;
-        len = 8 + match_len(cur + 8, cand + 8, limit > 8 ? limit - 8 : 0);
+        // measured up to the saturation length: the parse measures longer copies itself
+        const uint32_t lim = min(limit, kMatchLenSat);
+        len = 8 + match_len(cur + 8, cand + 8, lim > 8 ? lim - 8 : 0);
         len = min(len, limit);
       }
       if (len > best) {
@@ -109,9 +114,13 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
         if (len >= limit || len >= kMatchLenSat) break;   // the parse measures a long copy itself
       }
     }
-    for (int q = 0; q < cnt; q++) matches[(uint64_t)g * kMaxMatches + q] = local[q];
+    uint4 *rec = reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec);
+    rec[0] = make_uint4(local[0], local[1], local[2], local[3]);
+    rec[1] = make_uint4(local[4], local[5], (uint32_t)cnt, 0u);
+    return;
   }
-  nmatch[g] = (uint8_t)cnt;
+  uint4 *rec = reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec);
+  rec[1] = make_uint4(0u, 0u, 0u, 0u);   // no candidates: count 0
 }
 
 // ---------------------------------------------------------------- literal cost model per stream
@@ -134,9 +143,9 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, keys, vals);
 }
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
-                         int depth, uint32_t *matches, uint8_t *nmatch) {
+                         int depth, uint32_t *matches) {
   hipLaunchKernelGGL(find_matches_kernel, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, skeys, svals, total,
-                     depth, matches, nmatch);
+                     depth, matches);
 }
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h) {
   hipLaunchKernelGGL(lit_histo_kernel, dim3(nsegs), dim3(256), 0, st, jobs, segs, lit_h);

@@ -74,13 +74,12 @@ struct Staged {   // one position's parse inputs (lane j of a batch = position i
   uint32_t nm;
   uint32_t lit;
 };
-__device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches, const uint8_t *nmatch, const uint8_t *data,
-                                            uint32_t g, uint32_t p) {
-  st.nm = nmatch[g];
+__device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches, const uint8_t *data, uint32_t g, uint32_t p) {
   st.lit = data[p];
-  const uint32_t *src = matches + (uint64_t)g * kMaxMatches;
-#pragma unroll
-  for (int q = 0; q < kMaxMatches; q++) st.m[q] = src[q];   // entries past nm are ignored
+  const uint4 *rec = reinterpret_cast<const uint4 *>(matches + (uint64_t)g * kMatchRec);
+  const uint4 a = rec[0], b = rec[1];   // entries past the count are ignored
+  st.m[0] = a.x; st.m[1] = a.y; st.m[2] = a.z; st.m[3] = a.w; st.m[4] = b.x; st.m[5] = b.y;
+  st.nm = b.z;
 }
 __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (distance << 32) | length, 0 = literal
   const uint32_t cl = m & 0xFFFF;
@@ -89,7 +88,7 @@ __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (di
 
 __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5))) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const uint32_t *matches,
-                                                           const uint8_t *nmatch, uint64_t *choice /* per position+1 */) {
+                                                           uint64_t *choice /* per position+1 */) {
   __shared__ uint32_t lentab[24 * kLenTab];   // (insert code, length) -> fp16 (explicit distance) | fp16 (short code 0) << 16
   __shared__ float litc_all[kDpWaves][256];
   const float dist0 = dist_sym_cost(0);
@@ -142,7 +141,7 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
   float bmc[kMaxMatches], blc = 0.f;
   Staged pf;
   uint32_t pf_at = a;
-  if (a + lane < b) load_staged(pf, matches, nmatch, data, gbase + a + lane, a + lane);
+  if (a + lane < b) load_staged(pf, matches, data, gbase + a + lane, a + lane);
   uint32_t chd = 0, chm = 0;   // choices of the batch
   uint32_t i = a, i0 = a;
 #ifdef MIB_PROF
@@ -155,10 +154,10 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
     if (pf_at == i0) {
       cur = pf;
     } else if (i0 + lane < b) {   // the parse jumped past the prefetched batch
-      load_staged(cur, matches, nmatch, data, gbase + i0 + lane, i0 + lane);
+      load_staged(cur, matches, data, gbase + i0 + lane, i0 + lane);
     }
     const uint32_t nx = i0 + 64;
-    if (nx + lane < b) load_staged(pf, matches, nmatch, data, gbase + nx + lane, nx + lane);
+    if (nx + lane < b) load_staged(pf, matches, data, gbase + nx + lane, nx + lane);
     pf_at = nx;
     const uint32_t p = i0 + lane;
     const uint32_t nm = p < b ? cur.nm : 0u;
@@ -432,8 +431,8 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 }
 #endif
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
-               const uint32_t *matches, const uint8_t *nmatch, uint64_t *choice) {
-  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kDpWaves - 1) / kDpWaves), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h, matches, nmatch,
+               const uint32_t *matches, uint64_t *choice) {
+  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kDpWaves - 1) / kDpWaves), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h, matches,
                      choice);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {

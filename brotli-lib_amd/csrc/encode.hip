@@ -206,11 +206,12 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
                                         (uint32_t *)nullptr, (int)total, 0, 32, st));
   size_t need = 64 * 256;
   need += 4 * (size_t)total * 4 + sort_tmp;
-  need += (size_t)total * kMaxMatches * 4 + total;
+  need += (size_t)total * kMatchRec * 4;
   need += ((size_t)total + 1) * 8;
   need += cmd_total * (sizeof(RawCmd) + sizeof(Cmd) + 4);
   need += k * (sizeof(Job) + 1024 + 8) + ns1 * sizeof(Seg) + seg_job.size() * 4;
-  need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + kTreeSlots * kTreeBytes + 4 * (kLitCtx * 256 + 704 + kDistCtx * 128));
+  need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + kTreeSlots * kTreeBytes + 4 * (kLitSlots * 256 + kMaxBT * 704 + kMaxBT * kDistCtx * 128));
+  need += ns1 * kSubPerSeg * (sizeof(Unit) + kSubHist * 4);
   need += out_scratch + 64;
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
@@ -230,8 +231,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   uint32_t *keys = ar.take<uint32_t>(total), *vals = ar.take<uint32_t>(total);
   uint32_t *skeys = ar.take<uint32_t>(total), *svals = ar.take<uint32_t>(total);
   void *sort_ws = ar.take<uint8_t>(sort_tmp);
-  uint32_t *matches = ar.take<uint32_t>((size_t)total * kMaxMatches);
-  uint8_t *nmatch = ar.take<uint8_t>(total);
+  uint32_t *matches = ar.take<uint32_t>((size_t)total * kMatchRec);
   uint64_t *choice = ar.take<uint64_t>((size_t)total + 1);
   RawCmd *raw = ar.take<RawCmd>(cmd_total);
   Cmd *cmds = ar.take<Cmd>(cmd_total);
@@ -241,9 +241,11 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   Mb *d_mbs = ar.take<Mb>(nm1);
   uint32_t *d_seg_job = ar.take<uint32_t>(seg_job.size());
   uint32_t *lit_h = ar.take<uint32_t>(k * 256);
-  uint32_t *hl = ar.take<uint32_t>(nm1 * kLitCtx * 256);
-  uint32_t *hc = ar.take<uint32_t>(nm1 * 704);
-  uint32_t *hd = ar.take<uint32_t>(nm1 * kDistCtx * 128);
+  uint32_t *hl = ar.take<uint32_t>(nm1 * kLitSlots * 256);
+  uint32_t *hc = ar.take<uint32_t>(nm1 * kMaxBT * 704);
+  uint32_t *hd = ar.take<uint32_t>(nm1 * kMaxBT * kDistCtx * 128);
+  Unit *units = ar.take<Unit>(ns1 * kSubPerSeg);
+  uint32_t *unit_h = ar.take<uint32_t>(ns1 * kSubPerSeg * kSubHist);
   Codes *codes = ar.take<Codes>(nm1);
   uint8_t *hdr = ar.take<uint8_t>(nm1 * kHdrBytes);
   uint8_t *trees = ar.take<uint8_t>(nm1 * kTreeSlots * kTreeBytes);
@@ -259,9 +261,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
   if (nsegs) {
     CK(hipMemsetAsync(lit_h, 0, k * 256 * 4, st));
-    CK(hipMemsetAsync(hl, 0, nm1 * kLitCtx * 256 * 4, st));
-    CK(hipMemsetAsync(hc, 0, nm1 * 704 * 4, st));
-    CK(hipMemsetAsync(hd, 0, nm1 * kDistCtx * 128 * 4, st));
+    CK(hipMemsetAsync(hl, 0, nm1 * kLitSlots * 256 * 4, st));
+    CK(hipMemsetAsync(hc, 0, nm1 * kMaxBT * 704 * 4, st));
+    CK(hipMemsetAsync(hd, 0, nm1 * kMaxBT * kDistCtx * 128 * 4, st));
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
     const int depth = depth_for_quality(prm.quality);
     tm.start("hash_keys");
@@ -271,13 +273,13 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, 32, st));
     tm.stop();
     tm.start("find_matches");
-    launch_find_matches(st, d_jobs, skeys, svals, total, depth, matches, nmatch);
+    launch_find_matches(st, d_jobs, skeys, svals, total, depth, matches);
     tm.stop();
     tm.start("lit_histo");
     launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
     tm.stop();
     tm.start("dp_parse");
-    launch_dp(st, d_jobs, d_segs, nsegs, lit_h, matches, nmatch, choice);
+    launch_dp(st, d_jobs, d_segs, nsegs, lit_h, matches, choice);
     tm.stop();
     tm.start("backtrack");
     launch_backtrack(st, d_jobs, d_segs, nsegs, choice, raw);
@@ -285,8 +287,14 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
     launch_context_mode(st, d_jobs, d_mbs, nmbs);
-    launch_codes(st, d_jobs, d_segs, d_mbs, nsegs, raw, cmds, cmd_pos, hl, hc, hd);
+    launch_codes(st, d_jobs, d_segs, d_mbs, nsegs, raw, cmds, cmd_pos, units, unit_h);
     launch_dist_ring(st, d_jobs, (int)k, d_segs, cmds);
+    tm.stop();
+    tm.start("block_split");
+    launch_split(st, d_jobs, d_mbs, nmbs, units, unit_h, codes);
+    tm.stop();
+    tm.start("type_histo");
+    launch_histo(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, units, hl, hc, hd);
     tm.stop();
     tm.start("cluster");
     launch_cluster(st, d_jobs, d_mbs, nmbs, hl, hd);
@@ -295,11 +303,11 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_huffman(st, d_jobs, d_mbs, nmbs, hl, hc, hd, codes, trees, hdr);
     tm.stop();
     tm.start("sizes");
-    launch_sizes(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, codes);
+    launch_sizes(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, codes, units);
     launch_offsets(st, d_jobs, (int)k, d_mbs, d_segs, oscr);
     tm.stop();
     tm.start("emit");
-    launch_emit(st, d_jobs, d_mbs, nmbs, d_segs, nsegs, cmds, cmd_pos, codes, trees, hdr, oscr);
+    launch_emit(st, d_jobs, d_mbs, nmbs, d_segs, nsegs, cmds, cmd_pos, codes, units, trees, hdr, oscr);
     tm.stop();
   }
   tm.start("stored");
@@ -329,7 +337,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   return 0;
 }
 
-// workspace is ~65 bytes per position (keys 16, matches 25, choice 8, commands ~16): groups
+// workspace is ~72 bytes per position (keys 16, match records 32, choice 8, commands ~16): groups
 // of at most this many positions (~70 GB)
 constexpr uint64_t kGroupPositions = 1ull << 30;
 constexpr size_t kGroupStreams = 16384;   // job index must fit the 15-bit key field
