@@ -55,7 +55,7 @@ constexpr int kBlockTreesCap = 3091;   // engine.ts:163 Int32Array(3091)
 // 1024-stream batch fit the 160 KiB.  A metablock's prefix-code tables are built in HBM
 // scratch (packed, exact sizes) and, when they fit, copied into kLdsTab 16-bit entries
 // (nbits << 12 | symbol-or-subtable-offset), tree roots resolved to absolute indices.
-constexpr int kLdsTab = 12288;
+constexpr int kLdsTab = 12224;
 
 typedef __attribute__((address_space(1))) uint8_t GU8;          // HBM
 typedef const __attribute__((address_space(1))) int32_t GI32;
@@ -107,15 +107,27 @@ struct Dec {
   // compound dictionary
   const uint8_t *cd;
   int cd_total, cd_br_offset, cd_br_length, cd_br_copied, cd_br_index;
-  int lane;
   Lds *l;
   uint64_t guard, guard_limit;
 };
 
+// The decoder state lives in LDS (one copy per wave): loads from it are uniform (scalar
+// after readfirstlane) and, unlike a private-memory struct, never share a counter with the
+// outstanding ring stores.
+typedef __attribute__((address_space(3))) Dec DecS;
+#define LANE ((int)threadIdx.x)
+static_assert(sizeof(Lds) + sizeof(Dec) + 2 * kLdsTab <= 163840 / 4, "four streams per CU");
+
+// One stream per workgroup (one wave): the LDS working set lives at file scope, so the hot
+// loop addresses it with constant offsets instead of pointer registers.
+__shared__ Lds g_lds;
+__shared__ uint16_t g_ltab[kLdsTab];
+__shared__ Dec g_dec;   // the decoder state: LDS, so that it is wave-uniform and never waits on HBM stores
+
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
 #ifdef MIB_PROF   // timing experiment: cycles in command / literal / distance / copy, literal and command counts
-__device__ unsigned long long g_prof[8];   // + metablocks with LDS / HBM tables
+__device__ unsigned long long g_prof[16];   // + metablocks with LDS / HBM tables
 #endif
 
 // A block is one wave: a wave's LDS and global accesses are performed in order, so the
@@ -127,38 +139,38 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 // ---------------------------------------------------------------- bit reader
-__device__ __forceinline__ uint32_t half_at(const Dec &s, int h) {
+__device__ __forceinline__ uint32_t half_at(const DecS &s, int h) {
   if (h < 0 || h >= 2080) return 0;   // Int16Array(2080): undefined -> 0
   return (uint32_t)s.l->win[2 * h] | ((uint32_t)s.l->win[2 * h + 1] << 8);
 }
-__device__ __forceinline__ void fill16(Dec &s) {
+__device__ __forceinline__ void fill16(DecS &s) {
   if (s.bo >= 16) {
     s.acc = (half_at(s, s.ho++) << 16) | (s.acc >> 16);
     s.bo -= 16;
   }
 }
-__device__ __forceinline__ void force16(Dec &s) {
+__device__ __forceinline__ void force16(DecS &s) {
   s.acc = (half_at(s, s.ho++) << 16) | (s.acc >> 16);
   s.bo -= 16;
 }
-__device__ __forceinline__ uint32_t peek(const Dec &s) { return s.acc >> (s.bo & 31); }
-__device__ __forceinline__ int bits(Dec &s, int n) {
+__device__ __forceinline__ uint32_t peek(const DecS &s) { return s.acc >> (s.bo & 31); }
+__device__ __forceinline__ int bits(DecS &s, int n) {
   int v = (int)(peek(s) & ((1u << n) - 1u));
   s.bo += n;
   return v;
 }
-__device__ __forceinline__ int many_bits(Dec &s, int n) {
+__device__ __forceinline__ int many_bits(DecS &s, int n) {
   int lo = bits(s, 16);
   force16(s);
   return lo | (bits(s, n - 16) << 16);
 }
-__device__ int half_available(const Dec &s) {
+__device__ int half_available(const DecS &s) {
   int limit = s.eos ? (s.tail + 1) >> 1 : 2048;
   return limit - s.ho;
 }
 
 // readMoreInput (engine.ts:1764-1790): LDS memmove + HBM -> LDS fill, by the whole wave.
-__device__ int read_more_input(Dec &s) {
+__device__ __noinline__ int read_more_input(DecS &s) {
   if (s.eos) return half_available(s) >= -2 ? 0 : ERR(s, -16);
   int ro = s.ho << 1;
   int have = 4096 - ro;
@@ -167,21 +179,21 @@ __device__ int read_more_input(Dec &s) {
   const uint16_t *w16 = reinterpret_cast<const uint16_t *>(s.l->win);
 #pragma unroll
   for (int k = 0; k < 32; k++) {
-    int idx = s.lane + 64 * k;
+    int idx = LANE + 64 * k;
     tmp[k] = (2 * idx < have) ? w16[(ro >> 1) + idx] : 0;
   }
   wave_sync();
   uint16_t *wo = reinterpret_cast<uint16_t *>(s.l->win);
 #pragma unroll
   for (int k = 0; k < 32; k++) {
-    int idx = s.lane + 64 * k;
+    int idx = LANE + 64 * k;
     if (2 * idx < have) wo[idx] = tmp[k];
   }
   wave_sync();
   s.ho = 0;
   uint64_t avail = s.in_len - s.in_off;
   int n = (uint64_t)(4096 - have) < avail ? 4096 - have : (int)avail;
-  for (int i = s.lane; i < n; i += 64) s.l->win[have + i] = s.in[s.in_off + i];
+  for (int i = LANE; i < n; i += 64) s.l->win[have + i] = s.in[s.in_off + i];
   wave_sync();
   s.in_off += (uint64_t)n;
   have += n;
@@ -199,14 +211,14 @@ __device__ int read_more_input(Dec &s) {
     }                                         \
   } while (0)
 
-__device__ int check_health(Dec &s, int end_of_stream) {
+__device__ int check_health(DecS &s, int end_of_stream) {
   if (!s.eos) return 0;
   int byte_off = (s.ho << 1) + ((s.bo + 7) >> 3) - 4;
   if (byte_off > s.tail) return ERR(s, -13);
   if (end_of_stream && byte_off != s.tail) return ERR(s, -17);
   return 0;
 }
-__device__ int prepare(Dec &s) {
+__device__ int prepare(DecS &s) {
   MAYBE_REFILL(s);
   int h = check_health(s, 0);
   if (h) return h;
@@ -214,7 +226,7 @@ __device__ int prepare(Dec &s) {
   force16(s);
   return 0;
 }
-__device__ int jump_to_byte_boundary(Dec &s) {
+__device__ int jump_to_byte_boundary(DecS &s) {
   int pad = (32 - s.bo) & 7;
   if (pad && bits(s, pad) != 0) return ERR(s, -5);
   return 0;
@@ -227,14 +239,14 @@ __device__ int next_key(int key, int len) {
   return (key & (step - 1)) + step;
 }
 // group[off + p] = item for p = end - step, end - 2 step, ..., 0 ; lanes split the writes
-__device__ __forceinline__ void replicate(const Dec &s, int32_t *g, int cap, int off, int step, int end, int item) {
+__device__ __forceinline__ void replicate(const DecS &s, int32_t *g, int cap, int off, int step, int end, int item) {
   int n = end / step;
-  for (int k = s.lane; k < n; k += 64) {
+  for (int k = LANE; k < n; k += 64) {
     int i = off + k * step;
     if (i < cap) g[i] = item;
   }
 }
-__device__ int build_table(Dec &s, int32_t *group, int cap, int idx, int root, const int *lens, int nsym) {
+__device__ int build_table(DecS &s, int32_t *group, int cap, int idx, int root, const int *lens, int nsym) {
   int toff = group[idx];
   int count[16], offset[16];
   for (int i = 0; i < 16; i++) count[i] = offset[i] = 0;
@@ -243,7 +255,7 @@ __device__ int build_table(Dec &s, int32_t *group, int cap, int idx, int root, c
   for (int l = 1; l < 15; l++) offset[l + 1] = offset[l] + count[l];
   uint16_t *sorted = s.l->sorted;
   wave_sync();
-  if (s.lane == 0)
+  if (LANE == 0)
     for (int i = 0; i < nsym; i++)
       if (lens[i]) sorted[offset[lens[i]]++] = (uint16_t)i;
   for (int i = 0; i < nsym; i++)   // uniform copy of the per-length running offsets
@@ -283,7 +295,7 @@ __device__ int build_table(Dec &s, int32_t *group, int cap, int idx, int root, c
         tsize = 1 << tbits;
         total += tsize;
         low = key & mask;
-        if (s.lane == 0 && toff + low < cap) group[toff + low] = ((tbits + root) << 16) | (cur - toff - low);
+        if (LANE == 0 && toff + low < cap) group[toff + low] = ((tbits + root) << 16) | (cur - toff - low);
       }
       replicate(s, group, cap, cur + (key >> root), step, tsize, ((l - root) << 16) | sorted[sym++]);
       key = next_key(key, l);
@@ -292,7 +304,7 @@ __device__ int build_table(Dec &s, int32_t *group, int cap, int idx, int root, c
   wave_sync();
   return total;
 }
-__device__ __forceinline__ int read_symbol(Dec &s, const int32_t *g, int cap, int idx) {
+__device__ __forceinline__ int read_symbol(DecS &s, const int32_t *g, int cap, int idx) {
   int off = g[idx];
   uint32_t v = peek(s);
   off += (int)(v & 0xFF);
@@ -310,10 +322,10 @@ __device__ __forceinline__ int read_symbol(Dec &s, const int32_t *g, int cap, in
 }
 constexpr int kNoCap = 1 << 30;
 
-__device__ int read_code_lengths(Dec &s, const int *cl_lens, int nsym, int *lens) {   // engine.ts:305-369
+__device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, int *lens) {   // engine.ts:305-369
   int sym = 0, prev = 8, repeat = 0, repeat_len = 0, space = 32768;
   int32_t *table = s.l->cl_table;
-  if (s.lane == 0) table[32] = 0;
+  if (LANE == 0) table[32] = 0;
   wave_sync();
   build_table(s, table, kNoCap, 32, 5, cl_lens, 18);
   while (sym < nsym && space > 0) {
@@ -324,7 +336,7 @@ __device__ int read_code_lengths(Dec &s, const int *cl_lens, int nsym, int *lens
     int len = table[p] & 0xFFFF;
     if (len < 16) {
       repeat = 0;
-      if (s.lane == 0) lens[sym] = len;
+      if (LANE == 0) lens[sym] = len;
       sym++;
       if (len) {
         prev = len;
@@ -345,24 +357,24 @@ __device__ int read_code_lengths(Dec &s, const int *cl_lens, int nsym, int *lens
       repeat += bits(s, eb) + 3;
       int delta = repeat - old;
       if (sym + delta > nsym) return ERR(s, -2);
-      for (int k = s.lane; k < delta; k += 64) lens[sym + k] = repeat_len;
+      for (int k = LANE; k < delta; k += 64) lens[sym + k] = repeat_len;
       sym += delta;
       if (repeat_len) space -= delta << (15 - repeat_len);
     }
     wave_sync();
   }
   if (space != 0) return ERR(s, -18);
-  for (int k = sym + s.lane; k < nsym; k += 64) lens[k] = 0;
+  for (int k = sym + LANE; k < nsym; k += 64) lens[k] = 0;
   wave_sync();
   return 0;
 }
 
-__device__ int read_huffman_code(Dec &s, int amax, int alimit, int32_t *group, int cap, int idx) {   // :370-470
+__device__ int read_huffman_code(DecS &s, int amax, int alimit, int32_t *group, int cap, int idx) {   // :370-470
   int *lens = s.l->lens;
   MAYBE_REFILL(s);
   fill16(s);
   int kind = bits(s, 2);
-  for (int k = s.lane; k < alimit; k += 64) lens[k] = 0;
+  for (int k = LANE; k < alimit; k += 64) lens[k] = 0;
   wave_sync();
   if (kind == 1) {
     int syms[4];
@@ -380,7 +392,7 @@ __device__ int read_huffman_code(Dec &s, int amax, int alimit, int32_t *group, i
         if (syms[i] == syms[k]) return ERR(s, -7);
     int hid = n;
     if (n == 4) hid += bits(s, 1);
-    if (s.lane == 0) {
+    if (LANE == 0) {
       switch (hid) {
         case 1: lens[syms[0]] = 1; break;
         case 2: lens[syms[0]] = 1; lens[syms[1]] = 1; break;
@@ -414,7 +426,7 @@ __device__ int read_huffman_code(Dec &s, int amax, int alimit, int32_t *group, i
   return build_table(s, group, cap, idx, 8, lens, alimit);
 }
 
-__device__ int decode_var_len_byte(Dec &s) {
+__device__ int decode_var_len_byte(DecS &s) {
   fill16(s);
   if (bits(s, 1)) {
     int n = bits(s, 3);
@@ -424,11 +436,11 @@ __device__ int decode_var_len_byte(Dec &s) {
   return 0;
 }
 
-__device__ int decode_context_map(Dec &s, int size, uint8_t *map, int32_t *table_scratch) {   // :488-558
+__device__ int decode_context_map(DecS &s, int size, uint8_t *map, int32_t *table_scratch) {   // :488-558
   MAYBE_REFILL(s);
   int ntrees = decode_var_len_byte(s) + 1;
   if (ntrees == 1) {
-    for (int k = s.lane; k < size; k += 64) map[k] = 0;
+    for (int k = LANE; k < size; k += 64) map[k] = 0;
     wave_sync();
     return ntrees;
   }
@@ -438,7 +450,7 @@ __device__ int decode_context_map(Dec &s, int size, uint8_t *map, int32_t *table
   int asize = ntrees + rle_max;
   int tsize = kMaxHuffTable[(asize + 31) >> 5];
   int32_t *table = table_scratch;
-  if (s.lane == 0) table[tsize] = 0;
+  if (LANE == 0) table[tsize] = 0;
   wave_sync();
   int r = read_huffman_code(s, asize, asize, table, kNoCap, tsize);
   if (r < 0) return r;
@@ -448,23 +460,23 @@ __device__ int decode_context_map(Dec &s, int size, uint8_t *map, int32_t *table
     fill16(s);
     int code = read_symbol(s, table, kNoCap, tsize);
     if (code == 0) {
-      if (s.lane == 0) map[i] = 0;
+      if (LANE == 0) map[i] = 0;
       i++;
     } else if (code <= rle_max) {
       fill16(s);
       int reps = (1 << code) + bits(s, code);
       if (i + reps > size) return ERR(s, -3);
-      for (int k = s.lane; k < reps; k += 64) map[i + k] = 0;
+      for (int k = LANE; k < reps; k += 64) map[i + k] = 0;
       i += reps;
     } else {
-      if (s.lane == 0) map[i] = (uint8_t)(code - rle_max);
+      if (LANE == 0) map[i] = (uint8_t)(code - rle_max);
       i++;
     }
   }
   wave_sync();
   fill16(s);
   if (bits(s, 1) == 1) {   // inverse move-to-front, lane 0 (rare, small)
-    if (s.lane == 0) {
+    if (LANE == 0) {
       uint8_t *mtf = s.l->mtf;
       for (int k = 0; k < 256; k++) mtf[k] = (uint8_t)k;
       for (int k = 0; k < size; k++) {
@@ -480,14 +492,14 @@ __device__ int decode_context_map(Dec &s, int size, uint8_t *map, int32_t *table
   return ntrees;
 }
 
-__device__ int read_block_length(Dec &s, const int32_t *g, int idx) {
+__device__ int read_block_length(DecS &s, const int32_t *g, int idx) {
   fill16(s);
   int code = read_symbol(s, g, kBlockTreesCap, idx);
   int n = kBlockLenBits[code];
   fill16(s);
   return kBlockLenOff[code] + (n <= 16 ? bits(s, n) : many_bits(s, n));
 }
-__device__ int decode_block_type_and_length(Dec &s, int tree_type, int ntypes) {   // :559-580
+__device__ __noinline__ int decode_block_type_and_length(DecS &s, int tree_type, int ntypes) {   // :559-580
   int off = 4 + tree_type * 2;
   fill16(s);
   int bt = read_symbol(s, s.bt, kBlockTreesCap, 2 * tree_type);
@@ -500,20 +512,20 @@ __device__ int decode_block_type_and_length(Dec &s, int tree_type, int ntypes) {
   s.rings[off + 1] = bt;
   return len;
 }
-__device__ void build_ctx_tree_base(Dec &s) {
-  for (int k = s.lane; k < 512; k += 64) s.l->ctx_lut[k] = kRfcContextLut[s.clo1 + k];
-  const int tree = s.ctx_map[s.ctx_map_slice + s.lane];
+__device__ __noinline__ void build_ctx_tree_base(DecS &s) {
+  for (int k = LANE; k < 512; k += 64) s.l->ctx_lut[k] = kRfcContextLut[s.clo1 + k];
+  const int tree = s.ctx_map[s.ctx_map_slice + LANE];
   if (s.tab16) {
     // lut0[p1] | lut1[p2] with lut1 < 8 in every mode: one (p1, lut1[p2]) -> root table
     const int root = s.tab_lds[tree];   // the literal group starts at 0
     wave_sync();
-    for (int k = s.lane; k < 2048; k += 64) s.l->ctx_root[k] = (uint16_t)__shfl(root, s.l->ctx_lut[k >> 3] | (k & 7));
+    for (int k = LANE; k < 2048; k += 64) s.l->ctx_root[k] = (uint16_t)__shfl(root, s.l->ctx_lut[k >> 3] | (k & 7));
   } else {
-    s.l->ctx_tree_base[s.lane] = s.lit_group[tree];
+    s.l->ctx_tree_base[LANE] = s.lit_group[tree];
   }
   wave_sync();
 }
-__device__ void lit_block_switch(Dec &s) {
+__device__ __noinline__ void lit_block_switch(DecS &s) {
   s.lit_blen = decode_block_type_and_length(s, 0, s.n_lit_types);
   int t = s.rings[5];
   s.ctx_map_slice = t << 6;
@@ -524,15 +536,15 @@ __device__ void lit_block_switch(Dec &s) {
 }
 
 // back to the block's own ring: its content so far is the output's first ring_size bytes
-__device__ void leave_direct(Dec &s) {
+__device__ void leave_direct(DecS &s) {
   const int n = s.ring_size + 37;
-  for (int k = s.lane; k < n; k += 64) s.ring_scratch[k] = k < s.out_cap ? s.out[k] : 0;
+  for (int k = LANE; k < n; k += 64) s.ring_scratch[k] = k < s.out_cap ? s.out[k] : 0;
   wave_sync();
   s.ring = s.ring_scratch;
   s.direct = 0;
 }
 
-__device__ void maybe_realloc_ring(Dec &s) {   // :608-630 (the scratch slice is max-sized; copy semantics kept)
+__device__ void maybe_realloc_ring(DecS &s) {   // :608-630 (the scratch slice is max-sized; copy semantics kept)
   int new_size = s.max_ring;
   if (new_size > s.expected_total) {
     int minimal = s.expected_total;
@@ -550,13 +562,13 @@ __device__ void maybe_realloc_ring(Dec &s) {   // :608-630 (the scratch slice is
     leave_direct(s);
   }
   // a fresh Uint8Array: bytes beyond the old size are zero
-  for (int k = s.ring_size + s.lane; k < new_size + 37; k += 64) s.ring[k] = 0;
+  for (int k = s.ring_size + LANE; k < new_size + 37; k += 64) s.ring[k] = 0;
   wave_sync();
   s.ring_cap = new_size + 37;
   s.ring_size = new_size;
 }
 
-__device__ int decode_mb_length(Dec &s) {   // :204-256
+__device__ int decode_mb_length(DecS &s) {   // :204-256
   fill16(s);
   s.input_end = bits(s, 1);
   s.mbl = 0;
@@ -588,7 +600,7 @@ __device__ int decode_mb_length(Dec &s) {   // :204-256
   return 0;
 }
 
-__device__ int read_next_mb_header(Dec &s) {   // :631-678
+__device__ int read_next_mb_header(DecS &s) {   // :631-678
   if (s.input_end) {
     s.next_running = ST_FINISHED;
     s.running = ST_INIT_WRITE;
@@ -612,12 +624,12 @@ __device__ int read_next_mb_header(Dec &s) {   // :631-678
   return 0;
 }
 
-__device__ int read_partition(Dec &s, int tt, int ntypes) {   // :679-704
+__device__ int read_partition(DecS &s, int tt, int ntypes) {   // :679-704
   int32_t *bt = s.bt;
   int off = bt[2 * tt];
   if (ntypes <= 1) {
     wave_sync();
-    if (s.lane == 0) {
+    if (LANE == 0) {
       bt[2 * tt + 1] = off;
       bt[2 * tt + 2] = off;
     }
@@ -627,20 +639,20 @@ __device__ int read_partition(Dec &s, int tt, int ntypes) {   // :679-704
   int r = read_huffman_code(s, ntypes + 2, ntypes + 2, bt, kBlockTreesCap, 2 * tt);
   if (r < 0) return r;
   off += r;
-  if (s.lane == 0) bt[2 * tt + 1] = off;
+  if (LANE == 0) bt[2 * tt + 1] = off;
   wave_sync();
   r = read_huffman_code(s, 26, 26, bt, kBlockTreesCap, 2 * tt + 1);
   if (r < 0) return r;
   off += r;
-  if (s.lane == 0) bt[2 * tt + 2] = off;
+  if (LANE == 0) bt[2 * tt + 2] = off;
   wave_sync();
   return read_block_length(s, bt, 2 * tt + 1);
 }
 
-__device__ int decode_tree_group(Dec &s, int amax, int alimit, int n, int32_t *group) {
+__device__ int decode_tree_group(DecS &s, int amax, int alimit, int n, int32_t *group) {
   int next = n;
   for (int i = 0; i < n; i++) {
-    if (s.lane == 0) group[i] = next;
+    if (LANE == 0) group[i] = next;
     wave_sync();
     int r = read_huffman_code(s, amax, alimit, group, kNoCap, i);
     if (r < 0) return r;
@@ -649,7 +661,7 @@ __device__ int decode_tree_group(Dec &s, int amax, int alimit, int n, int32_t *g
   return next;   // the group's size in ints: its n roots and its tables
 }
 
-__device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
+__device__ int read_codes_and_maps(DecS &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
   int r;
   s.n_lit_types = decode_var_len_byte(s) + 1;
   if ((r = read_partition(s, 0, s.n_lit_types)) < 0) return r;
@@ -670,7 +682,7 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
     while (i < lim) {
       fill16(s);
       int m = bits(s, 2);
-      if (s.lane == 0) s.ctx_modes[i] = (uint8_t)m;
+      if (LANE == 0) s.ctx_modes[i] = (uint8_t)m;
       i++;
     }
     MAYBE_REFILL(s);
@@ -679,7 +691,7 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
   if ((r = decode_context_map(s, cml, s.ctx_map, ctxmap_table)) < 0) return r;
   int nlit_trees = r;
   int nontrivial = 0;
-  for (int k = s.lane; k < cml; k += 64)
+  for (int k = LANE; k < cml; k += 64)
     if (s.ctx_map[k] != (k >> 6)) nontrivial = 1;
   s.trivial_lit_ctx = __any(nontrivial) ? 0 : 1;
   if ((r = decode_context_map(s, s.n_dist_types << 2, s.dist_ctx_map, ctxmap_table)) < 0) return r;
@@ -699,13 +711,13 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
   const int total = dist_base + r;
   s.tab16 = total <= kLdsTab;
 #ifdef MIB_PROF
-  if (s.lane == 0) atomicAdd(&g_prof[s.tab16 ? 6 : 7], 1ull);
+  if (LANE == 0) atomicAdd(&g_prof[s.tab16 ? 6 : 7], 1ull);
 #endif
   s.cmd_base = cmd_base;
   s.dist_base = dist_base;
   if (s.tab16) {
     const int32_t *src = s.lit_group;
-    for (int k = s.lane; k < total; k += 64) {
+    for (int k = LANE; k < total; k += 64) {
       const int v = src[k];
       int o;
       if (k < nlit_trees) o = v;
@@ -717,7 +729,7 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
     wave_sync();
   }
   // calculateDistanceLut (:705-726), lane 0
-  if (s.lane == 0) {
+  if (LANE == 0) {
     int np = s.npostfix, nd = s.ndirect, postfix = 1 << np, b = 1, half = 0, k = 16;
     for (int q = 0; q < nd; q++) {
       dist_extra[k] = 0;
@@ -748,10 +760,10 @@ __device__ int read_codes_and_maps(Dec &s, int8_t *dist_extra, int32_t *dist_off
 }
 
 // copyRawBytes (:1876-1925) into the ring
-__device__ int copy_raw_bytes(Dec &s, int pos, int len) {
+__device__ int copy_raw_bytes(DecS &s, int pos, int len) {
   if (s.bo & 7) return ERR(s, -30);
   while (s.bo != 32 && len) {
-    if (s.lane == 0) s.ring[pos] = (uint8_t)peek(s);
+    if (LANE == 0) s.ring[pos] = (uint8_t)peek(s);
     pos++;
     s.bo += 8;
     len--;
@@ -762,7 +774,7 @@ __device__ int copy_raw_bytes(Dec &s, int pos, int len) {
   int cn = ha < (len >> 1) ? ha : (len >> 1);
   if (cn > 0) {
     int ro = s.ho << 1, delta = cn << 1;
-    for (int k = s.lane; k < delta; k += 64) s.ring[pos + k] = s.l->win[ro + k];
+    for (int k = LANE; k < delta; k += 64) s.ring[pos + k] = s.l->win[ro + k];
     wave_sync();
     pos += delta;
     len -= delta;
@@ -772,7 +784,7 @@ __device__ int copy_raw_bytes(Dec &s, int pos, int len) {
   if (half_available(s) > 0) {
     fill16(s);
     while (len) {
-      if (s.lane == 0) s.ring[pos] = (uint8_t)peek(s);
+      if (LANE == 0) s.ring[pos] = (uint8_t)peek(s);
       pos++;
       s.bo += 8;
       len--;
@@ -782,12 +794,12 @@ __device__ int copy_raw_bytes(Dec &s, int pos, int len) {
   }
   uint64_t avail = s.in_len - s.in_off;
   if ((uint64_t)len > avail) {   // readInput returns what is left, then 0 -> error -16
-    for (uint64_t k = s.lane; k < avail; k += 64) s.ring[pos + k] = s.in[s.in_off + k];
+    for (uint64_t k = LANE; k < avail; k += 64) s.ring[pos + k] = s.in[s.in_off + k];
     s.in_off += avail;
     wave_sync();
     return ERR(s, -16);
   }
-  for (int k = s.lane; k < len; k += 64) s.ring[pos + k] = s.in[s.in_off + k];
+  for (int k = LANE; k < len; k += 64) s.ring[pos + k] = s.in[s.in_off + k];
   s.in_off += (uint64_t)len;
   wave_sync();
   return 0;
@@ -795,7 +807,7 @@ __device__ int copy_raw_bytes(Dec &s, int pos, int len) {
 
 // write_ring (:868-879) + the reference's chunked output (:2223-2256) as one linear buffer.
 // Returns 0 (space left in the current chunk), 2 (chunk / known buffer full), or NEED_SPACE.
-__device__ int write_ring(Dec &s) {
+__device__ int write_ring(DecS &s) {
   int64_t chunk_left = s.chunk_start + s.chunk_size - s.out_flushed;
   int64_t b = s.rb_ready - s.rb_written;
   int64_t n = chunk_left < b ? chunk_left : b;
@@ -804,7 +816,7 @@ __device__ int write_ring(Dec &s) {
     uint8_t *dst = s.out + s.out_flushed;
     const uint8_t *src = s.ring + s.rb_written;
     if (dst != src) {   // (decoding in place: nothing to move)
-      for (int64_t k = s.lane; k < n; k += 64) dst[k] = src[k];
+      for (int64_t k = LANE; k < n; k += 64) dst[k] = src[k];
       wave_sync();
     }
     s.out_flushed += n;
@@ -854,7 +866,7 @@ __device__ int transform_word(uint8_t *dst, int doff, int soff, int wlen, int ti
   return off - doff;
 }
 
-__device__ int use_dictionary(Dec &s, int fence) {   // :903-983
+__device__ int use_dictionary(DecS &s, int fence) {   // :903-983
   if (s.distance > 0x7FFFFFFC) return ERR(s, -9);
   int address = s.distance - s.max_dist - 1 - s.cd_total;
   if (address < 0) {   // compound dictionary, one chunk (attachDictionaryChunk is called once)
@@ -880,7 +892,7 @@ __device__ int use_dictionary(Dec &s, int fence) {   // :903-983
   off += widx * wlen;
   if (tidx >= RFC_NUM_TRANSFORMS) return ERR(s, -9);
   int len = 0;
-  if (s.lane == 0) len = transform_word(s.ring, s.pos, off, wlen, tidx);
+  if (LANE == 0) len = transform_word(s.ring, s.pos, off, wlen, tidx);
   len = __shfl(len, 0);
   wave_sync();
   s.pos += len;
@@ -894,7 +906,7 @@ __device__ int use_dictionary(Dec &s, int fence) {   // :903-983
   return 0;
 }
 
-__device__ int copy_from_compound(Dec &s, int fence) {
+__device__ int copy_from_compound(DecS &s, int fence) {
   int pos = s.pos, orig = pos;
   while (s.cd_br_length != s.cd_br_copied) {
     int space = fence - pos;
@@ -904,7 +916,7 @@ __device__ int copy_from_compound(Dec &s, int fence) {
     if (len > rem) len = rem;
     if (len > space) len = space;
     if (s.cd_br_index >= 1) return MIB_E_JS_TYPE_ERROR;   // reads past the last chunk in JS
-    for (int k = s.lane; k < len; k += 64) s.ring[pos + k] = s.cd[s.cd_br_offset + k];
+    for (int k = LANE; k < len; k += 64) s.ring[pos + k] = s.cd[s.cd_br_offset + k];
     wave_sync();
     pos += len;
     s.cd_br_offset += len;
@@ -921,15 +933,15 @@ __device__ int copy_from_compound(Dec &s, int fence) {
 // LZ77 copy of `cl` bytes at ring position pos from distance dist (no fence crossing).
 // An overlapping copy (dist < cl) repeats the dist bytes before pos, so every byte is a
 // function of pre-copy data only: out[pos + j] = ring[src + j % dist]; all 64 lanes work.
-__device__ void ring_copy_fast(Dec &s, int src, int cl, int dist) {
+__device__ void ring_copy_fast(DecS &s, int src, int cl, int dist) {
   uint8_t *r = s.ring;
   int dst = s.pos;
   if (dist >= cl) {
-    for (int k = s.lane; k < cl; k += 64) r[dst + k] = r[src + k];
+    for (int k = LANE; k < cl; k += 64) r[dst + k] = r[src + k];
   } else {
-    int q = s.lane % dist;
+    int q = LANE % dist;
     int qstep = 64 % dist;
-    for (int k = s.lane; k < cl; k += 64) {
+    for (int k = LANE; k < cl; k += 64) {
       r[dst + k] = r[src + q];
       q += qstep;
       if (q >= dist) q -= dist;
@@ -938,48 +950,14 @@ __device__ void ring_copy_fast(Dec &s, int src, int cl, int dist) {
   wave_sync();
 }
 
-// one invocation of decompress(); returns 0, 1 (done), 2 (output full / compound return) or < 0
-__device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
-  int r;
-  if (s.running < 0) return ERR(s, -28);
-  if (s.running == ST_INITED) {
-    fill16(s);
-    int wb;
-    if (bits(s, 1) == 0) wb = 16;
-    else {
-      int n = bits(s, 3);
-      if (n) wb = 17 + n;
-      else {
-        n = bits(s, 3);
-        if (n == 1) wb = -1;
-        else if (n) wb = 8 + n;
-        else wb = 17;
-      }
-    }
-    if (wb == -1) return ERR(s, -11);
-    s.max_ring = 1 << wb;
-    s.max_back = s.max_ring - 16;
-    s.running = ST_BLOCK_START;
-  }
-  int fence = s.ring_size;
-  int rmask = s.ring_size - 1;
-  while (s.running != ST_FINISHED) {
-    if (++s.guard > s.guard_limit) return MIB_E_NO_PROGRESS;
-    switch (s.running) {
-      case ST_BLOCK_START:
-        if (s.mbl < 0) return ERR(s, -10);
-        if ((r = read_next_mb_header(s)) < 0) return r;
-        fence = s.ring_size;
-        if (s.pos + s.mbl <= s.ring_size) fence = 0x7FFFFFFF;
-        rmask = s.ring_size - 1;
-        continue;
-      case ST_COMPRESSED_BLOCK_START:
-        if ((r = read_codes_and_maps(s, dist_extra, dist_offset, ctxmap_table)) < 0) return r;
-        s.running = ST_MAIN_LOOP;
-        continue;
-      case ST_MAIN_LOOP:
-      case ST_INSERT_LOOP:
-      case ST_COPY_LOOP: {
+// The command / literal / copy loop (engine.ts:1059-1438) as a function of its own: only
+// the hot state is live in it, so it stays in SGPRs (the whole state machine inlined into
+// the kernel spilled ~190 SGPRs into VGPR lanes, read and written back on every command).
+// Returns 0 with s.running set for the state machine, or a negative error code.
+template <bool kTabLds>
+__device__ __noinline__ int hot_loop(int fence_in, int rmask_in) {
+  DecS &s = *(DecS *)&g_dec;
+  const int fence = __builtin_amdgcn_readfirstlane(fence_in), rmask = __builtin_amdgcn_readfirstlane(rmask_in);
         // The command / literal / copy loop runs on registers: the bit reader, positions,
         // lengths and block counters are loaded from `s` once, saved back around every
         // cold call (refill, block switch) and on every exit.
@@ -988,19 +966,19 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         // generic (flat) access would have to drain first.
         int phase = s.running;
         GU8 *ring = (GU8 *)s.ring;
-        LU16 *win16 = (LU16 *)s.l->win;
-        LI32 *ctb = (LI32 *)s.l->ctx_tree_base;
+        LU16 *win16 = (LU16 *)g_lds.win;
+        LI32 *ctb = (LI32 *)g_lds.ctx_tree_base;
         const int ring_cap = s.ring_cap, npostfix = s.npostfix, ndirect = s.ndirect, max_back = s.max_back;
-        const bool tab_lds = s.tab16 != 0;
-        LU16 *t16 = (LU16 *)s.tab_lds;
-        LU16 *croot = (LU16 *)s.l->ctx_root;
+        constexpr bool tab_lds = kTabLds;   // prefix-code tables in LDS (16-bit) or HBM
+        LU16 *t16 = (LU16 *)g_ltab;
+        LU16 *croot = (LU16 *)g_lds.ctx_root;
         const int cmd_base = __builtin_amdgcn_readfirstlane(s.cmd_base), dist_base = __builtin_amdgcn_readfirstlane(s.dist_base);
         GI32 *cmd_h = (GI32 *)s.cmd_group, *dist_h = (GI32 *)s.dist_group, *lit_h = (GI32 *)s.lit_group;
-        const int lane = s.lane;
+        const int lane = LANE;
         const uint64_t guard_limit = s.guard_limit;
         int trivial = s.trivial_lit_ctx, lit_tree = s.lit_tree_idx;
         const int ring_size = s.ring_size;
-        LU8 *clut = (LU8 *)s.l->ctx_lut;
+        LU8 *clut = (LU8 *)g_lds.ctx_lut;
         // The last two output bytes (the literal context) live in registers: reading them
         // back from the ring would wait for every outstanding ring store (vmcnt is in order).
         int c1 = __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 1) & rmask]);
@@ -1039,7 +1017,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
   do {                                                \
     if (ho > 2030) {                                  \
       HOT_SAVE();                                     \
-      int r_ = read_more_input(s);                    \
+      int r_ = U(read_more_input(s));                 \
       if (r_ < 0) return r_;                          \
       HOT_LOAD();                                     \
     }                                                 \
@@ -1104,7 +1082,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         };
         dist_roots();
 #ifdef MIB_PROF
-        uint64_t prof[6] = {0, 0, 0, 0, 0, 0};
+        uint64_t prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         uint64_t pt0 = __builtin_amdgcn_s_memtime();
 #define PMARK(slot)                                      \
   do {                                                   \
@@ -1116,6 +1094,12 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
 #define PMARK(slot) do {} while (0)
 #endif
         for (;;) {
+          // re-assert uniformity of the loop-carried state (free when it already is)
+          acc = (uint32_t)U((int)acc); bo = U(bo); ho = U(ho); pos = U(pos); j = U(j); mbl = U(mbl);
+          insert_len = U(insert_len); copy_len = U(copy_len); dist_code = U(dist_code); distance = U(distance);
+          cmd_blen = U(cmd_blen); lit_blen = U(lit_blen); dist_blen = U(dist_blen); max_dist = U(max_dist);
+          dr0 = U(dr0); dr1 = U(dr1); dr2 = U(dr2); dr3 = U(dr3); dridx = U(dridx); phase = U(phase);
+          c1 = U(c1); c2b = U(c2b);
           if (++guard > guard_limit) {
             HOT_SAVE();
             return MIB_E_NO_PROGRESS;
@@ -1135,10 +1119,12 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               if (tab_lds) cmd_root = U((int)t16[cmd_base + cmd_tree_idx]);
             }
             cmd_blen--;
+            PMARK(8);
             LFILL16();
             const int sym = __builtin_amdgcn_readfirstlane(tab_lds ? lsym16(cmd_root) : lsym(cmd_h, cmd_tree_idx));
             const int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
             dist_code = kCmdLut[4 * sym + 3];
+            PMARK(9);
             LFILL16();
             const int ib = cbits & 0xFF;
             insert_len = ins_off + (ib <= 16 ? lbits(ib) : lmany(ib));
@@ -1164,26 +1150,38 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               if (c2 < batch) batch = c2;
               if (d < batch) batch = d;
               if (d <= 0 && batch <= 0 && a > 0 && b > 0 && c2 > 0) batch = 1;   // Bug J fix
-              lit_blen -= batch;
-              const int end = j + batch;
+              lit_blen = U(lit_blen - batch);
+              const int end = U(j + batch);
+              PMARK(10);
               // 16-bit LDS tables: the context's root is one lookup, (p1 << 3 | lut1[p2]),
               // and lut1 of the literal just decoded is fetched beside it for the next one
               auto lit_run16 = [&]() {
+                acc = (uint32_t)U((int)acc);
+                bo = U(bo);
+                ho = U(ho);
+                j = U(j);
+                pos = U(pos);
+                // literals are gathered in a VGPR (lane = position & 63, v_writelane) and
+                // stored one 64-byte line at a time: one store request per line instead of
+                // one per byte, so the copies' loads wait behind far fewer stores
+                int fl0 = pos;
+                uint32_t ob = 0;
+                auto flush = [&]() {
+                  const int p = (fl0 & ~63) + lane;
+                  if (p >= fl0 && p < pos && p < ring_cap) ring[p] = (uint8_t)ob;
+                  fl0 = pos;
+                };
                 if (trivial) {
                   const int root = U((int)t16[lit_tree]);
                   while (j < end) {
-                    acc = (uint32_t)U((int)acc);
-                    bo = U(bo);
-                    ho = U(ho);
-                    j = U(j);
-                    pos = U(pos);
                     LFILL16();
                     const int val = lsym16(root);
-                    if (pos < ring_cap) ring[pos] = (uint8_t)val;
+                    ob = lane == (pos & 63) ? (uint32_t)val : ob;
                     pos++;
                     j++;
                     c2b = c1;
                     c1 = val;
+                    if ((pos & 63) == 0) flush();
                   }
                   c1 = U(c1);
                   c2b = U(c2b);
@@ -1193,25 +1191,20 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                   LU8 *lut1 = clut + 256;
                   int q2 = U((int)lut1[p2]);
                   while (j < end) {
-                    acc = (uint32_t)U((int)acc);
-                    bo = U(bo);
-                    ho = U(ho);
-                    j = U(j);
-                    pos = U(pos);
-                    p1 = U(p1);
-                    q2 = U(q2);
                     const int root = U((int)croot[(p1 << 3) | q2]);
                     q2 = U((int)lut1[p1]);
                     LFILL16();
                     c2b = p1;
                     p1 = U(lsym16(root));
-                    if (pos < ring_cap) ring[pos] = (uint8_t)p1;
+                    ob = lane == (pos & 63) ? (uint32_t)p1 : ob;
                     pos++;
                     j++;
+                    if ((pos & 63) == 0) flush();
                   }
                   c1 = U(p1);
                   c2b = U(c2b);
                 }
+                if (fl0 != pos) flush();
               };
               auto lit_run = [&](auto g) {
                 if (trivial) {
@@ -1276,6 +1269,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
               };
               if (tab_lds) lit_run16();
               else lit_run(lit_h);
+              PMARK(11);
               wave_sync();
               if (pos >= fence) {
                 s.next_running = ST_INSERT_LOOP;
@@ -1370,21 +1364,31 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
             const int src = (pos - dist) & rmask;
             if (src + cl < rmask && pos + cl < rmask) {
               int lastv = 0;   // each lane's last copied byte: lanes (cl - 1) & 63, (cl - 2) & 63 end the copy
+              // uniform trip counts (lane-dependent loop exits would make the whole loop nest,
+              // and with it the decoder state, divergent: VGPRs instead of SGPRs)
+              const int nit = U((cl + 63) >> 6);
               if (dist >= cl) {
-                for (int k = lane; k < cl; k += 64) {
-                  lastv = ring[src + k];
-                  ring[pos + k] = (uint8_t)lastv;
+                for (int it = 0; it < nit; it++) {
+                  const int k = it * 64 + lane;
+                  if (k < cl) {
+                    lastv = ring[src + k];
+                    ring[pos + k] = (uint8_t)lastv;
+                  }
                 }
               } else {
                 int q = lane % dist;
                 const int qstep = 64 % dist;
-                for (int k = lane; k < cl; k += 64) {
-                  lastv = ring[src + q];
-                  ring[pos + k] = (uint8_t)lastv;
+                for (int it = 0; it < nit; it++) {
+                  const int k = it * 64 + lane;
+                  if (k < cl) {
+                    lastv = ring[src + q];
+                    ring[pos + k] = (uint8_t)lastv;
+                  }
                   q += qstep;
                   if (q >= dist) q -= dist;
                 }
               }
+              PMARK(12);
               if (cl >= 2) {
                 c1 = __builtin_amdgcn_readlane(lastv, (cl - 1) & 63);
                 c2b = __builtin_amdgcn_readlane(lastv, (cl - 2) & 63);
@@ -1392,6 +1396,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                 c2b = c1;
                 c1 = __builtin_amdgcn_readlane(lastv, 0);
               }
+              PMARK(13);
               wave_sync();
               j = copy_len;
               mbl -= cl;
@@ -1409,11 +1414,15 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
                 if (chunk < 1) chunk = 1;
                 // byte p copies the byte dist back, or (overlap) its periodic image before pos
                 const int base = pos - dist;
-                for (int k = lane; k < chunk; k += 64) {
-                  const int p = pos + k;
-                  const int srcp = base + (dist > k ? k : k % dist);
-                  const uint8_t v = ring[srcp & rmask];
-                  if (p < ring_cap) ring[p] = v;
+                const int nit = U((chunk + 63) >> 6);
+                for (int it = 0; it < nit; it++) {
+                  const int k = it * 64 + lane;
+                  if (k < chunk) {
+                    const int p = pos + k;
+                    const int srcp = base + (dist > k ? k : k % dist);
+                    const uint8_t v = ring[srcp & rmask];
+                    if (p < ring_cap) ring[p] = v;
+                  }
                 }
                 wave_sync();
                 mbl -= chunk;
@@ -1439,7 +1448,7 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
         }
 #ifdef MIB_PROF
         if (lane == 0)
-          for (int q = 0; q < 6; q++) atomicAdd(&g_prof[q], (unsigned long long)prof[q]);
+          for (int q = 0; q < 16; q++) atomicAdd(&g_prof[q], (unsigned long long)prof[q]);
 #endif
 #undef PMARK
         HOT_SAVE();
@@ -1450,6 +1459,55 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
 #undef LFILL16
 #undef LREFILL
 #undef U
+        return 0;
+}
+
+// one invocation of decompress(); returns 0, 1 (done), 2 (output full / compound return) or < 0
+__device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
+  int r;
+  if (s.running < 0) return ERR(s, -28);
+  if (s.running == ST_INITED) {
+    fill16(s);
+    int wb;
+    if (bits(s, 1) == 0) wb = 16;
+    else {
+      int n = bits(s, 3);
+      if (n) wb = 17 + n;
+      else {
+        n = bits(s, 3);
+        if (n == 1) wb = -1;
+        else if (n) wb = 8 + n;
+        else wb = 17;
+      }
+    }
+    if (wb == -1) return ERR(s, -11);
+    s.max_ring = 1 << wb;
+    s.max_back = s.max_ring - 16;
+    s.running = ST_BLOCK_START;
+  }
+  int fence = s.ring_size;
+  int rmask = s.ring_size - 1;
+  while (s.running != ST_FINISHED) {
+    if (++s.guard > s.guard_limit) return MIB_E_NO_PROGRESS;
+    switch (s.running) {
+      case ST_BLOCK_START:
+        if (s.mbl < 0) return ERR(s, -10);
+        if ((r = read_next_mb_header(s)) < 0) return r;
+        fence = s.ring_size;
+        if (s.pos + s.mbl <= s.ring_size) fence = 0x7FFFFFFF;
+        rmask = s.ring_size - 1;
+        continue;
+      case ST_COMPRESSED_BLOCK_START:
+        if ((r = read_codes_and_maps(s, dist_extra, dist_offset, ctxmap_table)) < 0) return r;
+        s.running = ST_MAIN_LOOP;
+        continue;
+      case ST_MAIN_LOOP:
+      case ST_INSERT_LOOP:
+      case ST_COPY_LOOP: {
+        {
+          const int rr = s.tab16 ? hot_loop<true>(fence, rmask) : hot_loop<false>(fence, rmask);
+          if (rr < 0) return rr;
+        }
         continue;
       }
       case ST_USE_DICTIONARY:
@@ -1507,12 +1565,12 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
           if (s.pos > s.ring_size) {
             int extra = s.pos - s.ring_size;
             uint8_t v = 0;
-            if (s.lane < extra) v = s.ring[s.ring_size + s.lane];
+            if (LANE < extra) v = s.ring[s.ring_size + LANE];
             wave_sync();
-            if (s.lane < extra) s.ring[s.lane] = v;   // slack <= 37 + 64 bytes
+            if (LANE < extra) s.ring[LANE] = v;   // slack <= 37 + 64 bytes
             if (extra > 64) {
               for (int k = 64; k < extra; k++) {
-                if (s.lane == 0) s.ring[k] = s.ring[s.ring_size + k];
+                if (LANE == 0) s.ring[k] = s.ring[s.ring_size + k];
               }
             }
             wave_sync();
@@ -1536,8 +1594,6 @@ __device__ int decompress(Dec &s, int8_t *dist_extra, int32_t *dist_offset, int3
 //   [ring: ring_bytes][tables: kDecodeTableInts int32][ctx maps: kDecodeCtxBytes][dist luts]
 __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int njobs, uint8_t *scratch,
                                                             uint64_t per_block, uint64_t ring_bytes) {
-  __shared__ Lds lds;
-  __shared__ uint16_t ltab[kLdsTab];
   uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
   uint8_t *ring = base;
   int32_t *tables = reinterpret_cast<int32_t *>(base + ring_bytes);
@@ -1549,9 +1605,8 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
   const int lane = threadIdx.x;
   for (int jb = blockIdx.x; jb < njobs; jb += gridDim.x) {
     DecJob job = jobs[jb];
-    Dec s;
-    s.l = &lds;
-    s.lane = lane;
+    DecS &s = *(DecS *)&g_dec;
+    s.l = &g_lds;
     s.in = job.in;
     s.in_len = job.in_len;
     s.in_off = 0;
@@ -1580,7 +1635,7 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     s.dist_rb_idx = 3;
     s.ring_scratch = ring;
     s.direct = 0;
-    s.tab_lds = ltab;
+    s.tab_lds = g_ltab;
     s.tab16 = s.cmd_base = s.dist_base = 0;
     s.bt = block_trees;
     s.tab_hbm = tables;
@@ -1609,7 +1664,7 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
     s.guard = 0;
     s.guard_limit = 64ull * (job.in_len + 64) * 8 + 4ull * job.out_cap + (1ull << 26);
     // initState (:160-178): fresh zeroed byteBuffer (its stale tail is observable) and block trees
-    for (int i = lane; i < (int)sizeof(lds.win); i += 64) lds.win[i] = 0;
+    for (int i = lane; i < (int)sizeof(g_lds.win); i += 64) g_lds.win[i] = 0;
     for (int i = lane; i <= kBlockTreesCap; i += 64) block_trees[i] = 0;
     __syncthreads();
     if (lane == 0) block_trees[0] = 7;
@@ -1671,8 +1726,8 @@ extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t 
 
 #ifdef MIB_PROF
 extern "C" int mib_debug_read_prof(unsigned long long *out) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_prof), sizeof(unsigned long long) * 8);
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_prof), sizeof(unsigned long long) * 16);
+  unsigned long long z[16] = {0};
   hipMemcpyToSymbol(HIP_SYMBOL(mib::g_prof), z, sizeof(z));
   return 0;
 }

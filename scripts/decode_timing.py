@@ -21,7 +21,7 @@ slot = size + 4096
 dec = torch.empty(k * slot, dtype=torch.uint8, device=dev)
 import ctypes  # noqa: E402
 lib = brotli_amd._L()
-prof = (ctypes.c_ulonglong * 8)()
+prof = (ctypes.c_ulonglong * 16)()
 has_prof = hasattr(lib, 'mib_debug_read_prof')
 for it in range(3):
     sizes, st = ctx.decode(comp.data_ptr(), off, dec.data_ptr(), [i * slot for i in range(k + 1)])
@@ -29,5 +29,5 @@ for it in range(3):
           flush=True)
     if has_prof:
         lib.mib_debug_read_prof(prof)
-        names = ['cmd', 'literals', 'distance', 'copy', 'n_literals', 'n_commands', 'mb_lds_tables', 'mb_hbm_tables']
+        names = ['cmd_tail', 'lit_tail', 'distance', 'copy_rest', 'n_literals', 'n_commands', 'mb_lds_tables', 'mb_hbm_tables', 'cmd_head', 'cmd_sym_lut', 'lit_head', 'lit_loop', 'copy_ldst', 'copy_readlane', 's14', 's15']
         print({n: v / k for n, v in zip(names, prof)}, flush=True)
