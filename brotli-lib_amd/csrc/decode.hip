@@ -955,7 +955,7 @@ __device__ void ring_copy_fast(DecS &s, int src, int cl, int dist) {
 // the kernel spilled ~190 SGPRs into VGPR lanes, read and written back on every command).
 // Returns 0 with s.running set for the state machine, or a negative error code.
 template <bool kTabLds>
-__device__ __noinline__ int hot_loop(int fence_in, int rmask_in) {
+__device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_boundary) {
   DecS &s = *(DecS *)&g_dec;
   const int fence = __builtin_amdgcn_readfirstlane(fence_in), rmask = __builtin_amdgcn_readfirstlane(rmask_in);
         // The command / literal / copy loop runs on registers: the bit reader, positions,
@@ -1023,6 +1023,7 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in) {
     }                                                 \
   } while (0)
         HOT_LOAD();
+        const uint64_t guard0 = guard + 1;
         auto lbits = [&](int n) -> int {
           int v = (int)((acc >> (bo & 31)) & ((1u << n) - 1u));
           bo += n;
@@ -1105,6 +1106,10 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in) {
             return MIB_E_NO_PROGRESS;
           }
           if (phase == ST_MAIN_LOOP) {   // command (:1080-1152)
+            if (stop_at_boundary && guard != guard0) {   // back to the fast loop
+              s.running = ST_MAIN_LOOP;
+              break;
+            }
             if (mbl <= 0) {
               s.running = ST_BLOCK_START;
               break;
@@ -1462,6 +1467,247 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in) {
         return 0;
 }
 
+
+// The common case of the command loop, with no state-machine exits in it: LDS prefix
+// codes, no block switch, no input refill, no ring wrap or flush, no dictionary word.
+// Each command is checked up front (at its start, after its lengths, before its distance)
+// and whatever does not fit is left, at exactly the state the general loop would be in at
+// that point, to hot_loop (which then returns here at the next command boundary).
+// Bits are read in the same order as the general loop; only the refill / block-switch /
+// fence checks it makes are hoisted to where they provably cannot fire.
+template <bool kTrivial>
+__device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
+#define U(x) __builtin_amdgcn_readfirstlane(x)
+  DecS &s = *(DecS *)&g_dec;
+  GU8 *ring = (GU8 *)s.ring;
+  LU16 *win16 = (LU16 *)g_lds.win;
+  LU16 *t16 = (LU16 *)g_ltab;
+  LU16 *croot = (LU16 *)g_lds.ctx_root;
+  LU8 *lut1 = (LU8 *)g_lds.ctx_lut + 256;
+  const int lane = LANE;
+  const int rmask = U(rmask_in);
+  // positions stay below lim: no fence, flush or wrap inside a command
+  const int lim = U(min(fence_in, rmask));
+  const int npostfix = U(s.npostfix), ndirect = U(s.ndirect), max_back = U(s.max_back);
+  uint32_t acc = (uint32_t)U((int)s.acc);
+  int bo = U(s.bo), ho = U(s.ho), pos = U(s.pos), mbl = U(s.mbl);
+  int cmd_blen = U(s.cmd_blen), lit_blen = U(s.lit_blen), dist_blen = U(s.dist_blen), max_dist = U(s.max_dist);
+  int dr0 = U(s.rings[0]), dr1 = U(s.rings[1]), dr2 = U(s.rings[2]), dr3 = U(s.rings[3]), dridx = U(s.dist_rb_idx);
+  int c1 = U((int)s.ring[(pos - 1) & rmask]), c2b = U((int)s.ring[(pos - 2) & rmask]);
+  const int cmd_root = U((int)t16[s.cmd_base + s.cmd_tree_idx]);
+  const int lit_root = kTrivial ? U((int)t16[s.lit_tree_idx]) : 0;
+  uint32_t droot01, droot23;
+  {
+    const int db = s.dist_base, sl = s.dist_ctx_map_slice;
+    const uint8_t *dm = s.dist_ctx_map;
+    const int r0 = t16[db + dm[sl]], r1 = t16[db + dm[sl + 1]], r2 = t16[db + dm[sl + 2]], r3 = t16[db + dm[sl + 3]];
+    droot01 = (uint32_t)U((int)((uint32_t)r0 | ((uint32_t)r1 << 16)));
+    droot23 = (uint32_t)U((int)((uint32_t)r2 | ((uint32_t)r3 << 16)));
+  }
+  int insert_len = 0, copy_len = 0, dist_code = 0, distance = 0, j = 0, phase = ST_MAIN_LOOP;
+  uint32_t ncmd = 0;
+  auto fill = [&]() {   // ho stays below 2080 here: no bounds check
+    if (bo >= 16) {
+      acc = ((uint32_t)U((int)win16[ho]) << 16) | (acc >> 16);
+      ho++;
+      bo -= 16;
+    }
+  };
+  auto rbits = [&](int n) -> int {   // n <= 16 after fill(), or any n <= 24 via two steps
+    int v = (int)((acc >> (bo & 31)) & ((1u << n) - 1u));
+    bo += n;
+    return v;
+  };
+  auto rmany = [&](int n) -> int {
+    if (n <= 16) return rbits(n);
+    const int lo = rbits(16);
+    acc = ((uint32_t)U((int)win16[ho]) << 16) | (acc >> 16);
+    ho++;
+    bo -= 16;
+    return lo | (rbits(n - 16) << 16);
+  };
+  auto sym16 = [&](int root) -> int {
+    const uint32_t v = acc >> (bo & 31);
+    int off = root + (int)(v & 0xFF);
+    const int e0 = U((int)t16[off]);
+    const int nb = e0 >> 12;
+    if (nb <= 8) {
+      bo += nb;
+      return e0 & 0xFFF;
+    }
+    off += (e0 & 0xFFF) + (int)((v & ((1u << nb) - 1u)) >> 8);
+    const int e1 = U((int)t16[off]);
+    bo += (e1 >> 12) + 8;
+    return e1 & 0xFFF;
+  };
+  for (;;) {
+    // ---- command boundary: a block switch or refill goes to the general loop
+    if (mbl <= 0 || cmd_blen == 0 || ho > 2030 - 8) break;
+    uint32_t acc0 = acc;
+    int bo0 = bo, ho0 = ho;
+    fill();
+    const int sym = sym16(cmd_root);
+    const int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
+    dist_code = kCmdLut[4 * sym + 3];
+    fill();
+    insert_len = ins_off + rmany(cbits & 0xFF);
+    fill();
+    copy_len = copy_off + rmany(cbits >> 8);
+    // literals and copy must stay inside this block type, the window and the ring
+    if (insert_len > lit_blen || (int64_t)pos + insert_len + copy_len >= lim ||
+        ho + ((insert_len * 15) >> 4) > 2030 - 12) {
+      // hand the command over undecoded
+      acc = acc0;
+      bo = bo0;
+      ho = ho0;
+      break;
+    }
+    cmd_blen--;
+    // ---- literals
+    if (insert_len) {
+      int fl0 = pos;
+      uint32_t ob = 0;
+      const int end = pos + insert_len;
+      if (kTrivial) {
+        while (pos < end) {
+          fill();
+          const int val = sym16(lit_root);
+          ob = lane == (pos & 63) ? (uint32_t)val : ob;
+          pos++;
+          c2b = c1;
+          c1 = val;
+          if ((pos & 63) == 0) {
+            const int p = (fl0 & ~63) + lane;
+            if (p >= fl0) ring[p] = (uint8_t)ob;
+            fl0 = pos;
+          }
+        }
+      } else {
+        int q2 = U((int)lut1[c2b]);
+        while (pos < end) {
+          const int root = U((int)croot[(c1 << 3) | q2]);
+          q2 = U((int)lut1[c1]);
+          fill();
+          c2b = c1;
+          c1 = U(sym16(root));
+          ob = lane == (pos & 63) ? (uint32_t)c1 : ob;
+          pos++;
+          if ((pos & 63) == 0) {
+            const int p = (fl0 & ~63) + lane;
+            if (p >= fl0) ring[p] = (uint8_t)ob;
+            fl0 = pos;
+          }
+        }
+      }
+      if (fl0 != pos) {
+        const int p = (fl0 & ~63) + lane;
+        if (p >= fl0 && p < pos) ring[p] = (uint8_t)ob;
+      }
+      lit_blen -= insert_len;
+    }
+    ncmd++;
+    // ---- distance: anything unusual hands over with the literals done
+    j = insert_len;
+    phase = ST_INSERT_LOOP;
+    if (mbl - insert_len <= 0 || (dist_code >= 0 && dist_blen == 0) || ho > 2030 - 8) break;
+    const uint32_t dacc = acc;
+    const int dbo = bo, dho = ho, dmax = max_dist;
+    int dc = dist_code;
+    if (dc < 0) {
+      distance = dridx == 0 ? dr0 : dridx == 1 ? dr1 : dridx == 2 ? dr2 : dr3;
+    } else {
+      fill();
+      const uint32_t dpair = dc < 2 ? droot01 : droot23;
+      dc = U(sym16((int)((dpair >> (16 * (dc & 1))) & 0xFFFF)));
+      if (dc < 16) {
+        const int idx = (dridx + (int)((0xfff0006cu >> (2 * dc)) & 3)) & 3;
+        distance = (idx == 0 ? dr0 : idx == 1 ? dr1 : idx == 2 ? dr2 : dr3) + (int)((0xc298b0a626dbull >> (3 * dc)) & 7) - 3;
+      } else {
+        int eb, doff;
+        if (dc < 16 + ndirect) {
+          eb = 0;
+          doff = dc - 15;
+        } else {
+          const int dcp = dc - ndirect - 16, hcode = dcp >> npostfix, lcode = dcp & ((1 << npostfix) - 1);
+          eb = 1 + (hcode >> 1);
+          doff = ((((2 + (hcode & 1)) << eb) - 4) << npostfix) + lcode + ndirect + 1;
+        }
+        int bv;
+        if (bo + eb <= 32) {
+          bv = (int)((acc >> (bo & 31)) & ((1u << eb) - 1u));
+          bo += eb;
+        } else {
+          fill();
+          bv = rmany(eb);
+        }
+        distance = doff + (bv << npostfix);
+      }
+    }
+    if (max_dist != max_back && pos < max_back) max_dist = pos;
+    else max_dist = max_back;
+    const int src = (pos - distance) & rmask;
+    if (distance < 0 || distance > max_dist || copy_len > mbl - insert_len || src + copy_len >= rmask) {
+      // error, dictionary word or wrapping copy: redo the distance in the general loop
+      acc = dacc;
+      bo = dbo;
+      ho = dho;
+      max_dist = dmax;
+      break;
+    }
+    mbl -= insert_len;
+    if (dist_code >= 0) dist_blen--;
+    if (dc > 0) {
+      dridx = (dridx + 1) & 3;
+      if (dridx == 0) dr0 = distance;
+      else if (dridx == 1) dr1 = distance;
+      else if (dridx == 2) dr2 = distance;
+      else dr3 = distance;
+    }
+    // ---- copy (no wrap, no fence)
+    {
+      const int cl = copy_len, dist = distance;
+      int lastv = 0;
+      const int nit = U((cl + 63) >> 6);
+      if (dist >= cl) {
+        for (int it = 0; it < nit; it++) {
+          const int k = it * 64 + lane;
+          if (k < cl) {
+            lastv = ring[src + k];
+            ring[pos + k] = (uint8_t)lastv;
+          }
+        }
+      } else {
+        int q = lane % dist;
+        const int qstep = 64 % dist;
+        for (int it = 0; it < nit; it++) {
+          const int k = it * 64 + lane;
+          if (k < cl) {
+            lastv = ring[src + q];
+            ring[pos + k] = (uint8_t)lastv;
+          }
+          q += qstep;
+          if (q >= dist) q -= dist;
+        }
+      }
+      c2b = cl >= 2 ? __builtin_amdgcn_readlane(lastv, (cl - 2) & 63) : c1;
+      c1 = __builtin_amdgcn_readlane(lastv, (cl - 1) & 63);
+      mbl -= cl;
+      pos += cl;
+    }
+    phase = ST_MAIN_LOOP;
+    j = 0;
+  }
+  wave_sync();
+  s.acc = acc; s.bo = bo; s.ho = ho; s.pos = pos; s.mbl = mbl;
+  s.cmd_blen = cmd_blen; s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist;
+  s.rings[0] = dr0; s.rings[1] = dr1; s.rings[2] = dr2; s.rings[3] = dr3; s.dist_rb_idx = dridx;
+  s.insert_len = insert_len; s.copy_len = copy_len; s.dist_code = dist_code; s.j = j;
+  s.guard += 3ull * ncmd;
+  s.running = phase;
+  return 0;
+#undef U
+}
+
 // one invocation of decompress(); returns 0, 1 (done), 2 (output full / compound return) or < 0
 __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
   int r;
@@ -1505,7 +1751,18 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
       case ST_INSERT_LOOP:
       case ST_COPY_LOOP: {
         {
-          const int rr = s.tab16 ? hot_loop<true>(fence, rmask) : hot_loop<false>(fence, rmask);
+          int rr;
+          if (s.tab16) {
+            if (s.running == ST_MAIN_LOOP) {
+              rr = s.trivial_lit_ctx ? fast_loop<true>(fence, rmask) : fast_loop<false>(fence, rmask);
+              if (rr < 0) return rr;
+            }
+            // what the fast loop left (a block switch, a refill, a dictionary word, a wrap,
+            // the block end ...): one command of the general loop
+            rr = hot_loop<true>(fence, rmask, 1);
+          } else {
+            rr = hot_loop<false>(fence, rmask, 0);
+          }
           if (rr < 0) return rr;
         }
         continue;
