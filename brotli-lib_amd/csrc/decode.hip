@@ -1540,7 +1540,20 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     bo += (e1 >> 12) + 8;
     return e1 & 0xFFF;
   };
+#ifdef MIB_PROF
+  uint64_t fp[5] = {0, 0, 0, 0, 0};
+  uint64_t ft0 = __builtin_amdgcn_s_memtime();
+#define FMARK(k)                                      \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    fp[k] += t_ - ft0;                                \
+    ft0 = t_;                                         \
+  } while (0)
+#else
+#define FMARK(k) do {} while (0)
+#endif
   for (;;) {
+    FMARK(4);
     // ---- command boundary: a block switch or refill goes to the general loop
     if (mbl <= 0 || cmd_blen == 0 || ho > 2030 - 8) break;
     uint32_t acc0 = acc;
@@ -1563,6 +1576,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       break;
     }
     cmd_blen--;
+    FMARK(0);
     // ---- literals
     if (insert_len) {
       int fl0 = pos;
@@ -1606,6 +1620,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       lit_blen -= insert_len;
     }
     ncmd++;
+    FMARK(1);
     // ---- distance: anything unusual hands over with the literals done
     j = insert_len;
     phase = ST_INSERT_LOOP;
@@ -1663,6 +1678,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       else if (dridx == 2) dr2 = distance;
       else dr3 = distance;
     }
+    FMARK(2);
     // ---- copy (no wrap, no fence)
     {
       const int cl = copy_len, dist = distance;
@@ -1696,6 +1712,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     }
     phase = ST_MAIN_LOOP;
     j = 0;
+    FMARK(3);
   }
   wave_sync();
   s.acc = acc; s.bo = bo; s.ho = ho; s.pos = pos; s.mbl = mbl;
@@ -1704,8 +1721,16 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   s.insert_len = insert_len; s.copy_len = copy_len; s.dist_code = dist_code; s.j = j;
   s.guard += 3ull * ncmd;
   s.running = phase;
+#ifdef MIB_PROF
+  if (lane == 0) {
+    atomicAdd(&g_prof[14], (unsigned long long)ncmd);
+    atomicAdd(&g_prof[15], 1ull);
+    for (int q = 0; q < 5; q++) atomicAdd(&g_prof[8 + q], (unsigned long long)fp[q]);
+  }
+#endif
   return 0;
 #undef U
+#undef FMARK
 }
 
 // one invocation of decompress(); returns 0, 1 (done), 2 (output full / compound return) or < 0

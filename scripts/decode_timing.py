@@ -29,5 +29,5 @@ for it in range(3):
           flush=True)
     if has_prof:
         lib.mib_debug_read_prof(prof)
-        names = ['cmd_tail', 'lit_tail', 'distance', 'copy_rest', 'n_literals', 'n_commands', 'mb_lds_tables', 'mb_hbm_tables', 'cmd_head', 'cmd_sym_lut', 'lit_head', 'lit_loop', 'copy_ldst', 'copy_readlane', 's14', 's15']
+        names = ['cmd_tail', 'lit_tail', 'distance', 'copy_rest', 'n_literals', 'n_commands', 'mb_lds_tables', 'mb_hbm_tables', 'F_cmd', 'F_lit', 'F_dist', 'F_copy', 'F_top', 'copy_readlane', 'fast_cmds', 'fast_calls']
         print({n: v / k for n, v in zip(names, prof)}, flush=True)
