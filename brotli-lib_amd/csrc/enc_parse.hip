@@ -45,6 +45,7 @@ constexpr int kC = 5;                 // chunks: batch offset (< 64) + longest r
 constexpr int kDpWaves = 4;           // segments (waves) per workgroup, sharing the length table
 constexpr int kLenTab = kLongCopy + 1;
 constexpr float kInf = 3.0e38f;
+constexpr uint32_t kCostLast = 255;   // cost code of a match at the path's last distance
 static_assert(63 + kLongCopy < 64 * kC, "every relaxed length must land in a chunk");
 
 typedef const __attribute__((address_space(1))) uint8_t GCU8;
@@ -138,7 +139,8 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
   if (lane == 0) wc[0] = 0.f;   // node a
   // the current batch (registers, lane = position - i0) and the next one
   uint32_t bm[kMaxMatches], binfo = 0;   // binfo: nm | maxlen << 8 (clipped to the segment)
-  float bmc[kMaxMatches], blc = 0.f;
+  uint32_t bmc[kMaxMatches];              // distance | distance-cost code << 24 (quarter bits)
+  float blc = 0.f;
   Staged pf;
   uint32_t pf_at = a;
   if (a + lane < b) load_staged(pf, matches, data, gbase + a + lane, a + lane);
@@ -166,13 +168,14 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
       bm[q] = 0;
-      bmc[q] = 0.f;
+      bmc[q] = 0;
       if ((uint32_t)q < nm) {
         uint32_t extra;
         const uint32_t ln = min(match_length(cur.m[q]), b - p);
         const uint32_t dp = dist_prefix(match_dist(cur.m[q]) + 15, ndirect, npostfix, &extra);
         bm[q] = (ln << 24) | match_dist(cur.m[q]);
-        bmc[q] = (float)(dp >> 10) + dist_sym_cost(dp & 0x3FFu);
+        const float dc = (float)(dp >> 10) + dist_sym_cost(dp & 0x3FFu);
+        bmc[q] = match_dist(cur.m[q]) | (min((uint32_t)(dc * 4.f + 0.5f), kCostLast - 1) << 24);
         maxlen = ln;
       }
     }
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
           if (match_length(m) > (uint32_t)kLongCopy) {
             fd = match_dist(m);
             fl = match_length(m);
-            fdc = rdlf(bmc[q], off);
+            fdc = (float)(rdl(bmc[q], off) >> 24) * 0.25f;
           }
         }
       }
@@ -254,18 +257,20 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
       DPMARK(2);
       continue;
     }
-    // the match staircase of i: lengths (clipped), distances, distance costs
-    uint32_t mL[kMaxMatches], md[kMaxMatches];
-    float mc[kMaxMatches];
+    // the match staircase of i: lengths (clipped, scalar) and the packed (distance | cost
+    // code) words, moved once into wave-uniform VGPRs so that each chunk selects with one
+    // compare and one v_cndmask per match; a match at the path's last distance gets the
+    // code kCostLast (priced with short code 0)
+    uint32_t mL[kMaxMatches], vpk[kMaxMatches];
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
-      mL[q] = md[q] = 0;
-      mc[q] = 0.f;
+      mL[q] = 0;
+      vpk[q] = 0;
       if ((uint32_t)q < nm) {
-        const uint32_t m = rdl(bm[q], off);
-        mL[q] = match_length(m);
-        md[q] = match_dist(m);
-        mc[q] = rdlf(bmc[q], off);
+        mL[q] = match_length(rdl(bm[q], off));
+        uint32_t pk = rdl(bmc[q], off);
+        if (match_dist(pk) == ld) pk |= kCostLast << 24;
+        vpk[q] = pk;
       }
     }
     const uint32_t maxrel = max(1u, maxlen);
@@ -280,19 +285,18 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
       uint32_t nd = ld, nmeta = min(ins + 1, 65535u) << 16;
       if (l == 1) cand = ci + litcost;
       if (l >= 4 && l <= maxlen) {
-        uint32_t sd = 0;
-        float sc = 0.f;
+        uint32_t x = 0;
 #pragma unroll
         for (int q = kMaxMatches - 1; q >= 0; q--)
-          if (l <= mL[q]) {   // mL = 0 past nm
-            sd = md[q];
-            sc = mc[q];
-          }
+          x = l <= mL[q] ? vpk[q] : x;   // mL = 0 past nm
         const uint32_t tv = trow[l];
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
-        cand = base + (sd == ld ? pl : pn + sc);
-        nd = sd;
+        const uint32_t cc = x >> 24;
+        const float alt = pn + (float)cc * 0.25f;
+        const uint32_t use_last = 0u - (uint32_t)(cc == kCostLast);   // a select, not a branch
+        cand = base + __uint_as_float((__float_as_uint(pl) & use_last) | (__float_as_uint(alt) & ~use_last));
+        nd = match_dist(x);
         nmeta = l;
       }
       if (cand < wc[c]) {
