@@ -1,32 +1,41 @@
 #!/usr/bin/env python3
 """bench.py -- BASELINE.json metric: encode+decode MB/s at q11 lgwin=22 on 1/2/4/8 MI355X.
 
-Workload (one "step" = one pass of the hot path over one batch):
-  C4 per-GPU shard: 1024 independent 1 MiB enwik-style text buffers per GPU, resident in
-  HBM, quality 11, lgwin 22, GENERIC mode.  A step encodes the shard (mib_ctx_encode:
-  packed compressed streams in HBM), gathers the compressed shards to rank 0 over RCCL
-  (N > 1; the only collective) and decodes the shard back
-  (mib_ctx_decode) into HBM.  Round-trip bit-exactness is checked on device after the
-  warmup steps (outside the timed region).
+Workloads (one "step" = one pass of the hot path over one batch; inputs are
+resident in HBM when the timed region starts):
+  c4 (default)  C4 per-GPU shard: 1024 independent 1 MiB enwik-style text buffers per GPU,
+                q11, lgwin 22, GENERIC -- the configuration the metric's 1/2/4/8-GPU
+                numbers are quoted on.
+  c3            C3: 1024 x 256 KiB WOFF2-transformed-glyf-like buffers per GPU, q11, FONT.
+  c2            C2: one 64 MiB enwik-style buffer, q11 GENERIC (one stream: replicas at N > 1).
+A step encodes the batch (mib_ctx_encode: packed compressed streams in HBM), gathers the
+compressed shards to rank 0 over RCCL (N > 1, c3/c4; the only collective)
+and decodes them back (mib_ctx_decode) into HBM.  The round trip is checked bit-exact on
+device after the warmup steps (outside the timed region).
   value = uncompressed MB (10^6 B) processed by all ranks / step time (max over ranks).
   scaling "weak": per-GPU work fixed as N grows.
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 via torch.distributed.run
-(one rank per GPU, backend nccl = RCCL).
+Launch: python bench.py [--gpus N --steps K --warmup W --workload c4|c3|c2]; N > 1 via
+torch.distributed.run (one rank per GPU, backend nccl = RCCL).
 
 roofline: the step's dominant kernel (largest device time, HIP events recorded by the
-library on the launch stream), achieved = algorithmic bytes of one launch (input +
-output bytes of the streams it processed) / its mean launch time;
-peak = 8.0 TB/s HBM3E (MI355X_MICROARCH.md).  traffic = HBM bytes per launch from the
-rocprofv3 PMC passes committed in profiles/ (scripts/collect_pmc.sh), or null.
+library on the launch stream); achieved = algorithmic bytes of one launch (input + output
+bytes of the streams it processed) / its mean launch time; peak = 8.0 TB/s
+HBM3E (MI355X_MICROARCH.md).  traffic = HBM bytes per launch from the rocprofv3 PMC passes
+committed in profiles/ (scripts/collect_pmc.py), or null.
 
 cpu_baseline: the oracle (CPU restatement of the reference's q11 encoder + decoder,
-oracle/) on a bounded sample of the same workload, one buffer per host thread, rank 0.
+oracle/) on a bounded sample of the SAME buffers the GPU encoded (copied back from HBM),
+one buffer per host thread on every core of this process's CPU share, rank 0 only.  The
+same sample gives the compressed-size comparison GPU vs reference (ref-fixed) vs Node's
+native brotli (when `node` exists), all on identical bytes.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -34,6 +43,12 @@ sys.path.insert(0, os.path.join(ROOT, 'brotli-lib_amd', 'python'))
 
 MIB = 1 << 20
 PEAK_HBM_GBS = 8000.0
+WORKLOADS = {
+    # name: (streams per GPU, bytes per stream, mode, seed base, generator)
+    'c4': (1024, MIB, 0, 2000, 'enwik'),
+    'c3': (1024, 256 * 1024, 2, 1000, 'glyf'),
+    'c2': (1, 64 * MIB, 0, 2, 'enwik'),
+}
 
 
 def parse():
@@ -41,63 +56,145 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--streams', type=int, default=1024, help='buffers per GPU')
-    ap.add_argument('--size', type=int, default=MIB, help='bytes per buffer')
+    ap.add_argument('--workload', default='c4', choices=sorted(WORKLOADS))
+    ap.add_argument('--streams', type=int, default=-1, help='buffers per GPU (-1: the workload\'s)')
+    ap.add_argument('--size', type=int, default=-1, help='bytes per buffer (-1: the workload\'s)')
     ap.add_argument('--quality', type=int, default=11)
     ap.add_argument('--lgwin', type=int, default=22)
-    ap.add_argument('--cpu-sample', type=int, default=-1, help='buffers in the CPU baseline sample (-1 auto)')
+    ap.add_argument('--cpu-seconds', type=float, default=10.0, help='target wall time of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true')
     return ap.parse_args()
 
 
-def cpu_baseline(args):
-    """Oracle q11 encode + decode of 1 MiB buffers, one per thread (ctypes drops the GIL)."""
+def cpu_share():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota and by the
+    box's per-GPU share (OMP_NUM_THREADS is set to it on the GPU boxes; os.cpu_count()
+    shows the whole machine there)."""
+    n = len(os.sched_getaffinity(0))
+    if os.environ.get('OMP_NUM_THREADS', '').isdigit():
+        n = min(n, int(os.environ['OMP_NUM_THREADS']))
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            q, p = f.read().split()
+        if q != 'max':
+            n = min(n, max(1, int(int(q) // int(p))))
+    except Exception:
+        pass
+    return max(1, n)
+
+
+def make_inputs(wl, k, size, rank, dev):
+    """The batch, generated straight into HBM (k streams of `size` bytes, packed)."""
+    import numpy as np
+    import torch
+    from brotli_amd import datagen
+    _, _, _, seed0, gen = WORKLOADS[wl]
+    if gen == 'enwik':
+        # one device-generated text, cut into k buffers (seed per rank)
+        return datagen.enwik_device(k * size, seed0 + rank * 7919, dev)
+    from concurrent.futures import ProcessPoolExecutor
+    seeds = [seed0 + rank * k + i for i in range(k)]
+    with ProcessPoolExecutor(max(1, min(16, cpu_share()))) as ex:
+        bufs = list(ex.map(datagen.glyf_stream, [size] * k, seeds, chunksize=16))
+    host = np.frombuffer(b''.join(bufs), dtype=np.uint8)
+    return torch.from_numpy(host.copy()).to(dev)
+
+
+def node_native(sample, quality, lgwin, mode):
+    """Node's bundled native brotli (zlib.brotliCompressSync) on the same sample: sizes."""
+    try:
+        subprocess.run(['node', '--version'], check=True, capture_output=True, timeout=30)
+    except Exception:
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        paths = []
+        for i, b in enumerate(sample):
+            p = os.path.join(td, '%d.bin' % i)
+            with open(p, 'wb') as f:
+                f.write(b)
+            paths.append(p)
+        js = ("const z=require('zlib'),fs=require('fs');let t=0,s=0;const c=z.constants;"
+              "for(const p of process.argv.slice(1)){const d=fs.readFileSync(p);const t0=process.hrtime.bigint();"
+              "const e=z.brotliCompressSync(d,{params:{[c.BROTLI_PARAM_QUALITY]:%d,[c.BROTLI_PARAM_LGWIN]:%d,"
+              "[c.BROTLI_PARAM_MODE]:%d,[c.BROTLI_PARAM_SIZE_HINT]:d.length}});t+=Number(process.hrtime.bigint()-t0);s+=e.length;}"
+              "console.log(JSON.stringify({bytes:s,ns:t}));" % (quality, lgwin, mode))
+        try:
+            r = subprocess.run(['node', '-e', js] + paths, check=True, capture_output=True, timeout=600)
+            return json.loads(r.stdout.decode().strip().splitlines()[-1])
+        except Exception:
+            return None
+
+
+def cpu_baseline(sample, gpu_sizes, args, mode, what):
+    """Oracle q11 encode + decode of the sample buffers, one per thread (ctypes drops the GIL)."""
     from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, 'tests'))
     import _oracle
-    from brotli_amd import datagen
-    threads = max(1, min(16, os.cpu_count() or 1))
-    nbuf = args.cpu_sample if args.cpu_sample > 0 else threads
-    bufs = [datagen.enwik_text(args.size, 2000 + i) for i in range(nbuf)]
     _oracle.lib()
+    threads = cpu_share()
+
+    bad = []
 
     def one(d):
-        e = _oracle.encode(d, args.quality, args.lgwin)
-        assert _oracle.decode(e) == d
+        e = _oracle.encode(d, args.quality, args.lgwin, mode)
+        if _oracle.decode(e) != d:   # the reference encoder's own output failing its round trip
+            bad.append(d)
+            if os.environ.get('BENCH_DUMP_DIR'):
+                os.makedirs(os.environ['BENCH_DUMP_DIR'], exist_ok=True)
+                with open(os.path.join(os.environ['BENCH_DUMP_DIR'], 'oracle_bad_%d.bin' % len(bad)), 'wb') as f:
+                    f.write(d)
+                with open(os.path.join(os.environ['BENCH_DUMP_DIR'], 'oracle_bad_%d.br' % len(bad)), 'wb') as f:
+                    f.write(e)
         return len(e)
 
-    t0 = time.time()
+    # bounded: whole rounds of `threads` buffers until the target time is reached
+    sizes, done, t0 = [], 0, time.time()
     with ThreadPoolExecutor(threads) as ex:
-        sizes = list(ex.map(one, bufs))
+        while done < len(sample) and (time.time() - t0) < args.cpu_seconds:
+            batch = sample[done:done + threads]
+            sizes += list(ex.map(one, batch))
+            done += len(batch)
     dt = time.time() - t0
-    return {'value': round(nbuf * args.size / 1e6 / dt, 4), 'unit': 'MB/s', 'cores': min(threads, nbuf),
-            'kind': 'port',
-            'sample': '%d x %d B enwik-style buffers (seeds 2000+i), oracle q%d encode + decode, %d threads, %.1f s wall, '
-                      'ratio %.4f' % (nbuf, args.size, args.quality, min(threads, nbuf), dt,
-                                      sum(sizes) / (nbuf * args.size))}
+    nbytes = sum(len(b) for b in sample[:done])
+    ratio_ref = sum(sizes) / nbytes
+    ratio_gpu = sum(gpu_sizes[:done]) / nbytes
+    nn = min(done, 8)   # native brotli q11 runs ~1 MB/s on one core: a smaller sub-sample
+    nat = node_native(sample[:nn], args.quality, args.lgwin, mode)
+    nn_bytes = sum(len(b) for b in sample[:nn])
+    return {'value': round(nbytes / 1e6 / dt, 4), 'unit': 'MB/s', 'cores': min(threads, done), 'kind': 'port',
+            'sample': '%d x %d B %s (the first buffers the GPU encoded, copied back), oracle q%d encode + decode, '
+                      '%d threads (host nproc %d, CPU share %d), %.1f s wall' % (
+                          done, len(sample[0]), what, args.quality, min(threads, done), os.cpu_count() or 0,
+                          threads, dt)}, {
+        'sample_buffers': done, 'oracle_roundtrip_failures': len(bad), 'gpu': round(ratio_gpu, 5), 'oracle_ref_fixed': round(ratio_ref, 5),
+        'gpu_vs_ref_fixed': round(ratio_gpu / ratio_ref, 4),
+        'node_native_sample_buffers': nn if nat else 0,
+        'node_native_brotli': round(nat['bytes'] / nn_bytes, 5) if nat else None,
+        'gpu_vs_node_native': round(sum(gpu_sizes[:nn]) / nat['bytes'], 4) if nat else None,
+        'node_native_MBps_1thread': round(nn_bytes / 1e6 / (nat['ns'] * 1e-9), 3) if nat else None}
 
 
-def load_traffic(kernel, launch_bytes):
-    """HBM bytes per launch of `kernel` from profiles/pmc_summary.json (collect_pmc.sh)."""
+def load_traffic(kernel):
+    """HBM bytes per launch of `kernel` from profiles/pmc_summary.json (collect_pmc.py)."""
     p = os.path.join(ROOT, 'profiles', 'pmc_summary.json')
     try:
         with open(p) as f:
             d = json.load(f)
-        k = d['kernels'][kernel]
-        return int(k['hbm_bytes_per_launch'])
+        return int(d['kernels'][kernel]['hbm_bytes_per_launch'])
     except Exception:
         return None
 
 
 def main():
     args = parse()
+    wl = args.workload
+    k0, size0, mode, _, gen = WORKLOADS[wl]
+    k = args.streams if args.streams > 0 else k0
+    size = args.size if args.size > 0 else size0
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)   # before any device work
 
     import torch
     import torch.distributed as dist
@@ -106,20 +203,19 @@ def main():
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
     import brotli_amd
-    from brotli_amd import datagen, shard
+    from brotli_amd import shard
 
-    k, size = args.streams, args.size
     total = k * size
-    data = datagen.enwik_device(total, 2000 + rank, dev)
+    data = make_inputs(wl, k, size, rank, dev)
     in_off = [i * size for i in range(k + 1)]
     cap = total + total // 8 + 4096 * k
     comp = torch.empty(cap, dtype=torch.uint8, device=dev)
-    # output slots with room for a one-metablock stream's ring: the decoder writes in place
-    slot = size + 4096
+    slot = size + 4096   # decoded output slots (+ the decoder's slack)
     dec = torch.empty(k * slot, dtype=torch.uint8, device=dev)
     dec_off = [i * slot for i in range(k + 1)]
     ctx = brotli_amd.DeviceContext(local, profiling=True)
-    opts = {'quality': args.quality, 'lgwin': args.lgwin}
+    opts = {'quality': args.quality, 'lgwin': args.lgwin, 'mode': mode}
+    gather = world > 1 and k > 1 and not args.no_gather
 
     def step(times):
         out_off = ctx.encode(data.data_ptr(), in_off, comp.data_ptr(), cap, opts)
@@ -127,7 +223,7 @@ def main():
             t = times.setdefault(name, [0.0, 0])
             t[0] += ms
             t[1] += n
-        if world > 1 and not args.no_gather:
+        if gather:
             # the one collective: RCCL gather of the variable-length compressed shards to rank 0
             lens = [out_off[i + 1] - out_off[i] for i in range(k)]
             shard.gather_shards(comp[:out_off[-1]], lens, dst=0)
@@ -145,6 +241,7 @@ def main():
     if bad or not torch.equal(dec.view(k, slot)[:, :size], data.view(k, size)):
         raise SystemExit('round trip FAILED on rank %d: %d bad streams' % (rank, len(bad)))
     comp_bytes = out_off[-1]
+    gpu_sizes = [out_off[i + 1] - out_off[i] for i in range(k)]
 
     times = {}
     if world > 1:
@@ -166,18 +263,40 @@ def main():
         comp_all = int(cb.item())
     else:
         comp_all = comp_bytes
+
+    cpu, ratios = None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the CPU sample: the first buffers of the same batch (C2: 1 MiB slices of its one buffer)
+        piece = min(size, MIB)
+        nsamp = min(max(1, total // piece), 16 * cpu_share())
+        host = data[:nsamp * piece].cpu().numpy().tobytes()
+        sample = [host[i * piece:(i + 1) * piece] for i in range(nsamp)]
+        if piece == size:
+            samp_gpu = gpu_sizes[:nsamp]
+        else:   # GPU sizes of the slices: encode them alone on the device
+            s_in = torch.frombuffer(bytearray(host), dtype=torch.uint8).to(dev)
+            s_cap = nsamp * (piece + piece // 8 + 4096)
+            s_out = torch.empty(s_cap, dtype=torch.uint8, device=dev)
+            s_off = ctx.encode(s_in.data_ptr(), [i * piece for i in range(nsamp + 1)], s_out.data_ptr(), s_cap, opts)
+            samp_gpu = [s_off[i + 1] - s_off[i] for i in range(nsamp)]
+        what = {'enwik': 'enwik-style text', 'glyf': 'WOFF2-glyf-like streams'}[gen]
+        cpu, ratios = cpu_baseline(sample, samp_gpu, args, mode, what)
+
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         mb = world * total / 1e6
         enc_ms = sum(v[0] for n, v in times.items() if n != 'decode_streams_kernel') / args.steps
         dec_ms = times.get('decode_streams_kernel', [0.0, 1])[0] / args.steps
-        dom = max(times.items(), key=lambda kv: kv[1][0])
-        dom_name, (dom_ms, dom_n) = dom[0], dom[1]
-        # a kernel launched L times per step covers 1/L of the shard per launch
+        dom_name, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
+        # a kernel launched L times per step covers 1/L of the batch per launch
         launches_per_step = max(1, dom_n // args.steps)
         launch_bytes = (total + comp_bytes) // launches_per_step
         avg_ms = dom_ms / max(1, dom_n)
         achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+        desc = {'c4': 'C4 per-GPU shard: %d x %d B enwik-style text, q%d lgwin%d GENERIC',
+                'c3': 'C3: %d x %d B WOFF2-glyf-like streams, q%d lgwin%d FONT',
+                'c2': 'C2: %d x %d B enwik-style text (one stream), q%d lgwin%d GENERIC'}[wl] % (
+                    k, size, args.quality, args.lgwin)
         res = {
             'metric': 'encode+decode MB/s at q11 lgwin=22',
             'value': round(mb / dt * args.steps, 3),
@@ -191,18 +310,19 @@ def main():
             'vs_baseline': None,
             'dtype': 'u8',
             'data': 'synthetic',
-            'config': {'workload': 'C4 per-GPU shard: %d x %d B enwik-style text, q%d lgwin%d GENERIC, encode -> %s'
-                                   'decode round trip (bit-exact checked)' % (
-                                       k, size, args.quality, args.lgwin, 'RCCL gather -> ' if world > 1 else ''),
-                       'streams_per_gpu': k, 'bytes_per_stream': size, 'quality': args.quality, 'lgwin': args.lgwin,
-                       'parallelism': 'shard%d' % world},
+            'config': {'workload': desc + ', encode -> %sdecode round trip (bit-exact checked)' % (
+                           'RCCL gather -> ' if gather else ''),
+                       'name': wl, 'streams_per_gpu': k, 'bytes_per_stream': size, 'quality': args.quality,
+                       'lgwin': args.lgwin, 'mode': mode,
+                       'parallelism': ('shard%d' % world) if k > 1 else ('replicas%d' % world)},
             'encode_MBps': round(mb / (enc_ms * 1e-3), 3) if enc_ms else None,
             'decode_MBps': round(mb / (dec_ms * 1e-3), 3) if dec_ms else None,
             'compressed_ratio': round(comp_all / (world * total), 5),
+            'ratio_same_sample': ratios,
             'kernel_ms_per_step': {n: round(v[0] / args.steps, 3) for n, v in sorted(times.items())},
             'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 3), 'peak': PEAK_HBM_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 6),
-                         'traffic': load_traffic(dom_name, launch_bytes),
+                         'traffic': load_traffic(dom_name) if wl == 'c4' else None,
                          'algorithmic_bytes_per_launch': launch_bytes, 'avg_launch_ms': round(avg_ms, 3)},
             'cpu_baseline': cpu,
         }

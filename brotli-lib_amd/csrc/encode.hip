@@ -41,6 +41,8 @@ using namespace mib;
 using namespace mib::enc;
 
 extern "C" mib_ctx *mib_default_ctx(void);
+extern "C" void mib_default_lock(int on);
+extern "C" int mib_ctx_ready(mib_ctx *c);
 extern "C" void *mib_ctx_stream_of(mib_ctx *c);
 extern "C" int mib_ctx_device_of(mib_ctx *c);
 extern "C" void mib_ctx_clear_times(mib_ctx *c);
@@ -337,14 +339,28 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   return 0;
 }
 
-// workspace is ~72 bytes per position (keys 16, match records 32, choice 8, commands ~16): groups
-// of at most this many positions (~70 GB)
-constexpr uint64_t kGroupPositions = 1ull << 30;
+// Workspace is ~72 bytes per position (keys 16, match records 32, choice 8, commands ~16).
+// A call is split into as few groups as device memory allows -- one group when it fits, so
+// no small tail group runs a whole parse at low occupancy -- below the 2^31 position limit
+// of the 32-bit position indices.
+constexpr uint64_t kWsBytesPerPosition = 80;
 constexpr size_t kGroupStreams = 16384;   // job index must fit the 15-bit key field
+
+uint64_t group_position_limit(mib_ctx *ctx) {
+  size_t free_b = 0, total_b = 0;
+  uint64_t lim = (1ull << 31) - 4 * (uint64_t)kSeg;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    const Workspace *ws = reinterpret_cast<const Workspace *>(*mib_ctx_enc_ws(ctx));
+    const uint64_t usable = ((uint64_t)free_b + (ws ? ws->cap : 0)) / 10 * 8;   // leave 20% to the caller
+    lim = std::min<uint64_t>(lim, std::max<uint64_t>(usable / kWsBytesPerPosition, 1ull << 24));
+  }
+  return lim;
+}
 
 // Split k streams into groups and encode them back to back into d_out.
 int encode_streams(mib_ctx *ctx, const mib_enc_opts *o, const StreamDesc *sd, size_t k, uint8_t *d_out,
                    uint64_t out_cap, uint64_t *out_offsets, int32_t (*dc_out)[4], hipStream_t st) {
+  const uint64_t kGroupPositions = group_position_limit(ctx);
   Params prm = make_params(o);
   out_offsets[0] = 0;
   size_t i = 0;
@@ -420,8 +436,7 @@ void mib_encode_ws_free(void *p) {
 int mib_ctx_encode(mib_ctx *c, const mib_enc_opts *o, const uint8_t *d_in, const uint64_t *in_offsets, size_t k,
                    uint8_t *d_out, uint64_t out_cap, uint64_t *out_offsets, void *stream) {
   if (!c || !out_offsets || (k && (!d_in || !in_offsets || !d_out))) return MIB_E_INVALID_ARG;
-  if (!mib_default_ctx()) return MIB_E_NO_DEVICE;   // device checks + tables
-  CK(hipSetDevice(mib_ctx_device_of(c)));
+  if (mib_ctx_ready(c) != 0) return MIB_E_NO_DEVICE;   // this context's device: gfx950 check, tables
   hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)mib_ctx_stream_of(c);
   mib_ctx_clear_times(c);
   Params prm = make_params(o);
@@ -434,8 +449,14 @@ int mib_ctx_encode(mib_ctx *c, const mib_enc_opts *o, const uint8_t *d_in, const
 }
 
 // host buffers -> device -> encode -> host
+struct DefaultLock {   // the default context serves one host call at a time (runtime.cpp)
+  DefaultLock() { mib_default_lock(1); }
+  ~DefaultLock() { mib_default_lock(0); }
+};
+
 static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status,
                        mib_encoder *streaming, bool final_) {
+  DefaultLock use;
   mib_ctx *c = mib_default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
   CK(hipSetDevice(mib_ctx_device_of(c)));

@@ -34,8 +34,9 @@ namespace {
   } while (0)
 
 std::mutex g_mu;
-int g_device = 0;
-bool g_inited = false;
+int g_device = 0;                 // device of the default context (mib_init)
+constexpr int kMaxDevices = 64;
+bool g_dev_ready[kMaxDevices];    // per device: checked to be gfx950, command table uploaded
 
 void build_cmd_lut(int16_t *lut) {   // engine.ts:65-90
   static const int ins_bits[24] = {0, 0, 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 7, 8, 9, 10, 12, 14, 24};
@@ -63,24 +64,36 @@ void build_cmd_lut(int16_t *lut) {   // engine.ts:65-90
   }
 }
 
-int ensure_init() {
+// Every device a context runs on is checked (gfx950) and gets its own copy of the decoder's
+// __constant__ command table: module globals are per device.  Leaves `device` current.
+int ensure_device(int device) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_inited) return 0;
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MIB_E_NO_DEVICE;
-  if (g_device >= n) return MIB_E_NO_DEVICE;
-  HIP_OK(hipSetDevice(g_device));
+  if (device < 0 || device >= n || device >= kMaxDevices) return MIB_E_NO_DEVICE;
+  HIP_OK(hipSetDevice(device));
+  if (g_dev_ready[device]) return 0;
   hipDeviceProp_t prop;
-  HIP_OK(hipGetDeviceProperties(&prop, g_device));
+  HIP_OK(hipGetDeviceProperties(&prop, device));
   if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-    fprintf(stderr, "brotli_amd: device %d is %s, this build targets gfx950\n", g_device, prop.gcnArchName);
+    fprintf(stderr, "brotli_amd: device %d is %s, this build targets gfx950\n", device, prop.gcnArchName);
     return MIB_E_NO_DEVICE;
   }
   int16_t lut[704 * 4];
   build_cmd_lut(lut);
   HIP_OK(mib_decode_init_tables(lut));
-  g_inited = true;
+  HIP_OK(hipDeviceSynchronize());
+  g_dev_ready[device] = true;
   return 0;
+}
+
+int ensure_init() {
+  int dev;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    dev = g_device;
+  }
+  return ensure_device(dev);
 }
 
 // decodeWindowBits (engine.ts:91-124) on the first bits of a stream: sizes the ring scratch
@@ -137,11 +150,22 @@ extern "C" void mib_encode_ws_free(void *ws);
 namespace {
 
 mib_ctx *g_default_ctx = nullptr;
+// The host-buffer entry points (mib_encode / mib_decode / batches / BrotliEncoder) share the
+// default context's stream and scratch: one call at a time (recursive: a batch decode retries
+// a stream through mib_decode).
+std::recursive_mutex g_default_mu;
 
 mib_ctx *default_ctx() {
   if (ensure_init() != 0) return nullptr;
   std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_default_ctx) g_default_ctx = mib_ctx_new(g_device);
+  if (!g_default_ctx) {
+    g_default_ctx = new mib_ctx();
+    g_default_ctx->device = g_device;
+    if (hipStreamCreateWithFlags(&g_default_ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete g_default_ctx;
+      g_default_ctx = nullptr;
+    }
+  }
   return g_default_ctx;
 }
 
@@ -170,7 +194,7 @@ void mib_enc_opts_default(mib_enc_opts *o) {
 int mib_init(int device) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    if (g_inited && device != g_device) return MIB_E_INVALID_ARG;
+    if (g_default_ctx && device != g_device) return MIB_E_INVALID_ARG;   // the default context exists already
     g_device = device;
   }
   return ensure_init();
@@ -236,9 +260,10 @@ int64_t mib_decoded_size(const uint8_t *b, size_t n) {   // engine.ts:2155-2192 
 }
 
 mib_ctx *mib_ctx_new(int device) {
+  if (ensure_device(device) != 0) return nullptr;
   mib_ctx *c = new mib_ctx();
   c->device = device;
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return nullptr;
   }
@@ -260,6 +285,11 @@ void mib_ctx_set_profiling(mib_ctx *c, int on) { c->profiling = on != 0; }
 
 // internal (encode.hip)
 mib_ctx *mib_default_ctx(void) { return default_ctx(); }
+void mib_default_lock(int on) {
+  if (on) g_default_mu.lock();
+  else g_default_mu.unlock();
+}
+int mib_ctx_ready(mib_ctx *c) { return c ? ensure_device(c->device) : MIB_E_INVALID_ARG; }
 void *mib_ctx_stream_of(mib_ctx *c) { return (void *)c->stream; }
 int mib_ctx_device_of(mib_ctx *c) { return c->device; }
 void mib_ctx_clear_times(mib_ctx *c) { c->times.clear(); }
@@ -314,8 +344,7 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
 int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, size_t k, uint8_t *d_out,
                    const uint64_t *out_offsets, int64_t *out_sizes, int *status, void *stream) {
   if (!c || (k && (!d_in || !in_offsets || !d_out || !out_offsets))) return MIB_E_INVALID_ARG;
-  if (ensure_init() != 0) return MIB_E_NO_DEVICE;
-  hipSetDevice(c->device);
+  if (ensure_device(c->device) != 0) return MIB_E_NO_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   c->times.clear();
   std::vector<uint8_t> heads(2 * k + 2);
@@ -357,6 +386,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
   if (!out || (!in && n)) return MIB_E_INVALID_ARG;
   out->data = nullptr;
   out->size = 0;
+  std::lock_guard<std::recursive_mutex> use(g_default_mu);
   mib_ctx *c = default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
   hipSetDevice(c->device);
@@ -434,6 +464,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
 }
 
 int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
+  std::lock_guard<std::recursive_mutex> use(g_default_mu);
   mib_ctx *c = default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
   hipSetDevice(c->device);

@@ -140,6 +140,31 @@ def enwik_batch(count, length, seed0):
     return [enwik_text(length, seed0 + i) for i in range(count)]
 
 
+def _glyf_triplets(dx, dy, on_curve):
+    """WOFF2 §5.2 triplet encoding of point deltas, vectorised: (flag stream, glyph bytes)."""
+    x, y = dx.astype(np.int64), dy.astype(np.int64)
+    ax, ay = np.abs(x), np.abs(y)
+    sx, sy = (x >= 0).astype(np.int64), (y >= 0).astype(np.int64)
+    c0 = (x == 0) & (ay < 1280)
+    c1 = ~c0 & (y == 0) & (ax < 1280)
+    c2 = ~c0 & ~c1 & (ax <= 64) & (ay <= 64)
+    c3 = ~c0 & ~c1 & ~c2 & (ax <= 768) & (ay <= 768)
+    f = np.select([c0, c1, c2, c3],
+                  [((ay >> 8) << 1) + sy, 10 + ((ax >> 8) << 1) + sx,
+                   20 + ((ax - 1) & 0x30) + (((ay - 1) & 0x30) >> 2) + 2 * sx + sy,
+                   84 + 12 * (((ax - 1) >> 8) & 3) + ((((ay - 1) >> 8) & 3) << 2) + 2 * sx + sy],
+                  120 + 2 * sx + sy)
+    flags = ((f & 0x7F) | np.where(on_curve, 0, 0x80)).astype(np.uint8)
+    b = np.zeros((len(x), 3), dtype=np.int64)
+    b[:, 0] = np.select([c0, c1, c2, c3], [ay & 0xFF, ax & 0xFF, (((ax - 1) & 0xF) << 4) | ((ay - 1) & 0xF), (ax - 1) & 0xFF],
+                        (ax >> 4) & 0xFF)
+    b[:, 1] = np.where(c3, (ay - 1) & 0xFF, ((ax & 0xF) << 4) | ((ay >> 8) & 0xF))
+    b[:, 2] = ay & 0xFF
+    n = np.select([c0 | c1 | c2, c3], [1, 2], 3)
+    keep = np.arange(3)[None, :] < n[:, None]
+    return bytearray(flags.tobytes()), bytearray(b[keep].astype(np.uint8).tobytes())
+
+
 def glyf_stream(length, seed=1000):
     """WOFF2 §5.1 transformed-glyf-like stream: nContour (int16 BE per glyph), nPoints
     (255UInt16 per contour), flags (1 byte / point), triplet-coded glyph coordinates,
@@ -163,27 +188,7 @@ def glyf_stream(length, seed=1000):
     on_curve = rng.random(tot) < 0.6
     dx = np.rint(rng.normal(0, 40, tot)).astype(np.int64)
     dy = np.rint(rng.normal(0, 40, tot)).astype(np.int64)
-    flags = bytearray(tot)
-    glyph = bytearray()
-    for i in range(tot):
-        x, y = int(dx[i]), int(dy[i])
-        ax, ay = abs(x), abs(y)
-        if x == 0 and ay < 1280:
-            f = 0 + ((ay >> 8) << 1) + (1 if y >= 0 else 0)
-            glyph.append(ay & 0xFF)
-        elif y == 0 and ax < 1280:
-            f = 10 + ((ax >> 8) << 1) + (1 if x >= 0 else 0)
-            glyph.append(ax & 0xFF)
-        elif ax <= 64 and ay <= 64:
-            f = 20 + ((ax - 1) & 0x30) + (((ay - 1) & 0x30) >> 2) + (2 if x >= 0 else 0) + (1 if y >= 0 else 0)
-            glyph.append((((ax - 1) & 0xF) << 4) | ((ay - 1) & 0xF))
-        elif ax <= 768 and ay <= 768:
-            f = 84 + 12 * (((ax - 1) >> 8) & 3) + ((((ay - 1) >> 8) & 3) << 2) + (2 if x >= 0 else 0) + (1 if y >= 0 else 0)
-            glyph += bytes([(ax - 1) & 0xFF, (ay - 1) & 0xFF])
-        else:
-            f = 120 + (2 if x >= 0 else 0) + (1 if y >= 0 else 0)
-            glyph += bytes([(ax >> 4) & 0xFF, ((ax & 0xF) << 4) | ((ay >> 8) & 0xF), ay & 0xFF])
-        flags[i] = (f & 0x7F) | (0 if on_curve[i] else 0x80)
+    flags, glyph = _glyf_triplets(dx, dy, on_curve)
     # instruction lengths (255UInt16 per simple glyph) go to the glyph stream, bodies to instructions
     simple = int((ncont > 0).sum())
     ilen = rng.integers(0, 60, size=simple)

@@ -31,10 +31,13 @@ def gather_shards(local, lengths, dst=0, group=None):
     local:   1-D uint8 tensor holding this rank's streams back to back (on the backend's
              device: CUDA for nccl, CPU for gloo)
     lengths: list of this rank's stream lengths (sum <= local.numel())
-    Returns, on dst, a list over ranks of (packed uint8 tensor, [lengths]); None elsewhere.
+    dst:     the destination's rank WITHIN `group` (= the global rank when group is None)
+    Returns, on dst, a list over group ranks of (packed uint8 tensor, [lengths]); None elsewhere.
     """
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    # torch.distributed.gather takes a global rank for dst
+    gdst = dst if group is None else dist.get_global_rank(group, dst)
     dev = local.device
     nbytes = int(sum(lengths))
     meta = torch.tensor([nbytes, len(lengths)], dtype=torch.int64, device=dev)
@@ -52,9 +55,9 @@ def gather_shards(local, lengths, dst=0, group=None):
     if rank == dst:
         bufs = [torch.empty(max_bytes, dtype=torch.uint8, device=dev) for _ in range(world)]
         lbufs = [torch.empty(max_count, dtype=torch.int64, device=dev) for _ in range(world)]
-        dist.gather(send, bufs, dst=dst, group=group)
-        dist.gather(lens, lbufs, dst=dst, group=group)
+        dist.gather(send, bufs, dst=gdst, group=group)
+        dist.gather(lens, lbufs, dst=gdst, group=group)
         return [(bufs[r][:metas[r][0]], [int(x) for x in lbufs[r][:metas[r][1]].tolist()]) for r in range(world)]
-    dist.gather(send, None, dst=dst, group=group)
-    dist.gather(lens, None, dst=dst, group=group)
+    dist.gather(send, None, dst=gdst, group=group)
+    dist.gather(lens, None, dst=gdst, group=group)
     return None

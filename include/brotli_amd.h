@@ -12,7 +12,9 @@
  *   EncoderMode {GENERIC 0, TEXT 1, FONT 2}                src/encode/enc-constants.ts:56-60 -> MIB_MODE_*
  *
  * plus batch entry points (host or device-resident buffers) that shard independent buffers
- * over the GPU.  Every call is synchronous; handles are not thread-safe.
+ * over the GPU.  Every call is synchronous.  The host-buffer entry points
+ * share one default context and are serialised internally (safe from several threads); a
+ * mib_ctx / mib_encoder handle must not be used by two threads at once.
  * All compute runs on the GPU: there is no CPU fallback, a missing device is an error.
  *
  * Return codes: 0 = success; the reference decoder's own negative codes (-1..-30,

@@ -76,3 +76,20 @@ def test_encode_matches_ref_fixed(chunk):
 def test_peek_decoded_size():
     assert _oracle.peek_size(_oracle.encode(b'x' * 1000)) == 1000
     assert _oracle.peek_size(_oracle.encode(b'')) == 0
+
+
+def test_oracle_decoder_is_thread_safe():
+    """bench.py's cpu_baseline runs the oracle on many threads at once: concurrent decodes of
+    streams with different prefix codes must each give their own bytes."""
+    from concurrent.futures import ThreadPoolExecutor
+    pairs = []
+    for nm in sorted(os.listdir(os.path.join(G, 'vectors'))):
+        if nm.endswith('.compressed'):
+            with open(os.path.join(G, 'vectors', nm), 'rb') as f:
+                comp = f.read()
+            with open(os.path.join(G, 'vectors', nm[:-len('.compressed')]), 'rb') as f:
+                pairs.append((comp, f.read()))
+    work = pairs * 12
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(lambda p: _oracle.decode(p[0]) == p[1], work))
+    assert all(got)

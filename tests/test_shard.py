@@ -77,3 +77,35 @@ def test_shard_balance():
     parts = [shard.shard_indices(sizes, 8, r) for r in range(8)]
     assert sorted(sum(parts, [])) == list(range(1024))
     assert all(len(p) == 128 for p in parts)
+
+
+def _sub_worker(rank, world, port, out_q):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    group = dist.new_group([1, 2])   # a subgroup whose rank 0 is global rank 1
+    if rank in (1, 2):
+        payload = bytes([rank]) * (10 + rank)
+        packed = torch.tensor(list(payload), dtype=torch.uint8)
+        got = shard.gather_shards(packed, [len(payload)], dst=0, group=group)
+        if rank == 1:
+            out_q.put([(bytes(d.tolist()), lens) for d, lens in got])
+        else:
+            assert got is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_subgroup_gather_dst_is_group_rank():
+    """gather_shards(dst=0, group=g) delivers to g's rank 0 (global rank 1), not global rank 0."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sub_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert got == [(b'\x01' * 11, [11]), (b'\x02' * 12, [12])]
