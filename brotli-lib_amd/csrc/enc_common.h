@@ -270,31 +270,61 @@ __device__ __forceinline__ uint32_t switch_bits(const Codes &cd, int cat, const 
 }
 __device__ __forceinline__ bool switch_at(const Unit &u, int cat, uint32_t q) { return u.sw_count[cat] && q == u.first[cat]; }
 
-// Bits of command q of a segment: block switches, prefix code, extra bits, literals under
-// their contexts, distance (storeCommandExtra / storeSymbolWithContext / BlockEncoder,
-// metablock.ts:273-287,392-501,720-745).  lut = the context mode's 512-entry slice of the
-// RFC context lookup table; u = the command's block-split unit.
-__device__ __forceinline__ uint32_t command_bits(const Codes &cd, const Mb &mb, const uint8_t *lut, const Cmd &c,
-                                                 const uint8_t *lits, uint32_t p12, const Unit &u, uint32_t q) {
+// ---------------------------------------------------------------- command items
+// A command is coded as a sequence of ITEMS (storeCommandExtra / storeSymbolWithContext /
+// BlockEncoder, metablock.ts:273-287,392-501,720-745):
+//   item 0            command block switch, command prefix code, insert / copy extra bits,
+//                     literal block switch
+//   items 1 .. ins    one literal each, under its context (p1, p2 are the input bytes before it)
+//   item ins + 1      distance block switch, distance prefix code and extra bits (0 bits for
+//                     insert-only and implicit-last-distance commands)
+// Items are independent given the command, so literal-heavy segments (glyph data, long
+// inserts) spread over the lanes of a block instead of serialising on one lane per command.
+// `u` is the block-split unit of the command (by its insert position), q its index.
+__device__ __forceinline__ uint32_t item_count(const Cmd &c) { return c.ins + 2; }
+
+__device__ __forceinline__ uint32_t header_bits(const Codes &cd, const Cmd &c, const Unit &u, uint32_t q) {
   const int ic = ins_code(c.ins);
   const int cc = copy_code(c.copy ? c.copy : 2);
-  const uint8_t *lmap = mb.lit_cmap + u.type[0] * kLitCtx;
   uint32_t bits = cd.cd[u.type[1]][c.cmd_prefix] + kInsExtra[ic] + kCopyExtra[cc];
   if (switch_at(u, 1, q)) bits += switch_bits(cd, 1, u);
   if (switch_at(u, 0, q)) bits += switch_bits(cd, 0, u);
-  uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
-  for (uint32_t k = 0; k < c.ins; k++) {
-    const uint32_t lit = lits[k];
-    bits += cd.ld[lmap[lut[p1] | lut[256 + p2]]][lit];
-    p2 = p1;
-    p1 = lit;
-  }
-  if (c.copy && c.cmd_prefix >= 128) {
-    if (switch_at(u, 2, q)) bits += switch_bits(cd, 2, u);
-    bits += cd.dd[mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(c.copy)]][c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
-  }
   return bits;
 }
+__device__ __forceinline__ int literal_tree(const Mb &mb, const uint8_t *lut, const Unit &u, uint32_t p12) {
+  return mb.lit_cmap[u.type[0] * kLitCtx + (lut[p12 & 0xFF] | lut[256 + (p12 >> 8)])];
+}
+__device__ __forceinline__ uint32_t dist_bits(const Codes &cd, const Mb &mb, const Cmd &c, const Unit &u, uint32_t q) {
+  if (!c.copy || c.cmd_prefix < 128) return 0;
+  uint32_t bits = cd.dd[mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(c.copy)]][c.dist_prefix & 0x3FF] + (c.dist_prefix >> 10);
+  if (switch_at(u, 2, q)) bits += switch_bits(cd, 2, u);
+  return bits;
+}
+// bits of item k of command c (insert at stream position p)
+__device__ __forceinline__ uint32_t item_bits(const Codes &cd, const Mb &mb, const uint8_t *lut, const Job &jb,
+                                              const Cmd &c, uint32_t p, const Unit &u, uint32_t q, uint32_t k) {
+  if (k == 0) return header_bits(cd, c, u, q);
+  if (k > c.ins) return dist_bits(cd, mb, c, u, q);
+  const uint32_t lp = p + k - 1;
+  return cd.ld[literal_tree(mb, lut, u, prev2(jb, lp))][jb.data[lp]];
+}
+
+// Load-balanced expansion of a batch of at most B commands into their items: off[j] is the
+// first item of command j (exclusive scan of the counts), off[nb] the batch's total.
+template <int B>
+struct ItemMap {
+  uint32_t off[B + 1];
+  // the command owning item i (i < off[nb]): off[j] <= i < off[j + 1]
+  __device__ __forceinline__ uint32_t find(uint32_t i, uint32_t nb) const {
+    uint32_t lo = 0, hi = nb;
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    return lo;
+  }
+};
 
 // ---------------------------------------------------------------- kernel launchers (host)
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys,

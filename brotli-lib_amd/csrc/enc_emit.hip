@@ -106,50 +106,52 @@ __device__ __forceinline__ void put_switch(W &wr, const Codes &cd, int cat, cons
   wr.put((int)kBlkBits[bc], u.sw_count[cat] - kBlkOff[bc]);
 }
 
-// command q of its segment, with the block switches its unit places on it (same bits as
-// command_bits)
+// item k of command q (see item_bits in enc_common.h: same bits, in stream order)
 template <class W>
-__device__ __forceinline__ void write_command(W &wr, const Codes &cd, const Mb &mb, const uint8_t *lut, const Cmd &k,
-                                              const uint8_t *lits, uint32_t p12, const Unit &u, uint32_t q) {
-  if (switch_at(u, 1, q)) put_switch(wr, cd, 1, u);
-  const int ct = u.type[1];
-  wr.put(cd.cd[ct][k.cmd_prefix], cd.cc[ct][k.cmd_prefix]);
-  const int ic = ins_code(k.ins);
-  wr.put((int)kInsExtra[ic], k.ins - kInsBase[ic]);
-  const uint32_t clen = k.copy ? k.copy : 2;
-  const int cc = copy_code(clen);
-  wr.put((int)kCopyExtra[cc], clen - kCopyBase[cc]);
-  if (switch_at(u, 0, q)) put_switch(wr, cd, 0, u);
-  const uint8_t *lmap = mb.lit_cmap + u.type[0] * kLitCtx;
-  uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
-  for (uint32_t t = 0; t < k.ins; t++) {
-    const uint32_t lit = lits[t];
-    const int tree = lmap[lut[p1] | lut[256 + p2]];
+__device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb, const uint8_t *lut, const Job &jb,
+                                           const Cmd &c, uint32_t p, const Unit &u, uint32_t q, uint32_t k) {
+  if (k == 0) {
+    if (switch_at(u, 1, q)) put_switch(wr, cd, 1, u);
+    const int ct = u.type[1];
+    wr.put(cd.cd[ct][c.cmd_prefix], cd.cc[ct][c.cmd_prefix]);
+    const int ic = ins_code(c.ins);
+    wr.put((int)kInsExtra[ic], c.ins - kInsBase[ic]);
+    const uint32_t clen = c.copy ? c.copy : 2;
+    const int cc = copy_code(clen);
+    wr.put((int)kCopyExtra[cc], clen - kCopyBase[cc]);
+    if (switch_at(u, 0, q)) put_switch(wr, cd, 0, u);
+  } else if (k <= c.ins) {
+    const uint32_t lp = p + k - 1;
+    const uint32_t lit = jb.data[lp];
+    const int tree = literal_tree(mb, lut, u, prev2(jb, lp));
     wr.put(cd.ld[tree][lit], cd.lc[tree][lit]);
-    p2 = p1;
-    p1 = lit;
-  }
-  if (k.copy && k.cmd_prefix >= 128) {
+  } else if (c.copy && c.cmd_prefix >= 128) {
     if (switch_at(u, 2, q)) put_switch(wr, cd, 2, u);
-    const uint32_t dcode = k.dist_prefix & 0x3FF;
-    const int tree = mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(k.copy)];
+    const uint32_t dcode = c.dist_prefix & 0x3FF;
+    const int tree = mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(c.copy)];
     wr.put(cd.dd[tree][dcode], cd.dcd[tree][dcode]);
-    wr.put(k.dist_prefix >> 10, k.dist_extra);
+    wr.put(c.dist_prefix >> 10, c.dist_extra);
   }
 }
 
-// Block per segment: 256 commands at a time get their bit offsets from a block scan and are
-// written into an LDS window, which is then stored as whole words (the chunk's first and
-// last word are ORed: neighbours share them).  A command that does not fit the window (an
-// insert of tens of thousands of literals) is ORed straight into global memory.
+// Block per segment.  The segment's commands are taken kBlock at a time and expanded into
+// their items (header, literals, distance); kEmitItems items per lane per tile get their bit
+// offsets from a block scan and are ORed into an LDS window, which is then stored as whole
+// words (the tile's first and last word are ORed: neighbours share them).  A tile is at most
+// kBlock * kEmitItems items of <= 180 bits, so it always fits the window.
 constexpr int kWinWords = 8192;   // 32 KiB = 262144 bits
+constexpr int kEmitItems = 4;
+static_assert(kBlock * kEmitItems * 180 <= kWinWords * 32 - 64, "emit tile must fit the LDS window");
 __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                       const uint32_t *cmd_pos, const Codes *codes, const Unit *units,
                                                       uint8_t *out) {
   typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t win[kWinWords];
-  __shared__ uint32_t sh_fit_end;
+  __shared__ ItemMap<kBlock> map;
+  __shared__ Cmd sh_c[kBlock];
+  __shared__ uint32_t sh_p[kBlock];
+  __shared__ Unit sh_u[kSubPerSeg];
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
@@ -161,53 +163,67 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
-  const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
+  if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
   uint64_t bitpos = sg.bit_off;
   for (uint32_t base = 0; base < n; base += kBlock) {
-    const uint32_t q = base + t;
-    Cmd k;
-    Unit u;
-    uint32_t bits = 0;
-    if (q < n) {
-      k = c[q];
-      u = un[unit_of(sg, cp[q])];
-      bits = command_bits(cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]), u, q);
+    const uint32_t nb = min((uint32_t)kBlock, n - base);
+    uint32_t cnt = 0;
+    if ((uint32_t)t < nb) {
+      sh_c[t] = c[base + t];
+      sh_p[t] = cp[base + t];
+      cnt = item_count(sh_c[t]);
     }
-    uint32_t off, total;
-    Scan(scan_tmp).ExclusiveSum(bits, off, total);
-    const uint32_t rel0 = (uint32_t)(bitpos & 31);
-    const uint64_t w0 = bitpos >> 5;
-    const uint32_t need = (uint32_t)min((uint64_t)kWinWords, ((uint64_t)rel0 + total + 31) / 32);
-    for (uint32_t i = t; i < need; i += kBlock) win[i] = 0;
-    if (t == 0) sh_fit_end = rel0;
+    uint32_t off, nitems;
+    Scan(scan_tmp).ExclusiveSum(cnt, off, nitems);
+    map.off[t] = off;
+    if (t == 0) map.off[nb] = nitems;   // (nb <= kBlock; a later slot j > nb is never read)
     __syncthreads();
-    const bool fits = (uint64_t)rel0 + off + bits <= (uint64_t)kWinWords * 32;
-    if (q < n && bits) {
-      if (fits) {
+    for (uint32_t i0 = 0; i0 < nitems; i0 += kBlock * kEmitItems) {
+      uint32_t bits[kEmitItems], qj[kEmitItems], kk[kEmitItems];
+      const uint32_t first = i0 + (uint32_t)t * kEmitItems;
+      uint32_t j = first < nitems ? map.find(first, nb) : 0;
+      for (int e = 0; e < kEmitItems; e++) {
+        const uint32_t i = first + e;
+        bits[e] = 0;
+        qj[e] = j;
+        kk[e] = 0;
+        if (i < nitems) {
+          while (map.off[j + 1] <= i) j++;
+          qj[e] = j;
+          kk[e] = i - map.off[j];
+          const Cmd &k = sh_c[j];
+          const uint32_t p = sh_p[j];
+          bits[e] = item_bits(cd, mb, lut, jb, k, p, sh_u[unit_of(sg, p)], base + j, kk[e]);
+        }
+      }
+      uint32_t boff[kEmitItems], total;
+      Scan(scan_tmp).ExclusiveSum(bits, boff, total);
+      const uint32_t rel0 = (uint32_t)(bitpos & 31);
+      const uint64_t w0 = bitpos >> 5;
+      const uint32_t nw = (rel0 + total + 31) / 32;
+      for (uint32_t w = t; w < nw; w += kBlock) win[w] = 0;
+      __syncthreads();
+      for (int e = 0; e < kEmitItems; e++) {
+        if (!bits[e]) continue;
+        const uint32_t jj = qj[e];
+        const Cmd &k = sh_c[jj];
+        const uint32_t p = sh_p[jj];
         OrW<false> wr;
-        wr.init(win, rel0 + off);
-        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]), u, q);
-        wr.finish();
-        atomicMax(&sh_fit_end, rel0 + off + bits);
-      } else {
-        OrW<true> wr;
-        wr.init(words, bitpos + off);
-        write_command(wr, cd, mb, lut, k, jb.data + cp[q], prev2(jb, cp[q]), u, q);
+        wr.init(win, rel0 + boff[e]);
+        write_item(wr, cd, mb, lut, jb, k, p, sh_u[unit_of(sg, p)], base + jj, kk[e]);
         wr.finish();
       }
-    }
-    __syncthreads();
-    const uint32_t fit_end = sh_fit_end;
-    const uint32_t nw = (fit_end + 31) / 32;
-    for (uint32_t i = t; i < nw; i += kBlock) {
-      if (i == 0 || i == nw - 1) {
-        if (win[i]) atomicOr(words + w0 + i, win[i]);
-      } else {
-        words[w0 + i] = win[i];
+      __syncthreads();
+      for (uint32_t w = t; w < nw; w += kBlock) {
+        if (w == 0 || w == nw - 1) {
+          if (win[w]) atomicOr(words + w0 + w, win[w]);
+        } else {
+          words[w0 + w] = win[w];
+        }
       }
+      bitpos += total;
+      __syncthreads();
     }
-    bitpos += total;
-    __syncthreads();
   }
 }
 

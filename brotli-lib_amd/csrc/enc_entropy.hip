@@ -92,6 +92,9 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
   __shared__ uint32_t sh_h[kSubPerSeg * kSubHist];
   __shared__ uint32_t sh_n[kSubPerSeg][3], sh_first[kSubPerSeg][3];
   __shared__ uint32_t sh_run;
+  __shared__ ItemMap<kBlock> map;
+  __shared__ uint32_t sh_pos[kBlock];
+  __shared__ uint8_t sh_unit[kBlock];
   const Seg sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
@@ -158,7 +161,19 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
       }
       out[q] = c;
       outp[q] = pos;
-      for (uint32_t k = 0; k < ins; k++) atomicAdd(&hu[jb.data[pos + k]], 1u);
+    }
+    // the literals of the batch, spread over the lanes (items = inserts, see ItemMap)
+    sh_pos[t] = pos;
+    sh_unit[t] = (uint8_t)unit_of(sg, pos);
+    uint32_t loff, nlits;
+    Scan(scan_tmp).ExclusiveSum(q < n ? ins : 0u, loff, nlits);
+    const uint32_t nb = min((uint32_t)kBlock, n - base);
+    map.off[t] = loff;
+    if (t == 0) map.off[nb] = nlits;
+    __syncthreads();
+    for (uint32_t i = t; i < nlits; i += kBlock) {
+      const uint32_t j = map.find(i, nb);
+      atomicAdd(&sh_h[sh_unit[j] * kSubHist + jb.data[sh_pos[j] + i - map.off[j]]], 1u);
     }
     __syncthreads();
   }
@@ -187,8 +202,12 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
 __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Unit *units, uint32_t *hl,
                                                        uint32_t *hc, uint32_t *hd) {
+  typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
+  __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
   __shared__ uint8_t ut[kSubPerSeg][3];
+  __shared__ ItemMap<kBlock> map;
+  __shared__ uint32_t sh_pos[kBlock];
   uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
@@ -223,20 +242,26 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
     if (!(present >> ty & 1)) continue;
     for (int i = t; i < kLitCtx * 256; i += kBlock) sh_l[i] = 0;
     __syncthreads();
-    for (uint32_t q = t; q < n; q += kBlock) {
-      const uint32_t p = cp[q];
-      if (ut[unit_of(sg, p)][0] != ty) continue;
-      const Cmd k = c[q];
-      const uint32_t p12 = prev2(jb, p);
-      uint32_t p1 = p12 & 0xFF, p2 = p12 >> 8;
-      for (uint32_t x = 0; x < k.ins; x++) {
-        const uint32_t lit = jb.data[p + x];
-        atomicAdd(&sh_l[(lut[p1] | lut[256 + p2]) * 256 + lit], 1u);
-        p2 = p1;
-        p1 = lit;
+    for (uint32_t base = 0; base < n; base += kBlock) {   // the literals of this type, spread over the lanes
+      const uint32_t q = base + t, nb = min((uint32_t)kBlock, n - base);
+      uint32_t cnt = 0;
+      if (q < n) {
+        sh_pos[t] = cp[q];
+        if (ut[unit_of(sg, cp[q])][0] == ty) cnt = c[q].ins;
       }
+      uint32_t off, nlits;
+      Scan(scan_tmp).ExclusiveSum(cnt, off, nlits);
+      map.off[t] = off;
+      if (t == 0) map.off[nb] = nlits;
+      __syncthreads();
+      for (uint32_t i = t; i < nlits; i += kBlock) {
+        const uint32_t j = map.find(i, nb);
+        const uint32_t lp = sh_pos[j] + i - map.off[j];
+        const uint32_t p12 = prev2(jb, lp);
+        atomicAdd(&sh_l[(lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp]], 1u);
+      }
+      __syncthreads();
     }
-    __syncthreads();
     uint32_t *dst = hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256;
     for (int i = t; i < kLitCtx * 256; i += kBlock)
       if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
@@ -1227,25 +1252,50 @@ __global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hd
 }
 
 // ---------------------------------------------------------------- sizes: block per segment
+// The segment's bit size: the sum of item_bits over its commands' items (the same
+// load-balanced expansion as emit_kernel, so literal-heavy segments use every lane).
 __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
+  typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   typedef hipcub::BlockReduce<unsigned long long, kBlock> Reduce;
-  __shared__ typename Reduce::TempStorage tmp;
+  __shared__ typename Scan::TempStorage scan_tmp;
+  __shared__ typename Reduce::TempStorage red_tmp;
+  __shared__ ItemMap<kBlock> map;
+  __shared__ Cmd sh_c[kBlock];
+  __shared__ uint32_t sh_p[kBlock];
+  __shared__ Unit sh_u[kSubPerSeg];
   Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
+  const int t = threadIdx.x;
   const Mb &mb = mbs[sg.mb];
   const Codes &cd = codes[sg.mb];
   const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
-  const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
+  if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
   unsigned long long bits = 0;
-  for (uint32_t q = threadIdx.x; q < n; q += kBlock) {
-    const uint32_t p = cmd_pos[sg.cmd_off + q];
-    bits += command_bits(cd, mb, lut, cmds[sg.cmd_off + q], jb.data + p, prev2(jb, p), un[unit_of(sg, p)], q);
+  for (uint32_t base = 0; base < n; base += kBlock) {
+    const uint32_t nb = min((uint32_t)kBlock, n - base);
+    uint32_t cnt = 0;
+    if ((uint32_t)t < nb) {
+      sh_c[t] = cmds[sg.cmd_off + base + t];
+      sh_p[t] = cmd_pos[sg.cmd_off + base + t];
+      cnt = item_count(sh_c[t]);
+    }
+    uint32_t off, nitems;
+    Scan(scan_tmp).ExclusiveSum(cnt, off, nitems);
+    map.off[t] = off;
+    if (t == 0) map.off[nb] = nitems;
+    __syncthreads();
+    for (uint32_t i = t; i < nitems; i += kBlock) {
+      const uint32_t j = map.find(i, nb);
+      const uint32_t p = sh_p[j];
+      bits += item_bits(cd, mb, lut, jb, sh_c[j], p, sh_u[unit_of(sg, p)], base + j, i - map.off[j]);
+    }
+    __syncthreads();
   }
-  unsigned long long total = Reduce(tmp).Sum(bits);
-  if (threadIdx.x == 0) sg.bits = total;
+  unsigned long long total = Reduce(red_tmp).Sum(bits);
+  if (t == 0) sg.bits = total;
 }
 
 // ---------------------------------------------------------------- offsets: lane per stream
