@@ -16,14 +16,16 @@ namespace enc {
 
 constexpr uint32_t kSegBits = 16;
 constexpr uint32_t kSeg = 1u << kSegBits;     // 64 KiB parse segments
-constexpr int kMaxMatches = 6;                // staircase entries kept per position
-constexpr int kMatchRec = 8;                  // u32 per position record: 6 matches, count, 0 (one 32 B sector)
+constexpr int kMaxMatches = 4;                // staircase entries kept per position (the longest ones)
+constexpr int kMatchRec = 4;                  // u32 per position record: 4 matches, 0 = none (16 B)
 constexpr uint32_t kMatchLenSat = 255;        // a match is (length:8 | distance:24); 255 = "255 or more"
 constexpr int kLongCopy = 200;                // copies longer than this are taken outright (the
                                               // reference's MAX_ZOPFLI_LEN is 325 at q11, 150 at q10,
                                               // enc-constants.ts:32-33)
 constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
-constexpr uint32_t kInvalidKey = 0xFFFFFFFFu;
+constexpr uint32_t kHashBits = 17;            // hashBytes4 (match.ts:162-172)
+constexpr uint32_t kInvalidKey = 1u << kHashBits;   // (within a stream group) positions without 4 bytes
+constexpr int kGroupKeyBits = 6;              // sort key = stream group (<= 64 groups) << 18 | hash or invalid
 constexpr int kHdrBytes = 2048;               // metablock header: block-switch codes, context maps (not the trees)
 constexpr int kTreeBytes = 1024;              // one serialised prefix code
 constexpr int kLitCtx = 64;                   // literal contexts (RFC 7932 section 7.1)
@@ -327,10 +329,10 @@ struct ItemMap {
 };
 
 // ---------------------------------------------------------------- kernel launchers (host)
-void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys,
+void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals);
-void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
-                         int depth, uint32_t *matches);
+void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
+                         const uint32_t *svals, uint32_t total, int depth, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                const uint32_t *matches, uint64_t *choice);

@@ -8,14 +8,20 @@ namespace mib {
 namespace enc {
 
 // ---------------------------------------------------------------- 1. keys
-// Every global position (including the padding after each stream) gets a key; padding and
-// the last 3 bytes of a stream get the invalid key, which sorts after every real bucket.
-__global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys, uint32_t *vals) {
+// Every global position (including the padding after each stream) gets the key
+// (stream group << 18 | hash4), the invalid hash 2^17 for padding and a stream's last 3
+// bytes.  A stream group is 2^gshift consecutive streams (at most 64 groups a call, so keys
+// have at most 24 bits: three radix passes).  The sort is stable and global positions
+// ascend stream by stream, so within a bucket the entries of one stream are contiguous and
+// in position order -- a candidate walk stops where the stream changes -- and the entries a
+// wave of find_matches tiles touches stay within one group's streams (cache locality).
+__global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
+                                 uint32_t *vals) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
     uint32_t j = pos_job[g >> kSegBits];
     const Job &jb = jobs[j];
     uint32_t p = g - jb.pos_base;
-    keys[g] = (p + 4 <= jb.n && !jb.uncompressed) ? ((j << 17) | hash4(jb.data + p)) : kInvalidKey;
+    keys[g] = ((j >> gshift) << (kHashBits + 1)) | ((p + 4 <= jb.n && !jb.uncompressed) ? hash4(jb.data + p) : kInvalidKey);
     vals[g] = g;
   }
 }
@@ -44,7 +50,7 @@ __device__ __forceinline__ uint64_t load_prefix8(const uint8_t *p, uint32_t avai
   return v;
 }
 
-__global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *sorted_keys,
+__global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
                                                              const uint32_t *sorted_vals, uint32_t total, int depth,
                                                              uint32_t *matches) {
   __shared__ uint32_t skey[kTile + kBack];
@@ -58,8 +64,8 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     if (r >= 0 && r < (int64_t)total) {
       key = sorted_keys[r];
       g = sorted_vals[r];
-      if (key != kInvalidKey) {
-        const Job &jb = jobs[key >> 17];
+      if ((key & kInvalidKey) == 0) {
+        const Job &jb = jobs[pos_job[g >> kSegBits]];
         uint32_t p = g - jb.pos_base;
         pre = load_prefix8(jb.data + p, jb.n - p);
       }
@@ -74,8 +80,8 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
   const int me = kBack + threadIdx.x;
   const uint32_t key = skey[me], g = spos[me];
   int cnt = 0;
-  if (key != kInvalidKey) {
-    const Job &jb = jobs[key >> 17];
+  if ((key & kInvalidKey) == 0) {
+    const Job &jb = jobs[pos_job[g >> kSegBits]];
     const uint32_t p = g - jb.pos_base;
     const uint32_t max_dist = (1u << jb.lgwin) - 16;
     const uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
@@ -83,11 +89,11 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     const uint8_t *cur = jb.data + p;
     const uint64_t mine = spre[me];
     uint32_t best = 3;
-    uint32_t local[kMaxMatches];
+    uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
     const int dmax = min(depth, kBack);
     for (int t = 1; t <= dmax; t++) {
       const int e = me - t;
-      if (skey[e] != key) break;
+      if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
       const uint32_t d = g - spos[e];
       if (d > max_dist || best >= limit) break;
       const uint64_t x = mine ^ spre[e];
@@ -114,13 +120,11 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
         if (len >= limit || len >= kMatchLenSat) break;   // the parse measures a long copy itself
       }
     }
-    uint4 *rec = reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec);
-    rec[0] = make_uint4(local[0], local[1], local[2], local[3]);
-    rec[1] = make_uint4(local[4], local[5], (uint32_t)cnt, 0u);
+    // a match word is never 0 (length >= 4): the unused tail entries mark the count
+    *reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec) = make_uint4(local[0], local[1], local[2], local[3]);
     return;
   }
-  uint4 *rec = reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec);
-  rec[1] = make_uint4(0u, 0u, 0u, 0u);   // no candidates: count 0
+  *reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec) = make_uint4(0u, 0u, 0u, 0u);   // no candidates
 }
 
 // ---------------------------------------------------------------- literal cost model per stream
@@ -137,15 +141,15 @@ __global__ void lit_histo_kernel(const Job *jobs, const Seg *segs, uint32_t *lit
 }
 
 
-void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *keys,
+void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals) {
   const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total + 255) / 256);
-  hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, keys, vals);
+  hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, keys, vals);
 }
-void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *skeys, const uint32_t *svals, uint32_t total,
-                         int depth, uint32_t *matches) {
-  hipLaunchKernelGGL(find_matches_kernel, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, skeys, svals, total,
-                     depth, matches);
+void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
+                         const uint32_t *svals, uint32_t total, int depth, uint32_t *matches) {
+  hipLaunchKernelGGL(find_matches_kernel, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, pos_job, skeys, svals,
+                     total, depth, matches);
 }
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h) {
   hipLaunchKernelGGL(lit_histo_kernel, dim3(nsegs), dim3(256), 0, st, jobs, segs, lit_h);

@@ -77,10 +77,9 @@ struct Staged {   // one position's parse inputs (lane j of a batch = position i
 };
 __device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches, const uint8_t *data, uint32_t g, uint32_t p) {
   st.lit = data[p];
-  const uint4 *rec = reinterpret_cast<const uint4 *>(matches + (uint64_t)g * kMatchRec);
-  const uint4 a = rec[0], b = rec[1];   // entries past the count are ignored
-  st.m[0] = a.x; st.m[1] = a.y; st.m[2] = a.z; st.m[3] = a.w; st.m[4] = b.x; st.m[5] = b.y;
-  st.nm = b.z;
+  const uint4 a = *reinterpret_cast<const uint4 *>(matches + (uint64_t)g * kMatchRec);   // 0 = no entry
+  st.m[0] = a.x; st.m[1] = a.y; st.m[2] = a.z; st.m[3] = a.w;
+  st.nm = (a.x != 0u) + (a.y != 0u) + (a.z != 0u) + (a.w != 0u);
 }
 __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (distance << 32) | length, 0 = literal
   const uint32_t cl = m & 0xFFFF;

@@ -9,8 +9,9 @@
 // symbols -- restructured for the GPU (kernels in enc_match / enc_parse / enc_entropy /
 // enc_emit.hip):
 //
-//   hash_keys + radix sort   every position of every stream gets key (stream << 17 | hash4);
-//                            a stable device radix sort lays each bucket out as a flat chain
+//   hash_keys + radix sort   every position of every stream gets key (stream group | hash4),
+//                            <= 24 bits; a stable device radix sort lays each bucket out as
+//                            flat chains, one per stream, positions ascending
 //   find_matches             thread per sorted entry, LDS tile of the chain: the staircase of
 //                            (distance, length) matches, findAllMatches-style
 //   dp                       wave per 64 KiB segment: shortest path, 64 lanes relax the
@@ -203,9 +204,14 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   const int nsegs = (int)segs.size(), nmbs = (int)mbs.size();
   const size_t nm1 = std::max<size_t>(1, mbs.size()), ns1 = std::max<size_t>(1, segs.size());
 
+  const uint64_t last_job = k ? k - 1 : 0;
+  int gshift = 0;   // stream groups of the sort key: at most 2^kGroupKeyBits of them
+  while ((last_job >> gshift) >= (1u << kGroupKeyBits)) gshift++;
+  int key_bits = kHashBits + 1;
+  while (key_bits < (int)kHashBits + 1 + kGroupKeyBits && ((last_job >> gshift) >> (key_bits - kHashBits - 1)) != 0) key_bits++;
   size_t sort_tmp = 0;
   CK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                        (uint32_t *)nullptr, (int)total, 0, 32, st));
+                                        (uint32_t *)nullptr, (int)total, 0, key_bits, st));
   size_t need = 64 * 256;
   need += 4 * (size_t)total * 4 + sort_tmp;
   need += (size_t)total * kMatchRec * 4;
@@ -269,13 +275,13 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
     const int depth = depth_for_quality(prm.quality);
     tm.start("hash_keys");
-    launch_hash_keys(st, d_jobs, d_seg_job, total, keys, vals);
+    launch_hash_keys(st, d_jobs, d_seg_job, total, gshift, keys, vals);
     tm.stop();
     tm.start("radix_sort");
-    CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, 32, st));
+    CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, key_bits, st));
     tm.stop();
     tm.start("find_matches");
-    launch_find_matches(st, d_jobs, skeys, svals, total, depth, matches);
+    launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, matches);
     tm.stop();
     tm.start("lit_histo");
     launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
@@ -344,7 +350,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
 // no small tail group runs a whole parse at low occupancy -- below the 2^31 position limit
 // of the 32-bit position indices.
 constexpr uint64_t kWsBytesPerPosition = 80;
-constexpr size_t kGroupStreams = 16384;   // job index must fit the 15-bit key field
+constexpr size_t kGroupStreams = 65536;   // bounds the per-call descriptor arrays
 
 uint64_t group_position_limit(mib_ctx *ctx) {
   size_t free_b = 0, total_b = 0;
