@@ -29,25 +29,35 @@ __global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint3
 // One thread per SORTED entry: a bucket is a run of equal keys with positions ascending, so
 // the candidates of entry r are entries r-1, r-2, ... (most recent first) -- the
 // reference's hash chain / tree candidates (hash-binary-tree.ts:156-227), depth by
-// quality.  A 256-entry tile plus the 64 entries before it is staged in LDS with the 8
-// bytes following each position, so most candidates are rejected or measured without
-// touching HBM; only matches of 8+ bytes extend through global memory.  The staircase of
-// strictly increasing lengths (shortest distance for each length) is kept, longest last.
+// quality.  A 256-entry tile plus the 64 entries before it is staged in LDS with the 32
+// bytes following each position, so candidates are rejected or measured without touching
+// HBM unless a match reaches 32 bytes; only such matches extend through global memory.  The
+// staircase of strictly increasing lengths (shortest distance for each length) is kept,
+// longest last.
 constexpr int kTile = 256;
 constexpr int kBack = 64;
+constexpr int kPreW = 4;   // staged prefix: 4 x 8 bytes
 
-__device__ __forceinline__ uint64_t load_prefix8(const uint8_t *p, uint32_t avail) {
-  if (avail >= 12) {   // three aligned words (all inside the stream) and two funnel shifts
+// 32 bytes at p as four little-endian 64-bit words (zero past avail)
+__device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, uint64_t *o) {
+  if (avail >= 36) {   // nine aligned words (all inside the stream) and funnel shifts
     const uintptr_t a = (uintptr_t)p;
     const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-    const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
-    return ((uint64_t)hi << 32) | lo;
+    uint32_t v[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) v[i] = w[i];
+#pragma unroll
+    for (int i = 0; i < kPreW; i++) {
+      const uint32_t lo = __builtin_amdgcn_alignbyte(v[2 * i + 1], v[2 * i], sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(v[2 * i + 2], v[2 * i + 1], sh);
+      o[i] = ((uint64_t)hi << 32) | lo;
+    }
+    return;
   }
-  uint64_t v = 0;
-  for (uint32_t i = 0; i < avail; i++) v |= (uint64_t)p[i] << (8 * i);
-  return v;
+#pragma unroll
+  for (int i = 0; i < kPreW; i++) o[i] = 0;
+  for (uint32_t i = 0; i < avail && i < 8 * kPreW; i++) o[i >> 3] |= (uint64_t)p[i] << (8 * (i & 7));
 }
 
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
@@ -55,24 +65,25 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
                                                              uint32_t *matches) {
   __shared__ uint32_t skey[kTile + kBack];
   __shared__ uint32_t spos[kTile + kBack];
-  __shared__ uint64_t spre[kTile + kBack];
+  __shared__ uint64_t spre[kPreW][kTile + kBack];
   const uint32_t r0 = blockIdx.x * kTile;
   for (int t = threadIdx.x; t < kTile + kBack; t += kTile) {
     int64_t r = (int64_t)r0 - kBack + t;
     uint32_t key = 0xFFFFFFFEu, g = 0;
-    uint64_t pre = 0;
+    uint64_t pre[kPreW] = {0, 0, 0, 0};
     if (r >= 0 && r < (int64_t)total) {
       key = sorted_keys[r];
       g = sorted_vals[r];
       if ((key & kInvalidKey) == 0) {
         const Job &jb = jobs[pos_job[g >> kSegBits]];
         uint32_t p = g - jb.pos_base;
-        pre = load_prefix8(jb.data + p, jb.n - p);
+        load_prefix32(jb.data + p, jb.n - p, pre);
       }
     }
     skey[t] = key;
     spos[t] = g;
-    spre[t] = pre;
+#pragma unroll
+    for (int i = 0; i < kPreW; i++) spre[i][t] = pre[i];
   }
   __syncthreads();
   const uint32_t r = r0 + threadIdx.x;
@@ -87,7 +98,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     const uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
     const uint32_t limit = seg_end - p;   // copies never cross a parse segment
     const uint8_t *cur = jb.data + p;
-    const uint64_t mine = spre[me];
+    const uint64_t mine0 = spre[0][me];
     uint32_t best = 3;
     uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
     const int dmax = min(depth, kBack);
@@ -96,20 +107,35 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
       const uint32_t d = g - spos[e];
       if (d > max_dist || best >= limit) break;
-      const uint64_t x = mine ^ spre[e];
+      const uint64_t x0 = mine0 ^ spre[0][e];
       uint32_t len;
-      if (x) {
-        len = (uint32_t)(__ffsll((unsigned long long)x) - 1) >> 3;
+      if (x0) {
+        len = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;
         if (len <= best) continue;
-        len = min(len, limit);
       } else {
-        const uint8_t *cand = cur - d;
-        if (best >= 8 && cur[best] != cand[best]) continue;
-        // measured up to the saturation length: the parse measures longer copies itself
-        const uint32_t lim = min(limit, kMatchLenSat);
-        len = 8 + match_len(cur + 8, cand + 8, lim > 8 ? lim - 8 : 0);
-        len = min(len, limit);
+        // a candidate can only beat `best` if it matches byte `best` too
+        if (best < 8 * kPreW) {
+          const uint32_t sh = 8 * (best & 7);
+          if (((spre[best >> 3][me] ^ spre[best >> 3][e]) >> sh) & 0xFF) continue;
+        } else if (cur[best] != (cur - d)[best]) {
+          continue;
+        }
+        len = 8 * kPreW;
+#pragma unroll
+        for (int w = 1; w < kPreW; w++) {
+          const uint64_t x = spre[w][me] ^ spre[w][e];
+          if (x) {
+            len = 8 * w + ((uint32_t)(__ffsll((unsigned long long)x) - 1) >> 3);
+            break;
+          }
+        }
+        if (len == 8 * kPreW) {
+          // measured up to the saturation length: the parse measures longer copies itself
+          const uint32_t lim = min(limit, kMatchLenSat);
+          if (lim > len) len += match_len(cur + len, (cur - d) + len, lim - len);
+        }
       }
+      len = min(len, limit);
       if (len > best) {
         best = len;
         if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
