@@ -71,7 +71,7 @@ struct Lds {
   int32_t ctx_tree_base[64];
   uint8_t ctx_lut[512];        // the current literal context mode's slice of the RFC lookup table
   uint8_t mtf[256];
-  uint16_t ctx_root[2048];     // (p1 << 3 | lut1[p2]) -> root of the literal tree (16-bit tables)
+  uint16_t ctx_root[2048];     // (lut1[p2] << 8 | p1) -> root of the literal tree (16-bit tables)
 };
 
 struct Dec {
@@ -519,7 +519,7 @@ __device__ __noinline__ void build_ctx_tree_base(DecS &s) {
     // lut0[p1] | lut1[p2] with lut1 < 8 in every mode: one (p1, lut1[p2]) -> root table
     const int root = s.tab_lds[tree];   // the literal group starts at 0
     wave_sync();
-    for (int k = LANE; k < 2048; k += 64) s.l->ctx_root[k] = (uint16_t)__shfl(root, s.l->ctx_lut[k >> 3] | (k & 7));
+    for (int k = LANE; k < 2048; k += 64) s.l->ctx_root[k] = (uint16_t)__shfl(root, s.l->ctx_lut[k & 255] | (k >> 8));
   } else {
     s.l->ctx_tree_base[LANE] = s.lit_group[tree];
   }
@@ -1196,7 +1196,7 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
                   LU8 *lut1 = clut + 256;
                   int q2 = U((int)lut1[p2]);
                   while (j < end) {
-                    const int root = U((int)croot[(p1 << 3) | q2]);
+                    const int root = U((int)croot[(q2 << 8) | p1]);
                     q2 = U((int)lut1[p1]);
                     LFILL16();
                     c2b = p1;
@@ -1475,6 +1475,18 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
 // that point, to hot_loop (which then returns here at the next command boundary).
 // Bits are read in the same order as the general loop; only the refill / block-switch /
 // fence checks it makes are hoisted to where they provably cannot fire.
+//
+// Latency structure (one wave; every step of a command depends on the one before):
+//  * bit reader: the reference's (acc, bo, ho) are tracked exactly, but the bits come from a
+//    64-bit buffer holding the next two half-words as well, and the half-word after those is
+//    loaded one refill AHEAD -- a refill is a register shift, never an LDS round trip;
+//  * context-modelled literals: while literal k's prefix code is looked up, the lanes gather
+//    the whole root row of literal k + 1 (its p2 = literal k - 1 is known; ctx_root is laid
+//    out [lut1[p2]][p1]), so the next root is a readlane of the decoded symbol -- one LDS
+//    round trip per literal instead of two;
+//  * copies of <= 64 bytes: the source load is issued and the command loop goes on; the
+//    stores and the new (p1, p2) are completed when first needed (the next literals, the
+//    next copy, or the exit), so the load's latency overlaps the next command's header.
 template <bool kTrivial>
 __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
 #define U(x) __builtin_amdgcn_readfirstlane(x)
@@ -1482,20 +1494,34 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   GU8 *ring = (GU8 *)s.ring;
   LU16 *win16 = (LU16 *)g_lds.win;
   LU16 *t16 = (LU16 *)g_ltab;
-  LU16 *croot = (LU16 *)g_lds.ctx_root;
+  typedef const __attribute__((address_space(3))) uint64_t LU64;
+  LU64 *croot64 = (LU64 *)g_lds.ctx_root;
   LU8 *lut1 = (LU8 *)g_lds.ctx_lut + 256;
   const int lane = LANE;
   const int rmask = U(rmask_in);
   // positions stay below lim: no fence, flush or wrap inside a command
   const int lim = U(min(fence_in, rmask));
   const int npostfix = U(s.npostfix), ndirect = U(s.ndirect), max_back = U(s.max_back);
-  uint32_t acc = (uint32_t)U((int)s.acc);
   int bo = U(s.bo), ho = U(s.ho), pos = U(s.pos), mbl = U(s.mbl);
+  // buf = half-words ho-2 .. ho+1 (acc is its low half); pf = half-word ho+2, in flight
+  uint64_t buf = (uint64_t)(uint32_t)U((int)s.acc) |
+                 ((uint64_t)((uint32_t)U((int)win16[ho]) | ((uint32_t)U((int)win16[ho + 1]) << 16)) << 32);
+  uint32_t pf = win16[ho + 2];
   int cmd_blen = U(s.cmd_blen), lit_blen = U(s.lit_blen), dist_blen = U(s.dist_blen), max_dist = U(s.max_dist);
   int dr0 = U(s.rings[0]), dr1 = U(s.rings[1]), dr2 = U(s.rings[2]), dr3 = U(s.rings[3]), dridx = U(s.dist_rb_idx);
   int c1 = U((int)s.ring[(pos - 1) & rmask]), c2b = U((int)s.ring[(pos - 2) & rmask]);
   const int cmd_root = U((int)t16[s.cmd_base + s.cmd_tree_idx]);
   const int lit_root = kTrivial ? U((int)t16[s.lit_tree_idx]) : 0;
+  // lut1 of the literal context mode, packed: lane l holds entries l, l + 64, l + 128, l + 192
+  // as its four bytes (one readlane per lookup; a select among four registers would be
+  // turned into an indexed private array)
+  uint32_t lutp = 0;
+  if (!kTrivial)
+    lutp = (uint32_t)lut1[lane] | ((uint32_t)lut1[lane + 64] << 8) | ((uint32_t)lut1[lane + 128] << 16) |
+           ((uint32_t)lut1[lane + 192] << 24);
+  auto lut1_of = [lutp](int v) -> int {   // v wave-uniform
+    return (int)(((uint32_t)__builtin_amdgcn_readlane((int)lutp, v & 63) >> (8 * (v >> 6))) & 0xFF);
+  };
   uint32_t droot01, droot23;
   {
     const int db = s.dist_base, sl = s.dist_ctx_map_slice;
@@ -1506,28 +1532,32 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   }
   int insert_len = 0, copy_len = 0, dist_code = 0, distance = 0, j = 0, phase = ST_MAIN_LOOP;
   uint32_t ncmd = 0;
-  auto fill = [&]() {   // ho stays below 2080 here: no bounds check
-    if (bo >= 16) {
-      acc = ((uint32_t)U((int)win16[ho]) << 16) | (acc >> 16);
-      ho++;
-      bo -= 16;
-    }
+  // a copy whose source load is in flight: destination, length, the loaded byte per lane
+  int pend_cl = 0, pend_dst = 0;
+  int pend_v = 0;
+  auto shift16 = [&]() {   // the reference's acc/ho step, fed from the buffer; next half-word requested
+    buf = (buf >> 16) | ((uint64_t)(uint32_t)U((int)pf) << 48);
+    ho++;
+    bo -= 16;
+    pf = win16[ho + 2];
   };
-  auto rbits = [&](int n) -> int {   // n <= 16 after fill(), or any n <= 24 via two steps
-    int v = (int)((acc >> (bo & 31)) & ((1u << n) - 1u));
+  auto fill = [&]() {   // fill16: ho stays below 2080 here
+    if (bo >= 16) shift16();
+  };
+  auto peek32 = [&]() -> uint32_t { return (uint32_t)(buf >> (bo & 63)); };
+  auto rbits = [&](int n) -> int {   // n <= 16 after fill()
+    int v = (int)(peek32() & ((1u << n) - 1u));
     bo += n;
     return v;
   };
   auto rmany = [&](int n) -> int {
     if (n <= 16) return rbits(n);
     const int lo = rbits(16);
-    acc = ((uint32_t)U((int)win16[ho]) << 16) | (acc >> 16);
-    ho++;
-    bo -= 16;
+    shift16();
     return lo | (rbits(n - 16) << 16);
   };
   auto sym16 = [&](int root) -> int {
-    const uint32_t v = acc >> (bo & 31);
+    const uint32_t v = peek32();
     int off = root + (int)(v & 0xFF);
     const int e0 = U((int)t16[off]);
     const int nb = e0 >> 12;
@@ -1539,6 +1569,14 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     const int e1 = U((int)t16[off]);
     bo += (e1 >> 12) + 8;
     return e1 & 0xFFF;
+  };
+  auto finish_copy = [&]() {   // complete the copy in flight: stores, literal context
+    if (pend_cl) {
+      if (lane < pend_cl) ring[pend_dst + lane] = (uint8_t)pend_v;
+      c2b = pend_cl >= 2 ? __builtin_amdgcn_readlane(pend_v, pend_cl - 2) : c1;
+      c1 = __builtin_amdgcn_readlane(pend_v, pend_cl - 1);
+      pend_cl = 0;
+    }
   };
 #ifdef MIB_PROF
   uint64_t fp[5] = {0, 0, 0, 0, 0};
@@ -1556,7 +1594,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     FMARK(4);
     // ---- command boundary: a block switch or refill goes to the general loop
     if (mbl <= 0 || cmd_blen == 0 || ho > 2030 - 8) break;
-    uint32_t acc0 = acc;
+    const uint64_t buf0 = buf;
+    const uint32_t pf0 = pf;
     int bo0 = bo, ho0 = ho;
     fill();
     const int sym = sym16(cmd_root);
@@ -1570,7 +1609,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     if (insert_len > lit_blen || (int64_t)pos + insert_len + copy_len >= lim ||
         ho + ((insert_len * 15) >> 4) > 2030 - 12) {
       // hand the command over undecoded
-      acc = acc0;
+      buf = buf0;
+      pf = pf0;
       bo = bo0;
       ho = ho0;
       break;
@@ -1579,6 +1619,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     FMARK(0);
     // ---- literals
     if (insert_len) {
+      if (!kTrivial) finish_copy();   // (p1, p2) of the first literal
       int fl0 = pos;
       uint32_t ob = 0;
       const int end = pos + insert_len;
@@ -1597,13 +1638,15 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
           }
         }
       } else {
-        int q2 = U((int)lut1[c2b]);
+        int root = U((int)g_lds.ctx_root[(lut1_of(c2b) << 8) | c1]);
         while (pos < end) {
-          const int root = U((int)croot[(c1 << 3) | q2]);
-          q2 = U((int)lut1[c1]);
+          // the root row of the next literal (its p2 is the current c1), 4 entries per lane
+          const uint64_t row = croot64[(lut1_of(c1) << 6) | lane];
           fill();
           c2b = c1;
           c1 = U(sym16(root));
+          const uint64_t e = c1 & 2 ? row >> 32 : row;   // lane c1 >> 2 holds entries 4 (c1 >> 2) ..
+          root = __builtin_amdgcn_readlane((int)(uint32_t)(e >> (16 * (c1 & 1))), c1 >> 2) & 0xFFFF;
           ob = lane == (pos & 63) ? (uint32_t)c1 : ob;
           pos++;
           if ((pos & 63) == 0) {
@@ -1625,7 +1668,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     j = insert_len;
     phase = ST_INSERT_LOOP;
     if (mbl - insert_len <= 0 || (dist_code >= 0 && dist_blen == 0) || ho > 2030 - 8) break;
-    const uint32_t dacc = acc;
+    const uint64_t dbuf = buf;
+    const uint32_t dpf = pf;
     const int dbo = bo, dho = ho, dmax = max_dist;
     int dc = dist_code;
     if (dc < 0) {
@@ -1649,7 +1693,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
         }
         int bv;
         if (bo + eb <= 32) {
-          bv = (int)((acc >> (bo & 31)) & ((1u << eb) - 1u));
+          bv = (int)(peek32() & ((1u << eb) - 1u));
           bo += eb;
         } else {
           fill();
@@ -1663,7 +1707,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     const int src = (pos - distance) & rmask;
     if (distance < 0 || distance > max_dist || copy_len > mbl - insert_len || src + copy_len >= rmask) {
       // error, dictionary word or wrapping copy: redo the distance in the general loop
-      acc = dacc;
+      buf = dbuf;
+      pf = dpf;
       bo = dbo;
       ho = dho;
       max_dist = dmax;
@@ -1679,34 +1724,42 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       else dr3 = distance;
     }
     FMARK(2);
-    // ---- copy (no wrap, no fence)
+    // ---- copy (no wrap, no fence): the previous copy is completed first (this one may read it)
+    finish_copy();
     {
       const int cl = copy_len, dist = distance;
-      int lastv = 0;
-      const int nit = U((cl + 63) >> 6);
-      if (dist >= cl) {
-        for (int it = 0; it < nit; it++) {
-          const int k = it * 64 + lane;
-          if (k < cl) {
-            lastv = ring[src + k];
-            ring[pos + k] = (uint8_t)lastv;
-          }
-        }
+      if (cl <= 64) {   // one lane per byte: issue the load, complete later
+        const int q = dist >= cl ? lane : lane % dist;
+        pend_v = lane < cl ? (int)ring[src + q] : 0;
+        pend_dst = pos;
+        pend_cl = cl;
       } else {
-        int q = lane % dist;
-        const int qstep = 64 % dist;
-        for (int it = 0; it < nit; it++) {
-          const int k = it * 64 + lane;
-          if (k < cl) {
-            lastv = ring[src + q];
-            ring[pos + k] = (uint8_t)lastv;
+        int lastv = 0;
+        const int nit = U((cl + 63) >> 6);
+        if (dist >= cl) {
+          for (int it = 0; it < nit; it++) {
+            const int k = it * 64 + lane;
+            if (k < cl) {
+              lastv = ring[src + k];
+              ring[pos + k] = (uint8_t)lastv;
+            }
           }
-          q += qstep;
-          if (q >= dist) q -= dist;
+        } else {
+          int q = lane % dist;
+          const int qstep = 64 % dist;
+          for (int it = 0; it < nit; it++) {
+            const int k = it * 64 + lane;
+            if (k < cl) {
+              lastv = ring[src + q];
+              ring[pos + k] = (uint8_t)lastv;
+            }
+            q += qstep;
+            if (q >= dist) q -= dist;
+          }
         }
+        c2b = __builtin_amdgcn_readlane(lastv, (cl - 2) & 63);
+        c1 = __builtin_amdgcn_readlane(lastv, (cl - 1) & 63);
       }
-      c2b = cl >= 2 ? __builtin_amdgcn_readlane(lastv, (cl - 2) & 63) : c1;
-      c1 = __builtin_amdgcn_readlane(lastv, (cl - 1) & 63);
       mbl -= cl;
       pos += cl;
     }
@@ -1714,8 +1767,9 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     j = 0;
     FMARK(3);
   }
+  finish_copy();
   wave_sync();
-  s.acc = acc; s.bo = bo; s.ho = ho; s.pos = pos; s.mbl = mbl;
+  s.acc = (uint32_t)buf; s.bo = bo; s.ho = ho; s.pos = pos; s.mbl = mbl;
   s.cmd_blen = cmd_blen; s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist;
   s.rings[0] = dr0; s.rings[1] = dr1; s.rings[2] = dr2; s.rings[3] = dr3; s.dist_rb_idx = dridx;
   s.insert_len = insert_len; s.copy_len = copy_len; s.dist_code = dist_code; s.j = j;
