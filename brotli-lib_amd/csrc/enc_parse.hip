@@ -14,20 +14,25 @@ namespace enc {
 // than kLongCopy is taken outright and the parse jumps to its end, as the reference does
 // (:518-533).
 //
-// One wave per segment, the pending nodes in REGISTERS: the parse runs in batches of 64
-// positions starting at i0, and lane j of chunk k holds node i0 + 64 k + j.  Relaxing the
-// edge of length l out of i = i0 + off lands in chunk (off + l) / 64, lane (off + l) % 64:
-// every lane relaxes the one length that maps to it -- a lane-local compare/select, no LDS
-// round trip, no shuffle -- and only the chunks holding lengths 0..maxlen are touched.
-// Node i is read with three readlanes from chunk 0.  At a batch end the chunks move down
-// by one (chunk 0 is all consumed nodes).
+// kS segments per wave, kL = 64 / kS lanes each, the pending nodes in REGISTERS: a segment
+// is parsed in batches of kL positions starting at i0, and lane j of the segment's lane
+// group in chunk k holds node i0 + kL k + j.  Relaxing the edge of length l out of
+// i = i0 + off lands in chunk (off + l) / kL, lane (off + l) % kL: every lane relaxes the one
+// length that maps to it -- a lane-local compare/select, no LDS round trip -- and only the
+// chunks holding lengths 0..maxlen are touched.  The segments of a wave advance in lockstep
+// (one position each per step), so one VALU instruction relaxes kS positions: text's
+// staircases are short (maxlen ~ 10-30), and a 64-lane chunk per position left most lanes
+// idle.  Everything per segment is lane-group-uniform and lives in VGPRs; control flow that
+// differs between the segments (a segment's end, a long copy, a batch end) is predicated.
+// Node i is fetched with ds_bpermute from its lane; at a batch end the segment's chunks move
+// down by one (chunk 0 is all consumed nodes).
 //
 // The length-dependent half of a copy's price (copy code, its extra bits, the command
 // code it forms with the insert code, with and without short code 0) comes from an LDS
 // table indexed by (insert code, length), fp16 pairs, built once per workgroup.
-// Per-position inputs (matches, distance costs, literal cost) are staged one lane per
-// position, loaded a batch ahead, and read back with readlanes; the batch's choices are
-// collected the same way and stored as one coalesced write.
+// Per-position inputs (matches, distance-cost codes, literal cost) are staged one lane per
+// position into LDS, loaded a batch ahead, and read back with one broadcast read per
+// segment; the batch's choices are collected per lane and stored as one coalesced write.
 #ifdef MIB_PROF   // timing experiment: cycles in staging / node read / long copies / relaxation; counts
 __device__ unsigned long long g_dp_prof[8];
 #define DPMARK(slot)                                  \
@@ -41,19 +46,17 @@ __device__ unsigned long long g_dp_prof[8];
 #define DPMARK(slot) do {} while (0)
 #define DPCOUNT(slot, v) do {} while (0)
 #endif
-constexpr int kC = 5;                 // chunks: batch offset (< 64) + longest relaxed length (<= kLongCopy)
-constexpr int kDpWaves = 4;           // segments (waves) per workgroup, sharing the length table
+constexpr int kS = 2;                 // segments per wave
+constexpr int kL = 64 / kS;           // lanes per segment
+constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
+constexpr int kDpWaves = 4;           // waves per workgroup, sharing the length table
 constexpr int kLenTab = kLongCopy + 1;
 constexpr float kInf = 3.0e38f;
 constexpr uint32_t kCostLast = 255;   // cost code of a match at the path's last distance
-static_assert(63 + kLongCopy < 64 * kC, "every relaxed length must land in a chunk");
+static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
 
 typedef const __attribute__((address_space(1))) uint8_t GCU8;
 
-__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)l); }
-__device__ __forceinline__ float rdlf(float v, uint32_t l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)l));
-}
 // kCopyExtra / kInsExtra in closed form (no table loads on the serial path)
 __device__ __forceinline__ uint32_t copy_extra(int cc) { return cc < 8 ? 0u : cc < 18 ? (uint32_t)(cc - 6) >> 1 : cc < 23 ? (uint32_t)(cc - 12) : 24u; }
 __device__ __forceinline__ uint32_t ins_extra(int ic) {
@@ -70,7 +73,22 @@ __device__ __forceinline__ float copy_price(int ic, uint32_t l, bool last, float
   return (float)copy_extra(cc) + cmd_cost(cmd) + (last && cmd >= 128 ? dist0 : 0.f);
 }
 
-struct Staged {   // one position's parse inputs (lane j of a batch = position i0 + j)
+// ins_code / ins_extra (command.ts:29-64) without branches: the node's insert length is
+// lane-group-uniform but not wave-uniform here, so a branchy form would run every arm
+__device__ __forceinline__ int ins_code_sel(uint32_t n) {
+  const uint32_t a = n - 2u, lga = 31u - (uint32_t)__clz((int)(a | 1u));          // n in [6, 130)
+  const uint32_t nb = lga - 1u;
+  const uint32_t mid = (nb << 1) + (a >> nb) + 2u;
+  const uint32_t hi = 31u - (uint32_t)__clz((int)((n - 66u) | 1u)) + 10u;          // n in [130, 2114)
+  uint32_t c = n < 6u ? n : n < 130u ? mid : n < 2114u ? hi : n < 6210u ? 21u : n < 22594u ? 22u : 23u;
+  return (int)c;
+}
+__device__ __forceinline__ uint32_t ins_extra_sel(int ic) {
+  const uint32_t u = (uint32_t)ic;
+  return u < 6u ? 0u : u < 16u ? (u - 4u) >> 1 : u < 21u ? u - 10u : u == 21u ? 12u : u == 22u ? 14u : 24u;
+}
+
+struct Staged {   // one position's parse inputs as loaded
   uint32_t m[kMaxMatches];
   uint32_t nm;
   uint32_t lit;
@@ -81,16 +99,27 @@ __device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches,
   st.m[0] = a.x; st.m[1] = a.y; st.m[2] = a.z; st.m[3] = a.w;
   st.nm = (a.x != 0u) + (a.y != 0u) + (a.z != 0u) + (a.w != 0u);
 }
+struct StageEnt {   // one position's parse inputs in LDS (48 B: two b128 reads and a b64)
+  uint32_t m[kMaxMatches];   // (clipped length << 24) | distance, 0 = none
+  uint32_t mc[kMaxMatches];  // distance | distance-cost code << 24 (quarter bits)
+  uint32_t info;             // nm | maxlen << 8 (clipped to the segment)
+  float lc;                  // literal cost
+  uint32_t pad[2];
+};
 __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (distance << 32) | length, 0 = literal
   const uint32_t cl = m & 0xFFFF;
   return cl ? (((uint64_t)d << 32) | cl) : 0ull;
 }
+__device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lane_src << 2), (int)v);
+}
 
-__global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5))) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
+__global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const uint32_t *matches,
                                                            uint64_t *choice /* per position+1 */) {
   __shared__ uint32_t lentab[24 * kLenTab];   // (insert code, length) -> fp16 (explicit distance) | fp16 (short code 0) << 16
-  __shared__ float litc_all[kDpWaves][256];
+  __shared__ float litc_all[kDpWaves * kS][256];
+  __shared__ StageEnt stg_all[kDpWaves][64];
   const float dist0 = dist_sym_cost(0);
   for (int t = threadIdx.x; t < 24 * kLenTab; t += 64 * kDpWaves) {
     const int ic = t / kLenTab;
@@ -103,28 +132,40 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
     lentab[t] = v;
   }
   __syncthreads();
-  // the wave index is wave-uniform: say so, so that everything derived from the segment stays scalar
   const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int s = blockIdx.x * kDpWaves + (int)w;
-  if (s >= nsegs) return;
-  float *litc = litc_all[w];
-  const Seg sg = segs[s];
-  const Job &jb = jobs[sg.job];
-  const uint8_t *data = jb.data;
-  const uint32_t a = sg.start, b = sg.end, gbase = jb.pos_base;
-  const int ndirect = (int)jb.ndirect, npostfix = (int)jb.npostfix;
-  if (a >= b) return;
+  const uint32_t h = lane / kL, hl = lane % kL, hbase = h * kL;
+  const int sgi = (blockIdx.x * kDpWaves + (int)w) * kS + (int)h;
+  StageEnt *stg = stg_all[w];
+  float *litc = litc_all[w * kS + h];
+  // this lane group's segment (a = b: nothing to parse)
+  uint32_t a = 0, b = 0, gbase = 0, job = 0;
+  const uint8_t *data = nullptr;
+  int ndirect = 0, npostfix = 0;
+  if (sgi < nsegs) {
+    const Seg &sg = segs[sgi];
+    const Job &jb = jobs[sg.job];
+    a = sg.start;
+    b = sg.end;
+    gbase = jb.pos_base;
+    job = sg.job;
+    data = jb.data;
+    ndirect = (int)jb.ndirect;
+    npostfix = (int)jb.npostfix;
+  }
+  if (__ballot(a < b) == 0) return;
   // literal costs from the stream's order-0 histogram (zopfli-cost-model.ts:163-189)
   {
     uint32_t part = 0;
-    for (uint32_t k = lane; k < 256; k += 64) part += lit_histo[sg.job * 256 + k];
-    for (int o = 32; o; o >>= 1) part += __shfl_xor(part, o);
+    if (a < b)
+      for (uint32_t k = hl; k < 256; k += kL) part += lit_histo[job * 256 + k];
+    for (int o = kL / 2; o; o >>= 1) part += __shfl_xor(part, o);
     const float lt = log2f((float)max(part, 1u));
-    for (uint32_t k = lane; k < 256; k += 64) {
-      const uint32_t c = lit_histo[sg.job * 256 + k];
-      const float v = c ? lt - log2f((float)c) : lt + 2.f;
-      litc[k] = (float)(uint32_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f) * (1.f / 256.f);
-    }
+    if (a < b)
+      for (uint32_t k = hl; k < 256; k += kL) {
+        const uint32_t c = lit_histo[job * 256 + k];
+        const float v = c ? lt - log2f((float)c) : lt + 2.f;
+        litc[k] = (float)(uint32_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f) * (1.f / 256.f);
+      }
   }
   wave_sync();
   // the pending nodes: cost, last distance, (copy length that reached it | insert length << 16)
@@ -135,154 +176,165 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
     wc[c] = kInf;
     wd[c] = wm[c] = 0;
   }
-  if (lane == 0) wc[0] = 0.f;   // node a
-  // the current batch (registers, lane = position - i0) and the next one
-  uint32_t bm[kMaxMatches], binfo = 0;   // binfo: nm | maxlen << 8 (clipped to the segment)
-  uint32_t bmc[kMaxMatches];              // distance | distance-cost code << 24 (quarter bits)
-  float blc = 0.f;
+  if (hl == 0) wc[0] = 0.f;   // node a
   Staged pf;
   uint32_t pf_at = a;
-  if (a + lane < b) load_staged(pf, matches, data, gbase + a + lane, a + lane);
+  if (a + hl < b) load_staged(pf, matches, data, gbase + a + hl, a + hl);
   uint32_t chd = 0, chm = 0;   // choices of the batch
   uint32_t i = a, i0 = a;
+  bool done = a >= b;
 #ifdef MIB_PROF
   uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t pt0 = __builtin_amdgcn_s_memtime();
 #endif
-  // stage the batch starting at i0 (the window's chunk 0 starts there)
+  // stage the batch starting at i0 (the window's chunk 0 starts there) into this lane's entry
   auto stage = [&]() {
     Staged cur;
+    cur.nm = 0;
+    cur.lit = 0;
     if (pf_at == i0) {
       cur = pf;
-    } else if (i0 + lane < b) {   // the parse jumped past the prefetched batch
-      load_staged(cur, matches, data, gbase + i0 + lane, i0 + lane);
+    } else if (i0 + hl < b) {   // the parse jumped past the prefetched batch
+      load_staged(cur, matches, data, gbase + i0 + hl, i0 + hl);
     }
-    const uint32_t nx = i0 + 64;
-    if (nx + lane < b) load_staged(pf, matches, data, gbase + nx + lane, nx + lane);
+    const uint32_t nx = i0 + kL;
+    if (nx + hl < b) load_staged(pf, matches, data, gbase + nx + hl, nx + hl);
     pf_at = nx;
-    const uint32_t p = i0 + lane;
+    const uint32_t p = i0 + hl;
     const uint32_t nm = p < b ? cur.nm : 0u;
-    blc = p < b ? litc[cur.lit] : 0.f;
+    StageEnt e;
+    e.lc = p < b ? litc[cur.lit] : 0.f;
     uint32_t maxlen = 0;
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
-      bm[q] = 0;
-      bmc[q] = 0;
+      e.m[q] = 0;
+      e.mc[q] = 0;
       if ((uint32_t)q < nm) {
         uint32_t extra;
         const uint32_t ln = min(match_length(cur.m[q]), b - p);
         const uint32_t dp = dist_prefix(match_dist(cur.m[q]) + 15, ndirect, npostfix, &extra);
-        bm[q] = (ln << 24) | match_dist(cur.m[q]);
+        e.m[q] = (ln << 24) | match_dist(cur.m[q]);
         const float dc = (float)(dp >> 10) + dist_sym_cost(dp & 0x3FFu);
-        bmc[q] = match_dist(cur.m[q]) | (min((uint32_t)(dc * 4.f + 0.5f), kCostLast - 1) << 24);
+        e.mc[q] = match_dist(cur.m[q]) | (min((uint32_t)(dc * 4.f + 0.5f), kCostLast - 1) << 24);
         maxlen = ln;
       }
     }
-    binfo = nm | (maxlen << 8);
+    e.info = nm | (maxlen << 8);
+    e.pad[0] = e.pad[1] = 0;
+    stg[lane] = e;
     DPCOUNT(6, 1);
   };
-  stage();
+  if (!done) stage();
+  wave_sync();
   DPMARK(0);
   for (;;) {
-    const uint32_t off = i - i0;
-    // ---- node i
-    const float ci = rdlf(wc[0], off);
-    const uint32_t ld = rdl(wd[0], off), mm = rdl(wm[0], off);
-    chd = lane == off ? ld : chd;
-    chm = lane == off ? mm : chm;
-    if (i == b) break;
+    if (__ballot(!done) == 0) break;
+    const uint32_t off = i - i0;   // < kL
+    // ---- node i of each segment, from its lane of chunk 0
+    const uint32_t src = hbase + (off & (kL - 1));
+    const float ci = __uint_as_float(bperm(src, __float_as_uint(wc[0])));
+    const uint32_t ld = bperm(src, wd[0]), mm = bperm(src, wm[0]);
+    if (!done) {
+      chd = hl == off ? ld : chd;
+      chm = hl == off ? mm : chm;
+      if (i == b) {   // the last batch, through node b
+        const uint32_t p = i0 + hl;
+        if (p <= b && p != a) choice[gbase + p] = choice_of(chd, chm);
+        done = true;
+      }
+    }
+    const bool act = !done;
+    const StageEnt &e = stg[src];
+    const uint32_t info = e.info;
+    const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? (info >> 8) : 0u;
+    const float litcost = e.lc;
     const uint32_t ins = mm >> 16;
-    const uint32_t info = rdl(binfo, off);
-    const uint32_t nm = info & 0xFF, maxlen = info >> 8;
-    const float litcost = rdlf(blc, off);
-    const int ic = ins_code(ins);
-    const float base = ci + (float)ins_extra(ic);
+    const int ic = ins_code_sel(ins);
+    const float base = ci + (float)ins_extra_sel(ic);
     DPMARK(1);
     DPCOUNT(4, 1);
-    if (maxlen > (uint32_t)kLongCopy) {
-      // forceful long copy (backward-references-hq.ts:518-533): the shortest-distance match
-      // longer than kLongCopy
-      uint32_t fl = 0, fd = 0;
-      float fdc = 0.f;
+    const bool longc = maxlen > (uint32_t)kLongCopy;
+    if (__ballot(longc)) {
+      if (longc) {
+        // forceful long copy (backward-references-hq.ts:518-533): the shortest-distance match
+        // longer than kLongCopy; this segment's pending nodes are abandoned and the parse
+        // resumes at the copy's end with a new batch
+        uint32_t fl = 0, fd = 0;
+        float fdc = 0.f;
 #pragma unroll
-      for (int q = kMaxMatches - 1; q >= 0; q--) {
-        if ((uint32_t)q < nm) {
-          const uint32_t m = rdl(bm[q], off);
-          if (match_length(m) > (uint32_t)kLongCopy) {
-            fd = match_dist(m);
-            fl = match_length(m);
-            fdc = (float)(rdl(bmc[q], off) >> 24) * 0.25f;
+        for (int q = kMaxMatches - 1; q >= 0; q--) {
+          if ((uint32_t)q < nm) {
+            const uint32_t m = e.m[q];
+            if (match_length(m) > (uint32_t)kLongCopy) {
+              fd = match_dist(m);
+              fl = match_length(m);
+              fdc = (float)(e.mc[q] >> 24) * 0.25f;
+            }
           }
         }
-      }
-      const uint32_t limit = b - i;
-      if (fl == kMatchLenSat && limit > kMatchLenSat) {
-        // a saturated match: measure the copy, 64 bytes a step
-        GCU8 *cp = (GCU8 *)(data + i), *src = (GCU8 *)(data + i - fd);
-        const uint32_t cap = min(limit, 65535u);
-        for (;;) {
-          const uint32_t x = fl + lane;
-          const uint64_t ok = __ballot(x < cap && cp[x] == src[x]);
-          if (ok == ~0ull) {
-            fl += 64;
-            continue;
+        const uint32_t limit = b - i;
+        if (fl == kMatchLenSat && limit > kMatchLenSat) {
+          // a saturated match: measure the copy, kL bytes a step
+          GCU8 *cp = (GCU8 *)(data + i), *sp = (GCU8 *)(data + i - fd);
+          const uint32_t cap = min(limit, 65535u);
+          for (;;) {
+            const uint32_t x = fl + hl;
+            const uint64_t okb = __ballot(x < cap && cp[x] == sp[x]);
+            const uint32_t ok = (uint32_t)(okb >> hbase) & (uint32_t)((1ull << kL) - 1);
+            if (ok == (uint32_t)((1ull << kL) - 1)) {
+              fl += kL;
+              continue;
+            }
+            fl += (uint32_t)__ffs(~ok) - 1;
+            break;
           }
-          fl += (uint32_t)__ffsll((unsigned long long)~ok) - 1;
-          break;
+          fl = min(fl, cap);
         }
-        fl = min(fl, cap);
-      }
-      const int cc = copy_code(fl);
-      const bool last = fd == ld;
-      const int cmd = combine_codes(ic, cc, last);
-      const float fc = base + (float)copy_extra(cc) + cmd_cost(cmd) + (last ? (cmd < 128 ? 0.f : dist0) : fdc);
-      // store the batch's choices up to i; every pending node is abandoned; the parse
-      // resumes at the copy's end with a new batch
-      {
-        const uint32_t p = i0 + lane;
-        if (p <= i && p != a) choice[gbase + p] = choice_of(chd, chm);
-      }
-      i += fl;
-      i0 = i;
+        const int cc = copy_code(fl);
+        const bool last = fd == ld;
+        const int cmd = combine_codes(ic, cc, last);
+        const float fc = base + (float)copy_extra(cc) + cmd_cost(cmd) + (last ? (cmd < 128 ? 0.f : dist0) : fdc);
+        {
+          const uint32_t p = i0 + hl;
+          if (p <= i && p != a) choice[gbase + p] = choice_of(chd, chm);
+        }
+        i += fl;
+        i0 = i;
 #pragma unroll
-      for (int c = 0; c < kC; c++) wc[c] = kInf;
-      if (lane == 0) {
-        wc[0] = fc;
-        wd[0] = fd;
-        wm[0] = fl;
+        for (int c = 0; c < kC; c++) wc[c] = kInf;
+        if (hl == 0) {
+          wc[0] = fc;
+          wd[0] = fd;
+          wm[0] = fl;
+        }
+        stage();
+        DPCOUNT(7, 1);
       }
-      stage();
-      DPCOUNT(7, 1);
+      wave_sync();
       DPMARK(2);
       continue;
     }
-    // the match staircase of i: lengths (clipped, scalar) and the packed (distance | cost
-    // code) words, moved once into wave-uniform VGPRs so that each chunk selects with one
-    // compare and one v_cndmask per match; a match at the path's last distance gets the
-    // code kCostLast (priced with short code 0)
+    // the match staircase of i: lengths (clipped) and the packed (distance | cost code) words;
+    // a match at the path's last distance gets the code kCostLast (priced with short code 0)
     uint32_t mL[kMaxMatches], vpk[kMaxMatches];
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
-      mL[q] = 0;
-      vpk[q] = 0;
-      if ((uint32_t)q < nm) {
-        mL[q] = match_length(rdl(bm[q], off));
-        uint32_t pk = rdl(bmc[q], off);
-        if (match_dist(pk) == ld) pk |= kCostLast << 24;
-        vpk[q] = pk;
-      }
+      const uint32_t m = e.m[q];   // 0 past nm
+      mL[q] = act ? match_length(m) : 0u;
+      const uint32_t pk = e.mc[q];
+      vpk[q] = match_dist(pk) == ld ? (pk | (kCostLast << 24)) : pk;
     }
     const uint32_t maxrel = max(1u, maxlen);
     const uint32_t *trow = lentab + ic * kLenTab;
-    // relax every edge out of i: lane j of chunk k takes length 64 k + j - off
+    // relax every edge out of i: lane j of chunk k takes length kL k + j - off
 #pragma unroll
     for (int c = 0; c < kC; c++) {
-      if (c > 0 && 64u * c > off + maxrel) break;
+      if (c > 0 && __ballot(act && (uint32_t)(kL * c) <= off + maxrel) == 0) break;
       DPCOUNT(5, 1);
-      const uint32_t l = 64u * c + lane - off;   // wraps (huge) for consumed nodes
+      const uint32_t l = (uint32_t)(kL * c) + hl - off;   // wraps (huge) for consumed nodes
       float cand = kInf;
       uint32_t nd = ld, nmeta = min(ins + 1, 65535u) << 16;
-      if (l == 1) cand = ci + litcost;
+      if (l == 1 && act) cand = ci + litcost;
       if (l >= 4 && l <= maxlen) {
         uint32_t x = 0;
 #pragma unroll
@@ -304,20 +356,24 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
         wm[c] = nmeta;
       }
     }
-    i++;
-    if (i - i0 == 64) {
-      // batch end: store its choices, move the window down one chunk, stage the next batch
-      if (i0 + lane != a) choice[gbase + i0 + lane] = choice_of(chd, chm);   // node a belongs to the previous segment
+    if (act) i++;
+    const bool bend = act && i - i0 == (uint32_t)kL;
+    if (__ballot(bend)) {
+      if (bend) {
+        // batch end: store its choices, move the window down one chunk, stage the next batch
+        if (i0 + hl != a) choice[gbase + i0 + hl] = choice_of(chd, chm);   // node a belongs to the previous segment
 #pragma unroll
-      for (int c = 0; c + 1 < kC; c++) {
-        wc[c] = wc[c + 1];
-        wd[c] = wd[c + 1];
-        wm[c] = wm[c + 1];
+        for (int c = 0; c + 1 < kC; c++) {
+          wc[c] = wc[c + 1];
+          wd[c] = wd[c + 1];
+          wm[c] = wm[c + 1];
+        }
+        wc[kC - 1] = kInf;
+        wd[kC - 1] = wm[kC - 1] = 0;
+        i0 = i;
+        stage();
       }
-      wc[kC - 1] = kInf;
-      wd[kC - 1] = wm[kC - 1] = 0;
-      i0 = i;
-      stage();
+      wave_sync();
     }
     DPMARK(3);
   }
@@ -325,11 +381,6 @@ __global__ __launch_bounds__(64 * kDpWaves) __attribute__((amdgpu_waves_per_eu(5
   if (lane == 0)
     for (int q = 0; q < 8; q++) atomicAdd(&g_dp_prof[q], (unsigned long long)prof[q]);
 #endif
-  // the last batch, through node b
-  {
-    const uint32_t p = i0 + lane;
-    if (p <= b && p != a) choice[gbase + p] = choice_of(chd, chm);
-  }
 }
 
 // ---------------------------------------------------------------- 4. backtrack, wave per segment
@@ -435,7 +486,7 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 #endif
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                const uint32_t *matches, uint64_t *choice) {
-  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kDpWaves - 1) / kDpWaves), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h, matches,
+  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kDpWaves * kS - 1) / (kDpWaves * kS)), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h, matches,
                      choice);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {
