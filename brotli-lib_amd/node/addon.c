@@ -48,7 +48,11 @@ static int get_bytes(napi_env env, napi_value v, const uint8_t **p, size_t *n) {
 }
 
 static napi_value throw_code(napi_env env, int code) {
-  napi_throw_error(env, NULL, mib_strerror(code));
+  /* the reference's JS engine errors keep their type and message (engine.ts:998 subarray of
+     a missing dictionary chunk; Uint8Array.set out of range) */
+  if (code == MIB_E_JS_TYPE_ERROR) napi_throw_type_error(env, NULL, "Cannot read property 'subarray' of undefined");
+  else if (code == MIB_E_JS_RANGE_ERROR) napi_throw_range_error(env, NULL, "offset is out of bounds");
+  else napi_throw_error(env, NULL, mib_strerror(code));
   return NULL;
 }
 

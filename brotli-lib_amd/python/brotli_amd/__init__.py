@@ -133,9 +133,14 @@ def _opts(options):
 
 
 def _bytes(x):
-    if isinstance(x, (bytes, bytearray, memoryview)):
+    """Uint8Array / Int8Array equivalents: any buffer (bytes, bytearray, memoryview, array('b'),
+    numpy int8/uint8) is taken as its raw bytes, as decode.ts:31-33 views an Int8Array."""
+    if isinstance(x, (bytes, bytearray)):
         return bytes(x)
-    return bytes(bytearray(x))
+    try:
+        return bytes(memoryview(x).cast('B'))
+    except TypeError:
+        return bytes(bytearray(x))
 
 
 def brotliEncode(input, options=None):

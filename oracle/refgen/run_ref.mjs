@@ -37,7 +37,14 @@ for (const job of jobs) {
       if (out.length <= (job.inline_max || 4096)) r.out_b64 = Buffer.from(out).toString('base64')
       try { r.native_roundtrip = Buffer.compare(zlib.brotliDecompressSync(Buffer.from(out)), input) === 0 } catch (e) { r.native_roundtrip = false }
     } else if (job.op === 'decode') {
-      const out = m.dec.brotliDecode(new Uint8Array(input), job.opts)
+      let opts = job.opts
+      if (job.dict_b64 !== undefined) {   // customDictionary (compound dictionary), as Uint8Array or Int8Array
+        const d = Buffer.from(job.dict_b64, 'base64')
+        const u = new Uint8Array(d.length)
+        u.set(d)
+        opts = Object.assign({}, opts || {}, { customDictionary: job.dict_int8 ? new Int8Array(u.buffer) : u })
+      }
+      const out = m.dec.brotliDecode(new Uint8Array(input), opts)
       r.len = out.length
       r.sha256 = sha(out)
     } else if (job.op === 'bt_matches') {

@@ -46,8 +46,9 @@ def decode(data, out_size=None, dictionary=None):
         p = peek_size(data)
         out_size = p if p > 0 else -1
     o, n = _P(), ctypes.c_size_t()
-    d = dictionary or None
-    rc = lib().oracle_decode(data, len(data), d, len(d) if d else 0, out_size, ctypes.byref(o), ctypes.byref(n))
+    d = bytes(dictionary) if dictionary is not None else None   # an empty dictionary is still attached
+    rc = lib().oracle_decode(data, len(data), d, len(d) if d is not None else 0, out_size, ctypes.byref(o),
+                             ctypes.byref(n))
     if rc:
         return rc
     r = ctypes.string_at(o, n.value)

@@ -49,6 +49,37 @@ for (const c of errs) {
 }
 console.log('error corpus', ok)
 
+// customDictionary (compound dictionary): the reference decoder's outputs and errors, the
+// dictionary passed as Uint8Array or Int8Array (oracle/refgen/make_compound.py)
+function xorshiftBytes(seed, len) {   // brotli_amd.datagen.random_bytes(len, xorshift32(seed))
+  let x = seed >>> 0
+  const out = new Uint8Array(len)
+  for (let i = 0; i < len; i++) {
+    x ^= x << 13; x >>>= 0
+    x ^= x >>> 17
+    x ^= x << 5; x >>>= 0
+    out[i] = x & 0xff
+  }
+  return out
+}
+const comp = JSON.parse(fs.readFileSync(path.join(G, 'decode_compound.json'))).cases
+let cok = 0
+for (const c of comp) {
+  const input = new Uint8Array(Buffer.from(c.in_b64, 'base64'))
+  const d = xorshiftBytes(c.dict.seed, c.dict.len)
+  const dict = c.int8 ? new Int8Array(d.buffer) : d
+  let got
+  try {
+    got = crypto.createHash('sha256').update(lib.brotliDecode(input, { customDictionary: dict })).digest('hex')
+  } catch (e) {
+    got = e.message
+    if (!c.error.startsWith('Brotli error code')) assert.ok(e instanceof TypeError, 'TypeError expected')
+  }
+  assert.strictEqual(got, c.error !== undefined ? c.error : c.sha256, c.in_b64.slice(0, 40))
+  cok++
+}
+console.log('compound dictionary', cok)
+
 // round trips, options, modes
 const text = fs.readFileSync(path.join(G, 'vectors', 'alice29.txt'))
 for (const q of [0, 1, 5, 9, 10, 11]) {

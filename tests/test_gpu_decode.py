@@ -100,3 +100,26 @@ def test_random_truncations_match_oracle():
         except brotli_amd.BrotliError as e:
             got = e.code
         assert got == exp, cut
+
+
+def test_compound_dictionary_matches_reference():
+    """brotliDecode(data, {customDictionary}) against the reference's own outputs and errors
+    (tests/golden/decode_compound.json), the dictionary given as bytes and as signed int8."""
+    import array
+    n = 0
+    for c in _cases('decode_compound.json'):
+        data = base64.b64decode(c['in_b64'])
+        d = _inputs.resolve(c['dict'])
+        dic = array.array('b', d) if c['int8'] else d
+        try:
+            got = hashlib.sha256(brotli_amd.brotliDecode(data, {'customDictionary': dic})).hexdigest()
+        except brotli_amd.BrotliError as e:
+            got = e.code if 'subarray' in c.get('error', '') else str(e)
+        if 'error' not in c:
+            assert got == c['sha256'], c
+            n += 1
+        elif c['error'].startswith('Brotli error code'):
+            assert got == c['error'], (c, got)
+        else:
+            assert got == -106, (c, got)   # MIB_E_JS_TYPE_ERROR: the reference's TypeError
+    assert n > 100

@@ -93,3 +93,22 @@ def test_oracle_decoder_is_thread_safe():
     with ThreadPoolExecutor(8) as ex:
         got = list(ex.map(lambda p: _oracle.decode(p[0]) == p[1], work))
     assert all(got)
+
+
+def test_compound_dictionary_matches_reference():
+    """customDictionary (compound dictionary, engine.ts:142-159,946-1011): the oracle decodes
+    the reference-decoded corpus (oracle/refgen/make_compound.py) to the same bytes / errors,
+    including the reference's rule that a dictionary copy must end at the dictionary's end
+    (-9 otherwise) and its TypeError past the end (-1000 here)."""
+    n_ok = 0
+    for c in _load('decode_compound.json'):
+        data = base64.b64decode(c['in_b64'])
+        out = _oracle.decode(data, dictionary=_inputs.resolve(c['dict']))
+        if 'error' not in c:
+            assert not isinstance(out, int) and hashlib.sha256(out).hexdigest() == c['sha256'], c
+            n_ok += 1
+        elif c['error'].startswith('Brotli error code: '):
+            assert out == int(c['error'].split(': ')[1]), (c, out)
+        else:
+            assert 'subarray' in c['error'] and out == -1000, (c, out)
+    assert n_ok > 100
