@@ -8,6 +8,9 @@ resident in HBM when the timed region starts):
                 numbers are quoted on.
   c3            C3: 1024 x 256 KiB WOFF2-transformed-glyf-like buffers per GPU, q11, FONT.
   c2            C2: one 64 MiB enwik-style buffer, q11 GENERIC (one stream: replicas at N > 1).
+  c5            C5's shape per GPU: one stream streamed through BrotliEncoder.update() in 1 MiB
+                chunks (history window carried on the device), q9 lgwin 24 TEXT, then decoded
+                (64 MiB by default: --size for more).
 A step encodes the batch (mib_ctx_encode: packed compressed streams in HBM), gathers the
 compressed shards to rank 0 over RCCL (N > 1, c3/c4; the only collective)
 and decodes them back (mib_ctx_decode) into HBM.  The round trip is checked bit-exact on
@@ -48,6 +51,9 @@ WORKLOADS = {
     'c4': (1024, MIB, 0, 2000, 'enwik'),
     'c3': (1024, 256 * 1024, 2, 1000, 'glyf'),
     'c2': (1, 64 * MIB, 0, 2, 'enwik'),
+    # C5's per-GPU stream, shortened (the single-stream decode is the slow half): BrotliEncoder
+    # .update() in 1 MiB chunks, q9 lgwin 24, then one decode of the whole stream
+    'c5': (1, 64 * MIB, 1, 5000, 'enwik'),
 }
 
 
@@ -186,9 +192,75 @@ def load_traffic(kernel):
         return None
 
 
+def run_stream(args, rank, world, local):
+    """C5 leg: host chunks through the streaming encoder (PCIe inside: this is the API the
+    reference exposes), then the HIP decoder on the whole stream; both timed."""
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+    import brotli_amd
+    size = args.size if args.size > 0 else WORKLOADS['c5'][1]
+    q = 9 if args.quality == 11 else args.quality
+    lg = 24 if args.lgwin == 22 else args.lgwin
+    data = bytes(datagen_device(size, 5000 + rank, dev).cpu().numpy().tobytes())
+    opts = {'quality': q, 'lgwin': lg, 'mode': 1}
+    step = MIB
+
+    def enc():
+        e = brotli_amd.BrotliEncoder(opts)
+        parts = [e.update(data[p:p + step]) for p in range(0, size, step)]
+        parts.append(e.finish())
+        return b''.join(parts)
+    for _ in range(max(1, args.warmup)):
+        stream = enc()
+    if brotli_amd.brotliDecode(stream) != data:
+        raise SystemExit('c5 round trip FAILED')
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        stream = enc()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        out = brotli_amd.brotliDecode(stream)
+    t2 = time.perf_counter()
+    assert out == data
+    te, td = (t1 - t0) / args.steps, (t2 - t1) / args.steps
+    dt = te + td
+    if world > 1:
+        t = torch.tensor([dt, te, td], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, te, td = (float(x) for x in t.tolist())
+    if rank == 0:
+        mb = world * size / 1e6
+        print(json.dumps({
+            'metric': 'encode+decode MB/s at q11 lgwin=22', 'value': round(mb / dt, 3), 'unit': 'MB/s',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt * 1e3, 3),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+            'config': {'workload': 'C5 per GPU: one %d B enwik-style stream, BrotliEncoder.update() in 1 MiB host '
+                                   'chunks, q%d lgwin%d TEXT, then brotliDecode of the stream (host buffers: PCIe '
+                                   'included)' % (size, q, lg), 'name': 'c5', 'bytes_per_stream': size,
+                       'quality': q, 'lgwin': lg, 'parallelism': 'replicas%d' % world},
+            'encode_MBps': round(mb / te, 3), 'decode_MBps': round(mb / td, 3),
+            'compressed_ratio': round(len(stream) / size, 5), 'roofline': None, 'cpu_baseline': None}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def datagen_device(total, seed, dev):
+    from brotli_amd import datagen
+    return datagen.enwik_device(total, seed, dev)
+
+
 def main():
     args = parse()
     wl = args.workload
+    if wl == 'c5':
+        return run_stream(args, int(os.environ.get('RANK', '0')), int(os.environ.get('WORLD_SIZE', '1')),
+                          int(os.environ.get('LOCAL_RANK', '0')))
     k0, size0, mode, _, gen = WORKLOADS[wl]
     k = args.streams if args.streams > 0 else k0
     size = args.size if args.size > 0 else size0

@@ -25,7 +25,12 @@ constexpr int kLongCopy = 200;                // copies longer than this are tak
 constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
 constexpr uint32_t kHashBits = 17;            // hashBytes4 (match.ts:162-172)
 constexpr uint32_t kInvalidKey = 1u << kHashBits;   // (within a stream group) positions without 4 bytes
-constexpr int kGroupKeyBits = 6;              // sort key = stream group (<= 64 groups) << 18 | hash or invalid
+constexpr int kGroupKeyBits = 6;
+// Streaming history (BrotliEncoder across update() calls): per encoder, for every hash bucket
+// the stream positions of its kHistWays most recent earlier occurrences, newest first
+// (the reference keeps a hash chain over its ring, hash-chains.ts / encode.ts:354-374).
+constexpr int kHistWays = 16;
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;              // sort key = stream group (<= 64 groups) << 18 | hash or invalid
 constexpr int kHdrBytes = 2048;               // metablock header: block-switch codes, context maps (not the trees)
 constexpr int kTreeBytes = 1024;              // one serialised prefix code
 constexpr int kLitCtx = 64;                   // literal contexts (RFC 7932 section 7.1)
@@ -60,6 +65,10 @@ struct Job {                // one stream (or streaming chunk) to encode
   int32_t dc_in[4];         // the decoder's distance ring at the start (streaming continues it)
   uint32_t prev_bytes;      // the two bytes before data[0] (streaming: the previous chunk's tail), p1 | p2 << 8
   int32_t dc_out[4];        // and after the last command
+  uint32_t hist;            // streaming: bytes of the stream before data[0] that copies may reach
+  uint32_t abs_base;        // streaming: stream position of data[0] (mod 2^32)
+  uint32_t *hist_tab;       // streaming: the encoder's bucket table of earlier positions, or null
+  uint32_t pad_;
   uint64_t out_off;         // byte offset of its scratch output slice
   uint64_t out_cap;
   uint64_t total_bits;      // written by offsets / stored
@@ -332,8 +341,10 @@ struct ItemMap {
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals);
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
-                         const uint32_t *svals, uint32_t total, int depth, uint32_t *matches);
+                         const uint32_t *svals, uint32_t total, int depth, bool hist, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
+void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
+                        const uint32_t *svals, uint32_t total);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                const uint32_t *matches, uint64_t *choice);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);

@@ -60,6 +60,7 @@ __device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, 
   for (uint32_t i = 0; i < avail && i < 8 * kPreW; i++) o[i >> 3] |= (uint64_t)p[i] << (8 * (i & 7));
 }
 
+template <bool kHist>   // streaming chunks with a history table (a separate build of the walk)
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
                                                              const uint32_t *sorted_vals, uint32_t total, int depth,
                                                              uint32_t *matches) {
@@ -98,59 +99,168 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     const uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
     const uint32_t limit = seg_end - p;   // copies never cross a parse segment
     const uint8_t *cur = jb.data + p;
-    const uint64_t mine0 = spre[0][me];
     uint32_t best = 3;
     uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
-    const int dmax = min(depth, kBack);
-    for (int t = 1; t <= dmax; t++) {
-      const int e = me - t;
-      if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
-      const uint32_t d = g - spos[e];
-      if (d > max_dist || best >= limit) break;
-      const uint64_t x0 = mine0 ^ spre[0][e];
-      uint32_t len;
-      if (x0) {
-        len = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;
-        if (len <= best) continue;
+    if constexpr (!kHist) {
+      const uint64_t mine0 = spre[0][me];
+      const int dmax = min(depth, kBack);
+      for (int t = 1; t <= dmax; t++) {
+        const int e = me - t;
+        if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
+        const uint32_t d = g - spos[e];
+        if (d > max_dist || best >= limit) break;
+        const uint64_t x0 = mine0 ^ spre[0][e];
+        uint32_t len;
+        if (x0) {
+          len = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;
+          if (len <= best) continue;
       } else {
-        // a candidate can only beat `best` if it matches byte `best` too
-        if (best < 8 * kPreW) {
-          const uint32_t sh = 8 * (best & 7);
-          if (((spre[best >> 3][me] ^ spre[best >> 3][e]) >> sh) & 0xFF) continue;
-        } else if (cur[best] != (cur - d)[best]) {
-          continue;
-        }
-        len = 8 * kPreW;
+          // a candidate can only beat `best` if it matches byte `best` too
+          if (best < 8 * kPreW) {
+            const uint32_t sh = 8 * (best & 7);
+            if (((spre[best >> 3][me] ^ spre[best >> 3][e]) >> sh) & 0xFF) continue;
+          } else if (cur[best] != (cur - d)[best]) {
+            continue;
+          }
+          len = 8 * kPreW;
 #pragma unroll
-        for (int w = 1; w < kPreW; w++) {
-          const uint64_t x = spre[w][me] ^ spre[w][e];
-          if (x) {
-            len = 8 * w + ((uint32_t)(__ffsll((unsigned long long)x) - 1) >> 3);
-            break;
+          for (int w = 1; w < kPreW; w++) {
+            const uint64_t x = spre[w][me] ^ spre[w][e];
+            if (x) {
+              len = 8 * w + ((uint32_t)(__ffsll((unsigned long long)x) - 1) >> 3);
+              break;
+            }
+          }
+          if (len == 8 * kPreW) {
+            // measured up to the saturation length: the parse measures longer copies itself
+            const uint32_t lim = min(limit, kMatchLenSat);
+            if (lim > len) len += match_len(cur + len, (cur - d) + len, lim - len);
           }
         }
-        if (len == 8 * kPreW) {
-          // measured up to the saturation length: the parse measures longer copies itself
+        len = min(len, limit);
+        if (len > best) {
+          best = len;
+          if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
+            for (int q = 1; q < kMaxMatches; q++) local[q - 1] = local[q];
+            cnt--;
+          }
+          local[cnt++] = pack_match(d, len);
+          if (len >= limit || len >= kMatchLenSat) break;   // the parse measures a long copy itself
+        }
+      }
+      } else {
+      const uint64_t mine0 = spre[0][me];
+      // a candidate at distance d measured to len: the staircase keeps strictly longer ones;
+      // DONE: no longer candidate can matter (the parse measures a long copy itself)
+#define TAKE(d_, len_, DONE)                                               \
+    do {                                                                     \
+      const uint32_t l_ = min((len_), limit);                                \
+      if (l_ > best) {                                                       \
+        best = l_;                                                           \
+        if (cnt == kMaxMatches) {                                            \
+          for (int q = 1; q < kMaxMatches; q++) local[q - 1] = local[q];     \
+          cnt--;                                                             \
+        }                                                                    \
+        local[cnt++] = pack_match((d_), l_);                                 \
+        if (l_ >= limit || l_ >= kMatchLenSat) DONE;                         \
+      }                                                                      \
+    } while (0)
+      const int dmax = min(depth, kBack);
+      int t = 1;
+      bool stop = false;
+      for (; t <= dmax; t++) {
+        const int e = me - t;
+        if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
+        const uint32_t d = g - spos[e];
+        if (d > max_dist || best >= limit) {
+          stop = true;
+          break;
+        }
+        const uint64_t x0 = mine0 ^ spre[0][e];
+        uint32_t len;
+        if (x0) {
+          len = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;
+          if (len <= best) continue;
+        } else {
+          // a candidate can only beat `best` if it matches byte `best` too
+          if (best < 8 * kPreW) {
+            const uint32_t sh = 8 * (best & 7);
+            if (((spre[best >> 3][me] ^ spre[best >> 3][e]) >> sh) & 0xFF) continue;
+          } else if (cur[best] != (cur - d)[best]) {
+            continue;
+          }
+          len = 8 * kPreW;
+#pragma unroll
+          for (int w = 1; w < kPreW; w++) {
+            const uint64_t x = spre[w][me] ^ spre[w][e];
+            if (x) {
+              len = 8 * w + ((uint32_t)(__ffsll((unsigned long long)x) - 1) >> 3);
+              break;
+            }
+          }
+          if (len == 8 * kPreW) {
+            // measured up to the saturation length: the parse measures longer copies itself
+            const uint32_t lim = min(limit, kMatchLenSat);
+            if (lim > len) len += match_len(cur + len, (cur - d) + len, lim - len);
+          }
+        }
+        TAKE(d, len, { stop = true; break; });
+        if (stop) break;
+      }
+      // streaming: then the bucket's occurrences before this chunk (farther, newest first)
+      if (kHist && jb.hist_tab && !stop && t <= dmax) {
+        const uint32_t *slot = jb.hist_tab + (size_t)(key & ((1u << kHashBits) - 1)) * kHistWays;
+        const uint32_t A = jb.abs_base + p;
+        const uint32_t reach = min(max_dist, p + jb.hist);
+        for (int k = 0; k < kHistWays && t <= dmax && best < limit; k++, t++) {
+          const uint32_t c = slot[k];
+          if (c == kNoPos) break;
+          const uint32_t d = A - c;
+          if (d == 0 || d > reach) break;
+          const uint8_t *cand = cur - d;
+          if (cur[best] != cand[best]) continue;
           const uint32_t lim = min(limit, kMatchLenSat);
-          if (lim > len) len += match_len(cur + len, (cur - d) + len, lim - len);
+          bool fin = false;
+          TAKE(d, match_len(cur, cand, lim), fin = true);
+          if (fin) break;
         }
       }
-      len = min(len, limit);
-      if (len > best) {
-        best = len;
-        if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
-          for (int q = 1; q < kMaxMatches; q++) local[q - 1] = local[q];
-          cnt--;
-        }
-        local[cnt++] = pack_match(d, len);
-        if (len >= limit || len >= kMatchLenSat) break;   // the parse measures a long copy itself
-      }
+#undef TAKE
     }
     // a match word is never 0 (length >= 4): the unused tail entries mark the count
     *reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec) = make_uint4(local[0], local[1], local[2], local[3]);
     return;
   }
   *reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec) = make_uint4(0u, 0u, 0u, 0u);   // no candidates
+}
+
+// ---------------------------------------------------------------- streaming history update
+// After a chunk's matches: every bucket the chunk touched gets its newest kHistWays stream
+// positions (this chunk's, from the end of its sorted run, then the older table entries).
+// The thread at a run's end owns the bucket: no two threads write one slot.
+__global__ void hist_update_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
+                                   const uint32_t *sorted_vals, uint32_t total) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= total) return;
+  const uint32_t key = sorted_keys[r];
+  if (key & kInvalidKey) return;
+  const uint32_t g = sorted_vals[r];
+  const uint32_t j = pos_job[g >> kSegBits];
+  const Job &jb = jobs[j];
+  if (!jb.hist_tab) return;
+  if (r + 1 < total && sorted_keys[r + 1] == key && pos_job[sorted_vals[r + 1] >> kSegBits] == j) return;   // not the run's end
+  uint32_t *slot = jb.hist_tab + (size_t)(key & ((1u << kHashBits) - 1)) * kHistWays;
+  uint32_t nw[kHistWays];
+  int m = 0;
+  for (uint32_t q = r; m < kHistWays; q--) {
+    const uint32_t gq = sorted_vals[q];
+    nw[m++] = jb.abs_base + (gq - jb.pos_base);
+    if (q == 0 || sorted_keys[q - 1] != key || sorted_vals[q - 1] < jb.pos_base) break;
+  }
+  uint32_t old[kHistWays];
+  for (int k = 0; k < kHistWays; k++) old[k] = slot[k];
+  for (int k = m; k < kHistWays; k++) nw[k] = old[k - m];
+  for (int k = 0; k < kHistWays; k++) slot[k] = nw[k];
 }
 
 // ---------------------------------------------------------------- literal cost model per stream
@@ -173,9 +283,17 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, keys, vals);
 }
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
-                         const uint32_t *svals, uint32_t total, int depth, uint32_t *matches) {
-  hipLaunchKernelGGL(find_matches_kernel, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, pos_job, skeys, svals,
-                     total, depth, matches);
+                         const uint32_t *svals, uint32_t total, int depth, bool hist, uint32_t *matches) {
+  if (hist)
+    hipLaunchKernelGGL(find_matches_kernel<true>, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, pos_job, skeys,
+                       svals, total, depth, matches);
+  else
+    hipLaunchKernelGGL(find_matches_kernel<false>, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, pos_job, skeys,
+                       svals, total, depth, matches);
+}
+void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
+                        const uint32_t *svals, uint32_t total) {
+  hipLaunchKernelGGL(hist_update_kernel, dim3((total + 255) / 256), dim3(256), 0, st, jobs, pos_job, skeys, svals, total);
 }
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h) {
   hipLaunchKernelGGL(lit_histo_kernel, dim3(nsegs), dim3(256), 0, st, jobs, segs, lit_h);

@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <vector>
 
 #include "enc_common.h"
@@ -122,6 +123,9 @@ struct StreamDesc {
   uint32_t final_;
   int32_t dc[4];
   uint32_t prev_bytes;   // p1 | p2 << 8 before data[0] (streaming)
+  uint32_t hist;         // streaming: history bytes before data[0] (device-resident, contiguous)
+  uint32_t abs_base;     // streaming: stream position of data[0]
+  uint32_t *hist_tab;    // streaming: the encoder's bucket table (null: none)
 };
 
 struct Params {
@@ -149,6 +153,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   std::vector<Mb> mbs;
   std::vector<uint32_t> seg_job;   // per 64 KiB of global positions: its stream
   uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0;
+  bool any_hist = false;
   for (size_t j = 0; j < k; j++) {
     Job &jb = jobs[j];
     memset(&jb, 0, sizeof(jb));
@@ -163,6 +168,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.final_ = sd[j].final_;
     for (int q = 0; q < 4; q++) jb.dc_in[q] = jb.dc_out[q] = sd[j].dc[q];
     jb.prev_bytes = sd[j].prev_bytes;
+    jb.hist = sd[j].hist;
+    jb.abs_base = sd[j].abs_base;
+    jb.hist_tab = sd[j].hist_tab;
+    if (jb.hist_tab) any_hist = true;
     jb.pos_base = (uint32_t)pos_total;
     jb.seg_base = (uint32_t)segs.size();
     jb.mb_base = (uint32_t)mbs.size();
@@ -281,7 +290,8 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, key_bits, st));
     tm.stop();
     tm.start("find_matches");
-    launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, matches);
+    launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, any_hist, matches);
+    if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
     tm.stop();
     tm.start("lit_histo");
     launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
@@ -399,6 +409,9 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
   d.dc[2] = 15;
   d.dc[3] = 16;
   d.prev_bytes = 0;
+  d.hist = 0;
+  d.abs_base = 0;
+  d.hist_tab = nullptr;
   if (!one_shot) {
     d.hdr_lgwin = (uint32_t)prm.lgwin;
   } else if (n == 0) {
@@ -422,14 +435,24 @@ uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096; }
 
 struct mib_encoder {
   mib_enc_opts opts;
-  std::vector<uint8_t> pending;
+  std::vector<uint8_t> pending;   // input not yet handed to the device
   bool started = false;
   bool finished = false;
   int32_t dc[4] = {4, 11, 15, 16};
-  uint32_t prev_bytes = 0;   // the last two bytes handed to the engine (literal contexts)
-  uint64_t block = 1 << 16;
+  uint32_t prev_bytes = 0;        // the last two bytes handed to the engine (literal contexts)
+  uint64_t block = 1 << 16;       // the reference's 2^lgblock (enc-constants.ts:129-147)
+  uint64_t chunk = 8ull << 20;    // input per device encode: whole blocks, at least this much
+  // device state (the default context's device): the window of history plus the chunk,
+  // ping-ponged so the next chunk's history is one device copy; the bucket table of earlier
+  // positions; the output buffer
+  int device = -1;
+  uint8_t *buf[2] = {nullptr, nullptr};
+  uint64_t buf_cap = 0;
+  int cur = 0;
+  uint64_t hist = 0;              // history bytes at buf[cur][0, hist)
+  uint64_t abs = 0;               // stream bytes encoded so far
+  uint32_t *tab = nullptr;
 };
-
 extern "C" {
 
 void mib_encode_ws_free(void *p) {
@@ -460,8 +483,7 @@ struct DefaultLock {   // the default context serves one host call at a time (ru
   ~DefaultLock() { mib_default_lock(0); }
 };
 
-static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status,
-                       mib_encoder *streaming, bool final_) {
+static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status) {
   DefaultLock use;
   mib_ctx *c = mib_default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
@@ -484,18 +506,9 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
   for (size_t i = 0; i < k; i++)
     if (in[i].size) hipMemcpyAsync(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice, st);
   std::vector<StreamDesc> sd(k);
-  for (size_t i = 0; i < k; i++) {
-    fill_desc(sd[i], d_in + ioff[i], in[i].size, prm, streaming == nullptr);
-    if (streaming) {
-      sd[i].hdr_lgwin = streaming->started ? 0 : (uint32_t)prm.lgwin;
-      sd[i].final_ = final_ ? 1 : 0;
-      for (int q = 0; q < 4; q++) sd[i].dc[q] = streaming->dc[q];
-      sd[i].prev_bytes = streaming->prev_bytes;
-    }
-  }
+  for (size_t i = 0; i < k; i++) fill_desc(sd[i], d_in + ioff[i], in[i].size, prm, true);
   std::vector<uint64_t> ooff(k + 1, 0);
-  std::vector<int32_t> dcs(4 * std::max<size_t>(k, 1));
-  int rc = encode_streams(c, o, sd.data(), k, d_out, cap, ooff.data(), (int32_t(*)[4])dcs.data(), st);
+  int rc = encode_streams(c, o, sd.data(), k, d_out, cap, ooff.data(), nullptr, st);
   if (rc == 0) {
     std::vector<uint8_t> host(ooff[k]);
     if (ooff[k] && hipMemcpy(host.data(), d_out, ooff[k], hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
@@ -506,11 +519,97 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
       if (len) memcpy(out[i].data, host.data() + ooff[i], len);
       if (status) status[i] = 0;
     }
-    if (streaming && k == 1)
-      for (int q = 0; q < 4; q++) streaming->dc[q] = dcs[q];
   }
   hipFree(d_out);
   hipFree(d_in);
+  return rc;
+}
+
+// BrotliEncoder on the device: encoders es[0..k) (same options) each encode ns[i] bytes of
+// their pending input in ONE launch sequence.  A chunk's matches reach the encoder's history
+// (the last 2^lgwin bytes, kept in HBM) through the sorted chunk and the bucket table, so the
+// stream is what a one-shot encode with the same window would produce, cut into chunks.
+static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *finals, size_t k,
+                       std::vector<uint8_t> *accs) {
+  DefaultLock use;
+  mib_ctx *c = mib_default_ctx();
+  if (!c) return MIB_E_NO_DEVICE;
+  const int dev = mib_ctx_device_of(c);
+  CK(hipSetDevice(dev));
+  hipStream_t st = (hipStream_t)mib_ctx_stream_of(c);
+  const Params prm = make_params(&es[0]->opts);
+  const uint64_t window = 1ull << prm.lgwin;
+  uint64_t cap = 0;
+  for (size_t i = 0; i < k; i++) {
+    mib_encoder *e = es[i];
+    if (e->device >= 0 && e->device != dev) return MIB_E_INVALID_ARG;
+    const uint64_t need = window + std::max<uint64_t>(ns[i], e->chunk) + 256;
+    if (e->buf_cap < need) {   // (first use, or a final chunk larger than the others)
+      uint8_t *nb[2] = {nullptr, nullptr};
+      for (int b = 0; b < 2; b++)
+        if (hipMalloc(&nb[b], need) != hipSuccess) {
+          if (nb[0]) hipFree(nb[0]);
+          return MIB_E_OUT_OF_MEMORY;
+        }
+      if (e->hist) CK(hipMemcpyAsync(nb[0], e->buf[e->cur], e->hist, hipMemcpyDeviceToDevice, st));
+      CK(hipStreamSynchronize(st));
+      for (int b = 0; b < 2; b++)
+        if (e->buf[b]) hipFree(e->buf[b]);
+      e->buf[0] = nb[0];
+      e->buf[1] = nb[1];
+      e->cur = 0;
+      e->buf_cap = need;
+    }
+    if (!e->tab) {
+      if (hipMalloc(&e->tab, sizeof(uint32_t) * kHistWays << kHashBits) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+      CK(hipMemsetAsync(e->tab, 0xFF, sizeof(uint32_t) * kHistWays << kHashBits, st));
+    }
+    e->device = dev;
+    cap += out_bound(ns[i]);
+  }
+  uint8_t *d_out = nullptr;
+  if (hipMalloc(&d_out, cap + 64) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  std::vector<StreamDesc> sd(k);
+  for (size_t i = 0; i < k; i++) {
+    mib_encoder *e = es[i];
+    uint8_t *base = e->buf[e->cur] + e->hist;
+    if (ns[i]) CK(hipMemcpyAsync(base, e->pending.data(), ns[i], hipMemcpyHostToDevice, st));
+    CK(hipMemsetAsync(base + ns[i], 0, 64, st));
+    fill_desc(sd[i], base, ns[i], prm, false);
+    sd[i].hdr_lgwin = e->started ? 0 : (uint32_t)prm.lgwin;
+    sd[i].final_ = finals[i] ? 1 : 0;
+    for (int q = 0; q < 4; q++) sd[i].dc[q] = e->dc[q];
+    sd[i].prev_bytes = e->prev_bytes;
+    sd[i].hist = (uint32_t)e->hist;
+    sd[i].abs_base = (uint32_t)e->abs;
+    sd[i].hist_tab = e->tab;
+  }
+  std::vector<uint64_t> ooff(k + 1, 0);
+  std::vector<int32_t> dcs(4 * std::max<size_t>(k, 1));
+  int rc = encode_streams(c, &es[0]->opts, sd.data(), k, d_out, cap, ooff.data(), (int32_t(*)[4])dcs.data(), st);
+  if (rc == 0) {
+    std::vector<uint8_t> host(ooff[k]);
+    if (ooff[k] && hipMemcpy(host.data(), d_out, ooff[k], hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
+    for (size_t i = 0; rc == 0 && i < k; i++) {
+      mib_encoder *e = es[i];
+      accs[i].insert(accs[i].end(), host.data() + ooff[i], host.data() + ooff[i + 1]);
+      for (int q = 0; q < 4; q++) e->dc[q] = dcs[4 * i + q];
+      const uint64_t n = ns[i];
+      for (uint64_t q = n - std::min<uint64_t>(n, 2); q < n; q++)   // the chunk's last bytes
+        e->prev_bytes = ((e->prev_bytes << 8) & 0xFF00) | e->pending[q];
+      e->started = true;
+      // the next chunk's history: the last 2^lgwin bytes, moved to the other buffer's front
+      const uint64_t keep = std::min<uint64_t>(window, e->hist + n);
+      if (keep)
+        CK(hipMemcpyAsync(e->buf[e->cur ^ 1], e->buf[e->cur] + e->hist + n - keep, keep, hipMemcpyDeviceToDevice, st));
+      e->cur ^= 1;
+      e->hist = keep;
+      e->abs += n;
+      e->pending.erase(e->pending.begin(), e->pending.begin() + (ptrdiff_t)n);
+    }
+    CK(hipStreamSynchronize(st));
+  }
+  hipFree(d_out);
   return rc;
 }
 
@@ -520,7 +619,7 @@ int mib_encode(const uint8_t *in, size_t n, const mib_enc_opts *o, mib_buf *out)
   out->size = 0;
   if (n >= (1ull << 31)) return MIB_E_INVALID_ARG;
   mib_span s{in, n};
-  return encode_host(&s, 1, o, out, nullptr, nullptr, true);
+  return encode_host(&s, 1, o, out, nullptr);
 }
 
 int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status) {
@@ -532,12 +631,14 @@ int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_bu
     if ((!in[i].data && in[i].size) || in[i].size >= (1ull << 31)) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
-  return encode_host(in, k, o, out, status, nullptr, true);
+  return encode_host(in, k, o, out, status);
 }
 
-// BrotliEncoder (encode.ts:290-409): input is cut into blocks of 2^lgblock (computeLgBlock,
-// enc-constants.ts:129-147); each full block becomes metablocks ending in a byte-aligning
-// empty metadata block, so update() can return whole bytes.  The distance cache carries over.
+// BrotliEncoder (encode.ts:290-409): input is taken in whole blocks of 2^lgblock
+// (computeLgBlock, enc-constants.ts:129-147), at least `chunk` bytes per device encode; each
+// encode ends in a byte-aligning empty metadata block so update() returns whole bytes.  The
+// distance ring, the literal context and the 2^lgwin window of history carry over (the
+// reference's ring, encode.ts:312-374, without Bug D's overwrite).
 mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
   mib_encoder *e = new mib_encoder();
   if (o) e->opts = *o;
@@ -551,41 +652,74 @@ mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
     if (prm.quality >= 9 && prm.lgwin > lgblock) lgblock = std::min(18, prm.lgwin);
   }
   e->block = 1ull << lgblock;
+  e->chunk = std::max<uint64_t>(e->block, e->chunk);
   return e;
 }
 
-static int encoder_emit(mib_encoder *e, const uint8_t *p, size_t n, bool final_, std::vector<uint8_t> &acc) {
-  mib_span s{p, n};
-  mib_buf b{nullptr, 0};
-  int st = 0;
-  int rc = encode_host(&s, 1, &e->opts, &b, &st, e, final_);
-  if (rc) return rc;
-  acc.insert(acc.end(), b.data, b.data + b.size);
-  mib_buf_free(&b);
-  e->started = true;
-  for (size_t i = 0; i < n && i < 2; i++)   // shift in the chunk's last bytes
-    e->prev_bytes = ((e->prev_bytes << 8) & 0xFF00) | p[n - (n < 2 ? n : 2) + i];
+static int take_acc(std::vector<uint8_t> &acc, mib_buf *out) {
+  out->data = (uint8_t *)malloc(acc.size() ? acc.size() : 1);
+  if (!out->data) return MIB_E_OUT_OF_MEMORY;
+  out->size = acc.size();
+  if (acc.size()) memcpy(out->data, acc.data(), acc.size());
+  return 0;
+}
+
+static bool same_opts(const mib_enc_opts &a, const mib_enc_opts &b) {
+  const Params x = make_params(&a), y = make_params(&b);
+  return x.quality == y.quality && x.lgwin == y.lgwin && x.npostfix == y.npostfix && x.ndirect == y.ndirect;
+}
+
+int mib_encoder_update_batch(mib_encoder *const *es, const mib_span *in, size_t k, mib_buf *out) {
+  if (k && (!es || !in || !out)) return MIB_E_INVALID_ARG;
+  for (size_t i = 0; i < k; i++) {
+    out[i].data = nullptr;
+    out[i].size = 0;
+    if (!es[i] || es[i]->finished || (!in[i].data && in[i].size)) return MIB_E_INVALID_ARG;
+    for (size_t j = 0; j < i; j++)
+      if (es[j] == es[i]) return MIB_E_INVALID_ARG;
+  }
+  std::vector<std::vector<uint8_t>> accs(k);
+  std::vector<mib_encoder *> run;
+  std::vector<uint64_t> ns;
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < k; i++) {
+    mib_encoder *e = es[i];
+    e->pending.insert(e->pending.end(), in[i].data, in[i].data + in[i].size);
+  }
+  // encoders with a full chunk pending, grouped by options, one launch sequence per group
+  std::vector<bool> done(k, false);
+  for (size_t i = 0; i < k; i++) {
+    if (done[i]) continue;
+    run.clear();
+    ns.clear();
+    idx.clear();
+    for (size_t j = i; j < k; j++) {
+      mib_encoder *e = es[j];
+      if (done[j] || !same_opts(e->opts, es[i]->opts)) continue;
+      done[j] = true;
+      if (e->pending.size() < e->chunk) continue;
+      run.push_back(e);
+      ns.push_back(e->pending.size() / e->block * e->block);
+      idx.push_back(j);
+    }
+    if (run.empty()) continue;
+    std::vector<std::vector<uint8_t>> acc(run.size());
+    std::unique_ptr<bool[]> fin(new bool[run.size()]());
+    int rc = encoder_run(run.data(), ns.data(), fin.get(), run.size(), acc.data());
+    if (rc) return rc;
+    for (size_t q = 0; q < run.size(); q++) accs[idx[q]].swap(acc[q]);
+  }
+  for (size_t i = 0; i < k; i++) {
+    int rc = take_acc(accs[i], &out[i]);
+    if (rc) return rc;
+  }
   return 0;
 }
 
 int mib_encoder_update(mib_encoder *e, const uint8_t *in, size_t n, mib_buf *out) {
   if (!e || !out || (!in && n)) return MIB_E_INVALID_ARG;
-  out->data = nullptr;
-  out->size = 0;
-  if (e->finished) return MIB_E_INVALID_ARG;
-  e->pending.insert(e->pending.end(), in, in + n);
-  std::vector<uint8_t> acc;
-  size_t off = 0;
-  while (e->pending.size() - off >= e->block) {
-    int rc = encoder_emit(e, e->pending.data() + off, e->block, false, acc);
-    if (rc) return rc;
-    off += e->block;
-  }
-  e->pending.erase(e->pending.begin(), e->pending.begin() + off);
-  out->data = (uint8_t *)malloc(acc.size() ? acc.size() : 1);
-  out->size = acc.size();
-  if (acc.size()) memcpy(out->data, acc.data(), acc.size());
-  return 0;
+  mib_span s{in, n};
+  return mib_encoder_update_batch(&e, &s, 1, out);
 }
 
 int mib_encoder_finish(mib_encoder *e, mib_buf *out) {
@@ -594,17 +728,24 @@ int mib_encoder_finish(mib_encoder *e, mib_buf *out) {
   out->size = 0;
   std::vector<uint8_t> acc;
   if (!e->finished) {
-    int rc = encoder_emit(e, e->pending.data(), e->pending.size(), true, acc);
+    const uint64_t n = e->pending.size();
+    const bool fin = true;
+    int rc = encoder_run(&e, &n, &fin, 1, &acc);
     if (rc) return rc;
-    e->pending.clear();
     e->finished = true;
   }
-  out->data = (uint8_t *)malloc(acc.size() ? acc.size() : 1);
-  out->size = acc.size();
-  if (acc.size()) memcpy(out->data, acc.data(), acc.size());
-  return 0;
+  return take_acc(acc, out);
 }
 
-void mib_encoder_free(mib_encoder *e) { delete e; }
+void mib_encoder_free(mib_encoder *e) {
+  if (!e) return;
+  if (e->device >= 0) {
+    hipSetDevice(e->device);
+    for (int b = 0; b < 2; b++)
+      if (e->buf[b]) hipFree(e->buf[b]);
+    if (e->tab) hipFree(e->tab);
+  }
+  delete e;
+}
 
 }  // extern "C"

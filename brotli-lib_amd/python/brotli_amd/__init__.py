@@ -16,7 +16,7 @@ import ctypes
 import os
 
 __all__ = ['brotliEncode', 'BrotliEncoder', 'brotliDecode', 'brotliDecodedSize', 'EncoderMode', 'BrotliError',
-           'encode_batch', 'decode_batch', 'DeviceContext', 'library_path']
+           'encode_batch', 'decode_batch', 'encoder_update_batch', 'DeviceContext', 'library_path']
 
 _PKG = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 # BROTLI_AMD_LIB: an instrumented build of the same library (timing experiments only)
@@ -87,6 +87,8 @@ def _L():
         lib.mib_encoder_update.argtypes = [ctypes.c_void_p, u8p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
         lib.mib_encoder_finish.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Buf)]
         lib.mib_encoder_free.argtypes = [ctypes.c_void_p]
+        lib.mib_encoder_update_batch.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(_Span), ctypes.c_size_t,
+                                                 ctypes.POINTER(_Buf)]
         lib.mib_encode_batch.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.POINTER(_Opts),
                                          ctypes.POINTER(_Buf), ctypes.POINTER(ctypes.c_int)]
         lib.mib_decode_batch.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.POINTER(_Buf),
@@ -179,6 +181,20 @@ class BrotliEncoder:
         if getattr(self, '_h', None):
             _L().mib_encoder_free(self._h)
             self._h = None
+
+
+def encoder_update_batch(encoders, chunks):
+    """Advance independent BrotliEncoders by one chunk each in one GPU launch sequence;
+    returns each encoder's update() result."""
+    k = len(encoders)
+    keep = [_bytes(b) for b in chunks]
+    hs = (ctypes.c_void_p * k)(*[e._h for e in encoders])
+    spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
+    outs = (_Buf * k)()
+    rc = _L().mib_encoder_update_batch(hs, spans, k, outs)
+    if rc:
+        raise _err(rc)
+    return [_take(outs[i]) for i in range(k)]
 
 
 def brotliDecodedSize(data):

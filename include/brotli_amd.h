@@ -74,12 +74,18 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
 /* brotliDecodedSize (decode.ts:9-11 -> engine.ts:2155-2192): -1 when unknown. */
 int64_t mib_decoded_size(const uint8_t *in, size_t n);
 
-/* BrotliEncoder (encode.ts:290-490): update() returns the newly completed bytes. */
+/* BrotliEncoder (encode.ts:290-490): update() returns the newly completed bytes.  The
+ * encoder keeps its 2^lgwin window of history in HBM, so matches reach across update()
+ * calls; input is encoded in whole 2^lgblock blocks, several MiB per device pass, so
+ * update() may return nothing until enough input has arrived (finish() returns the rest). */
 typedef struct mib_encoder mib_encoder;
 mib_encoder *mib_encoder_new(const mib_enc_opts *o);
 int mib_encoder_update(mib_encoder *e, const uint8_t *in, size_t n, mib_buf *out);
 int mib_encoder_finish(mib_encoder *e, mib_buf *out);
 void mib_encoder_free(mib_encoder *e);
+/* k independent encoders (distinct handles) advance by one chunk each in one launch sequence
+ * (encoders with equal options share it); out[i] is encoder i's update() result. */
+int mib_encoder_update_batch(mib_encoder *const *e, const mib_span *in, size_t k, mib_buf *out);
 
 /* Batches of independent buffers in host memory; one result (and status) per buffer. */
 int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status);
