@@ -250,6 +250,103 @@ static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
   return out;
 }
 
+/* ---- asynchronous batches: the GPU work runs on a libuv worker thread (napi_async_work),
+   the JS thread gets a Promise; the input arrays are held by references until it settles */
+typedef struct {
+  napi_async_work work;
+  napi_deferred deferred;
+  napi_ref *refs;   /* the inputs, alive until complete() */
+  uint32_t k;
+  int decode;       /* 0: encode batch, 1: decode batch */
+  mib_enc_opts o;
+  mib_span *in;
+  mib_buf *res;
+  int *st;
+  int rc;
+} AsyncBatch;
+
+static void async_execute(napi_env env, void *data) {
+  AsyncBatch *a = (AsyncBatch *)data;
+  a->rc = a->decode ? mib_decode_batch(a->in, a->k, a->res, a->st) : mib_encode_batch(a->in, a->k, &a->o, a->res, a->st);
+}
+
+static void async_complete(napi_env env, napi_status status, void *data) {
+  AsyncBatch *a = (AsyncBatch *)data;
+  napi_value out, err;
+  if (a->rc == 0 && status == napi_ok) {
+    napi_create_array_with_length(env, a->k, &out);
+    for (uint32_t i = 0; i < a->k; i++) {
+      napi_value v;
+      if (a->st[i]) {   /* a stream that failed to decode: its Error, in its slot */
+        napi_value msg;
+        napi_create_string_utf8(env, mib_strerror(a->st[i]), NAPI_AUTO_LENGTH, &msg);
+        napi_create_error(env, NULL, msg, &v);
+        mib_buf_free(&a->res[i]);
+      } else {
+        void *dst;
+        napi_create_buffer_copy(env, a->res[i].size, a->res[i].size ? (const void *)a->res[i].data : (const void *)"", &dst, &v);
+        mib_buf_free(&a->res[i]);
+      }
+      napi_set_element(env, out, i, v);
+    }
+    napi_resolve_deferred(env, a->deferred, out);
+  } else {
+    napi_value msg;
+    napi_create_string_utf8(env, mib_strerror(a->rc ? a->rc : MIB_E_NO_DEVICE), NAPI_AUTO_LENGTH, &msg);
+    napi_create_error(env, NULL, msg, &err);
+    napi_reject_deferred(env, a->deferred, err);
+    for (uint32_t i = 0; i < a->k; i++) mib_buf_free(&a->res[i]);
+  }
+  for (uint32_t i = 0; i < a->k; i++) napi_delete_reference(env, a->refs[i]);
+  napi_delete_async_work(env, a->work);
+  free(a->refs), free(a->in), free(a->res), free(a->st), free(a);
+}
+
+/* encodeBatchAsync(inputs, quality, lgwin, mode) / decodeBatchAsync(inputs) -> Promise */
+static napi_value start_async(napi_env env, napi_callback_info info, int decode) {
+  size_t argc = 4;
+  napi_value argv[4], promise, name;
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  bool is_arr = false;
+  uint32_t k = 0;
+  if (argc < 1 || napi_is_array(env, argv[0], &is_arr) != napi_ok || !is_arr) {
+    napi_throw_type_error(env, NULL, "inputs: Uint8Array[]");
+    return NULL;
+  }
+  CHECK(env, napi_get_array_length(env, argv[0], &k));
+  AsyncBatch *a = (AsyncBatch *)calloc(1, sizeof(AsyncBatch));
+  a->k = k;
+  a->decode = decode;
+  mib_enc_opts_default(&a->o);
+  if (!decode) {
+    a->o.quality = get_int(env, argc > 1 ? argv[1] : NULL, a->o.quality);
+    a->o.lgwin = get_int(env, argc > 2 ? argv[2] : NULL, a->o.lgwin);
+    a->o.mode = get_int(env, argc > 3 ? argv[3] : NULL, a->o.mode);
+  }
+  a->in = (mib_span *)calloc(k ? k : 1, sizeof(mib_span));
+  a->res = (mib_buf *)calloc(k ? k : 1, sizeof(mib_buf));
+  a->st = (int *)calloc(k ? k : 1, sizeof(int));
+  a->refs = (napi_ref *)calloc(k ? k : 1, sizeof(napi_ref));
+  for (uint32_t i = 0; i < k; i++) {
+    napi_value e;
+    napi_get_element(env, argv[0], i, &e);
+    if (get_bytes(env, e, &a->in[i].data, &a->in[i].size)) {
+      for (uint32_t q = 0; q < i; q++) napi_delete_reference(env, a->refs[q]);
+      free(a->refs), free(a->in), free(a->res), free(a->st), free(a);
+      napi_throw_type_error(env, NULL, "every input must be a Uint8Array");
+      return NULL;
+    }
+    napi_create_reference(env, e, 1, &a->refs[i]);
+  }
+  CHECK(env, napi_create_promise(env, &a->deferred, &promise));
+  napi_create_string_utf8(env, decode ? "brotli_amd.decodeBatch" : "brotli_amd.encodeBatch", NAPI_AUTO_LENGTH, &name);
+  CHECK(env, napi_create_async_work(env, NULL, name, async_execute, async_complete, a, &a->work));
+  CHECK(env, napi_queue_async_work(env, a->work));
+  return promise;
+}
+static napi_value js_encode_batch_async(napi_env env, napi_callback_info info) { return start_async(env, info, 0); }
+static napi_value js_decode_batch_async(napi_env env, napi_callback_info info) { return start_async(env, info, 1); }
+
 static napi_value init(napi_env env, napi_value exports) {
   napi_property_descriptor props[] = {
       {"encode", 0, js_encode, 0, 0, 0, napi_default, 0},
@@ -259,6 +356,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"encoderUpdate", 0, js_encoder_update, 0, 0, 0, napi_default, 0},
       {"encoderFinish", 0, js_encoder_finish, 0, 0, 0, napi_default, 0},
       {"encodeBatch", 0, js_encode_batch, 0, 0, 0, napi_default, 0},
+      {"encodeBatchAsync", 0, js_encode_batch_async, 0, 0, 0, napi_default, 0},
+      {"decodeBatchAsync", 0, js_decode_batch_async, 0, 0, 0, napi_default, 0},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -76,4 +76,17 @@ function brotliEncodeBatch(inputs, options) {
   return native.encodeBatch(inputs, q, lg, m).map(toU8)
 }
 
-module.exports = { brotliEncode, BrotliEncoder, brotliDecode, brotliDecodedSize, EncoderMode, brotliEncodeBatch }
+// the same, off the JS thread: the GPU work runs on a worker (napi_async_work), a Promise
+// resolves to the outputs (decode: a stream that fails gives its Error in its slot)
+function brotliEncodeBatchAsync(inputs, options) {
+  const [q, lg, m] = clampOptions(options)
+  return native.encodeBatchAsync(inputs, q, lg, m).then((outs) => outs.map(toU8))
+}
+function brotliDecodeBatchAsync(inputs) {
+  return native.decodeBatchAsync(inputs).then((outs) => outs.map((o) => (o instanceof Error ? o : toU8(o))))
+}
+
+module.exports = {
+  brotliEncode, BrotliEncoder, brotliDecode, brotliDecodedSize, EncoderMode,
+  brotliEncodeBatch, brotliEncodeBatchAsync, brotliDecodeBatchAsync,
+}

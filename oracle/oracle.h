@@ -25,6 +25,10 @@ int oracle_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_
 int oracle_encode(const uint8_t *in, size_t n, int quality, int lgwin, int mode,
                   uint8_t **out, size_t *out_n);
 
+/* createHqZopfliBackwardReferences pass 1: every position's findAllMatches list (ref-fixed
+ * binary tree, hash-binary-tree.ts:57-227), flat: i, count, (distance, length) x count. */
+int64_t oracle_bt_matches(const uint8_t *in, size_t n, int lgwin, uint32_t *out, size_t cap);
+
 void oracle_free(void *p);
 
 #ifdef __cplusplus

@@ -36,6 +36,25 @@ def encode(data, quality=11, lgwin=22, mode=0):
     return r
 
 
+def bt_matches(data, lgwin=22):
+    """per-position findAllMatches lists (pass 1 of the q11 parse): [(i, [(distance, length)...])]"""
+    import array
+    cap = 8 * len(data) + 64
+    buf = (ctypes.c_uint32 * cap)()
+    lib().oracle_bt_matches.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+    lib().oracle_bt_matches.restype = ctypes.c_int64
+    w = lib().oracle_bt_matches(data, len(data), lgwin, buf, cap)
+    if w < 0:
+        raise RuntimeError('oracle_bt_matches: output too small')
+    v = array.array('I', bytes(buf)[:4 * w])
+    out, k = [], 0
+    while k < w:
+        i, c = v[k], v[k + 1]
+        out.append((i, [(v[k + 2 + 2 * q], v[k + 3 + 2 * q]) for q in range(c)]))
+        k += 2 + 2 * c
+    return out
+
+
 def peek_size(data):
     return lib().oracle_peek_decoded_size(data, len(data))
 

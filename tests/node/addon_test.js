@@ -135,4 +135,18 @@ for (let i = 0; i < 32; i++) bufs.push(new Uint8Array(text.subarray(i * 1000, i 
 const outs = lib.brotliEncodeBatch(bufs, { quality: 11 })
 for (let i = 0; i < bufs.length; i++) eq(lib.brotliDecode(outs[i]), bufs[i], 'batch ' + i)
 console.log('batch ok')
-console.log('ALL OK')
+
+// asynchronous batches (napi_async_work): the JS thread stays free while the GPU works
+;(async () => {
+  let ticks = 0
+  const timer = setInterval(() => { ticks++ }, 1)
+  const aouts = await lib.brotliEncodeBatchAsync(bufs, { quality: 11 })
+  for (let i = 0; i < bufs.length; i++) eq(aouts[i], outs[i], 'async batch ' + i)
+  const bad = new Uint8Array([0x1b, 0x3f, 0xff, 0xff])
+  const decs = await lib.brotliDecodeBatchAsync([...aouts, bad])
+  clearInterval(timer)
+  for (let i = 0; i < bufs.length; i++) eq(decs[i], bufs[i], 'async decode ' + i)
+  assert.ok(decs[bufs.length] instanceof Error, 'a bad stream gives its Error')
+  console.log('async batch ok, timer ticks while waiting:', ticks)
+  console.log('ALL OK')
+})().catch((e) => { console.error(e); process.exit(1) })

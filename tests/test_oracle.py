@@ -112,3 +112,13 @@ def test_compound_dictionary_matches_reference():
         else:
             assert 'subarray' in c['error'] and out == -1000, (c, out)
     assert n_ok > 100
+
+
+def test_bt_matches_match_reference():
+    """The oracle's binary-tree match finder (hash-binary-tree.ts:57-227, Bug B fixed) gives
+    the reference's per-position match lists (tests/golden/bt_matches.json)."""
+    for c in _load('bt_matches.json'):
+        data = _inputs.resolve(c['input'])
+        got = _oracle.bt_matches(data, c.get('lgwin', 22))
+        exp = [(i, [tuple(m) for m in ms]) for i, ms in c['lists']]
+        assert got == exp, c['input']
