@@ -18,6 +18,13 @@ struct DecJob {
   int64_t result_len;     // out: bytes produced
   int32_t status;         // out: 0, reference error code, or MIB_E_*
   int32_t max_ring_log;   // window bits from the stream header (host peek), sizes scratch
+  // part mode (parts.h): the job is one part of a stream that carries a part index
+  const void *part_entry; // this part's PartEntry (device); null: a whole-stream job
+  const void *next_entry; // the next part's entry, null for the stream's last part
+  const int64_t *ppos;    // the stream's part start positions, [nparts] = its total
+  uint64_t *prog;         // the stream's progress words (zeroed before the launch)
+  int32_t pidx, nparts;
+  int64_t total;          // the stream's decoded size (from the index)
 };
 
 constexpr int kDecodeBlock = 64;                    // one wave per stream

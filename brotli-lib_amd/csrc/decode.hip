@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include "common.h"
+#include "parts.h"
 #define RFC_CONST static __device__ const
 #include "rfc_tables.h"
 
@@ -65,13 +66,16 @@ typedef const __attribute__((address_space(3))) uint16_t LU16;
 
 struct Lds {
   uint8_t win[4160 + 64];    // byteBuffer (4160) + read slack
-  int lens[1080];            // code lengths scratch
+  uint8_t lens[1080];        // code lengths scratch
   uint16_t sorted[1080];
   int32_t cl_table[33];
   int32_t ctx_tree_base[64];
   uint8_t ctx_lut[512];        // the current literal context mode's slice of the RFC lookup table
   uint8_t mtf[256];
   uint16_t ctx_root[2048];     // (lut1[p2] << 8 | p1) -> root of the literal tree (16-bit tables)
+  // part mode (parts.h): the 64 parts before this one -- lane l <-> part pidx - 1 - l: their
+  // output ranges and the progress last acquired from them
+  int part_lo[64], part_hi[64], part_seen[64];
 };
 
 struct Dec {
@@ -107,6 +111,16 @@ struct Dec {
   // compound dictionary
   const uint8_t *cd;
   int cd_total, cd_br_offset, cd_br_length, cd_br_copied, cd_br_index;
+  // input position of win[0] (absolute bit position = (win_base + 2 ho) * 8 - 32 + bo)
+  int64_t win_base;
+  // the current metablock: header bit offset, output position, length (part checks)
+  int64_t mb_bit;
+  int mb_pos, mb_len;
+  // part mode: [part_start, part_end) of the output, progress publishing, the stream's
+  // progress words (part_end = INT_MAX: whole-stream mode)
+  int part, part_start, part_end, pub_next, pidx, cover_lo;
+  uint64_t *prog;
+  const int64_t *ppos;   // the stream's part start positions (+ its total at [nparts])
   Lds *l;
   uint64_t guard, guard_limit;
 };
@@ -117,6 +131,7 @@ struct Dec {
 typedef __attribute__((address_space(3))) Dec DecS;
 #define LANE ((int)threadIdx.x)
 static_assert(sizeof(Lds) + sizeof(Dec) + 2 * kLdsTab <= 163840 / 4, "four streams per CU");
+constexpr uint64_t kPartFailed = ~0ull;   // a part's progress word when it failed
 
 // One stream per workgroup (one wave): the LDS working set lives at file scope, so the hot
 // loop addresses it with constant offsets instead of pointer registers.
@@ -191,6 +206,7 @@ __device__ __noinline__ int read_more_input(DecS &s) {
   }
   wave_sync();
   s.ho = 0;
+  s.win_base += ro;
   uint64_t avail = s.in_len - s.in_off;
   int n = (uint64_t)(4096 - have) < avail ? 4096 - have : (int)avail;
   for (int i = LANE; i < n; i += 64) s.l->win[have + i] = s.in[s.in_off + i];
@@ -232,6 +248,91 @@ __device__ int jump_to_byte_boundary(DecS &s) {
   return 0;
 }
 
+// ---------------------------------------------------------------- part mode (parts.h)
+constexpr int kPartFail = -120;   // internal: the part cannot vouch for its bytes (stream falls back)
+
+__device__ __forceinline__ int64_t abs_bit(const DecS &s) { return (s.win_base + 2 * (int64_t)s.ho) * 8 - 32 + s.bo; }
+
+// position the bit reader at absolute bit `bit` with a fresh 4 KiB window from there
+__device__ int part_seek(DecS &s, int64_t bit) {
+  const int64_t byte0 = (bit >> 3) & ~1ll;
+  if (byte0 < 0 || (uint64_t)byte0 > s.in_len) return kPartFail;
+  s.in_off = (uint64_t)byte0;
+  s.win_base = byte0 - 4096;
+  s.ho = 2048;
+  s.bo = 32;
+  s.acc = 0;
+  s.eos = 0;
+  s.tail = 0;
+  const int r = prepare(s);
+  if (r < 0) return r;
+  s.bo += (int)(bit - 8 * byte0);
+  return 0;
+}
+
+// All output bytes below pos are stored: publish pos (every storing lane drains, one
+// agent-scope release, then the flag -- MI355X_MICROARCH.md "Valid forms").
+__device__ __noinline__ void part_publish(int pos) {
+  DecS &s = *(DecS *)&g_dec;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (LANE == 0) __hip_atomic_store(s.prog + s.pidx, (uint64_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  s.pub_next = pos + (int)kPartPublish;
+}
+__device__ __noinline__ void part_fail() {
+  DecS &s = *(DecS *)&g_dec;
+  if (LANE == 0) __hip_atomic_store(s.prog + s.pidx, kPartFailed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bytes [a, b) of earlier parts (a < b <= part_start) are readable once every part
+// overlapping them has published at least min(b, its end): lane l checks part pidx - 1 - l
+// against the progress this wave last acquired; parts further back are polled directly.
+__device__ __forceinline__ bool part_ready_near(int a, int b, int lo, int hi, int seen, int cover_lo) {
+  const bool ok = hi <= a || lo >= b || seen >= (b < hi ? b : hi);
+  return a >= cover_lo && __all(ok);
+}
+__device__ __noinline__ int part_wait(int a, int b) {
+  DecS &s = *(DecS *)&g_dec;
+  const int lane = LANE, pidx = s.pidx;
+  const int64_t *ppos = s.ppos;
+  const int lo = g_lds.part_lo[lane], hi = g_lds.part_hi[lane];
+  const int cover_lo = s.cover_lo;
+  for (uint32_t spin = 0;; spin++) {
+    const int w = pidx - 1 - lane;
+    const uint64_t v = w >= 0 ? __hip_atomic_load(s.prog + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    if (__any(v == kPartFailed)) return kPartFail;
+    const int seen = (int)(v < 0x7FFFFFFFull ? v : 0x7FFFFFFFull);
+    g_lds.part_seen[lane] = seen;
+    bool ok = hi <= a || lo >= b || seen >= (b < hi ? b : hi);
+    // parts beyond the 64 nearest: polled one by one (lane 0), from the nearest down
+    if (a < cover_lo) {
+      int far = 1;   // 1 ready, 0 not yet, -1 failed
+      if (lane == 0) {
+        for (int q = pidx - 65; q >= 0 && ppos[q + 1] > a; q--) {
+          const int e = (int)ppos[q + 1];
+          const uint64_t pv = __hip_atomic_load(s.prog + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (pv == kPartFailed || (int64_t)pv < (b < e ? b : e)) {
+            far = pv == kPartFailed ? -1 : 0;
+            break;
+          }
+        }
+      }
+      far = __shfl(far, 0);
+      if (far < 0) return kPartFail;
+      ok = ok && far > 0;
+    }
+    if (__all(ok)) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 drops what it held
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      wave_sync();
+      return 0;
+    }
+    if (spin > (1u << 24)) return kPartFail;   // (bounded: a part never waits on a later one)
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 // ---------------------------------------------------------------- Huffman tables (engine.ts:1677-1762)
 __device__ int next_key(int key, int len) {
   int step = 1 << (len - 1);
@@ -246,7 +347,8 @@ __device__ __forceinline__ void replicate(const DecS &s, int32_t *g, int cap, in
     if (i < cap) g[i] = item;
   }
 }
-__device__ int build_table(DecS &s, int32_t *group, int cap, int idx, int root, const int *lens, int nsym) {
+template <class L>
+__device__ int build_table(DecS &s, int32_t *group, int cap, int idx, int root, const L *lens, int nsym) {
   int toff = group[idx];
   int count[16], offset[16];
   for (int i = 0; i < 16; i++) count[i] = offset[i] = 0;
@@ -322,7 +424,7 @@ __device__ __forceinline__ int read_symbol(DecS &s, const int32_t *g, int cap, i
 }
 constexpr int kNoCap = 1 << 30;
 
-__device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, int *lens) {   // engine.ts:305-369
+__device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, uint8_t *lens) {   // engine.ts:305-369
   int sym = 0, prev = 8, repeat = 0, repeat_len = 0, space = 32768;
   int32_t *table = s.l->cl_table;
   if (LANE == 0) table[32] = 0;
@@ -336,7 +438,7 @@ __device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, int *len
     int len = table[p] & 0xFFFF;
     if (len < 16) {
       repeat = 0;
-      if (LANE == 0) lens[sym] = len;
+      if (LANE == 0) lens[sym] = (uint8_t)len;
       sym++;
       if (len) {
         prev = len;
@@ -357,7 +459,7 @@ __device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, int *len
       repeat += bits(s, eb) + 3;
       int delta = repeat - old;
       if (sym + delta > nsym) return ERR(s, -2);
-      for (int k = LANE; k < delta; k += 64) lens[sym + k] = repeat_len;
+      for (int k = LANE; k < delta; k += 64) lens[sym + k] = (uint8_t)repeat_len;
       sym += delta;
       if (repeat_len) space -= delta << (15 - repeat_len);
     }
@@ -370,7 +472,7 @@ __device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, int *len
 }
 
 __device__ int read_huffman_code(DecS &s, int amax, int alimit, int32_t *group, int cap, int idx) {   // :370-470
-  int *lens = s.l->lens;
+  uint8_t *lens = s.l->lens;
   MAYBE_REFILL(s);
   fill16(s);
   int kind = bits(s, 2);
@@ -607,8 +709,12 @@ __device__ int read_next_mb_header(DecS &s) {   // :631-678
     return 0;
   }
   MAYBE_REFILL(s);
+  const int64_t hbit = abs_bit(s);
   int r = decode_mb_length(s);
   if (r < 0) return r;
+  s.mb_bit = hbit;
+  s.mb_pos = s.pos;
+  s.mb_len = s.mbl;
   if (s.mbl == 0 && !s.is_metadata) return 0;
   if (s.is_uncompressed || s.is_metadata) {
     r = jump_to_byte_boundary(s);
@@ -979,6 +1085,8 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
         int trivial = s.trivial_lit_ctx, lit_tree = s.lit_tree_idx;
         const int ring_size = s.ring_size;
         LU8 *clut = (LU8 *)g_lds.ctx_lut;
+        const int part = __builtin_amdgcn_readfirstlane(s.part), part_end = __builtin_amdgcn_readfirstlane(s.part_end);
+        const int pstart = __builtin_amdgcn_readfirstlane(s.part_start), cover_lo = __builtin_amdgcn_readfirstlane(s.cover_lo);
         // The last two output bytes (the literal context) live in registers: reading them
         // back from the ring would wait for every outstanding ring store (vmcnt is in order).
         int c1 = __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 1) & rmask]);
@@ -1106,6 +1214,11 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
             return MIB_E_NO_PROGRESS;
           }
           if (phase == ST_MAIN_LOOP) {   // command (:1080-1152)
+            if (pos >= part_end) {   // part mode: the next part starts here
+              s.running = ST_MAIN_LOOP;
+              break;
+            }
+            if (part && pos >= U(s.pub_next)) part_publish(pos);
             if (stop_at_boundary && guard != guard0) {   // back to the fast loop
               s.running = ST_MAIN_LOOP;
               break;
@@ -1367,6 +1480,14 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
           {   // copy (:1379-1433)
             const int dist = distance, cl = copy_len - j;
             const int src = (pos - dist) & rmask;
+            if (part && src < pstart) {   // the source reaches into earlier parts
+              const int b = U(min(min(src + cl, pos), pstart));
+              if (!part_ready_near(src, b, g_lds.part_lo[lane], g_lds.part_hi[lane], g_lds.part_seen[lane], cover_lo) &&
+                  part_wait(src, b) < 0) {
+                HOT_SAVE();
+                return kPartFail;
+              }
+            }
             if (src + cl < rmask && pos + cl < rmask) {
               int lastv = 0;   // each lane's last copied byte: lanes (cl - 1) & 63, (cl - 2) & 63 end the copy
               // uniform trip counts (lane-dependent loop exits would make the whole loop nest,
@@ -1500,7 +1621,16 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   const int lane = LANE;
   const int rmask = U(rmask_in);
   // positions stay below lim: no fence, flush or wrap inside a command
-  const int lim = U(min(fence_in, rmask));
+  const int lim = U(min(min(fence_in, rmask), s.part_end));
+  // part mode: publishing, and the 64 earlier parts' ranges / acquired progress (lane l)
+  const int part = U(s.part), pstart = U(s.part_start), cover_lo = U(s.cover_lo);
+  int pub_next = U(s.pub_next);
+  int plo = 0, phi = 0, pseen = 0;
+  if (part) {
+    plo = g_lds.part_lo[LANE];
+    phi = g_lds.part_hi[LANE];
+    pseen = g_lds.part_seen[LANE];
+  }
   const int npostfix = U(s.npostfix), ndirect = U(s.ndirect), max_back = U(s.max_back);
   int bo = U(s.bo), ho = U(s.ho), pos = U(s.pos), mbl = U(s.mbl);
   // buf = half-words ho-2 .. ho+1 (acc is its low half); pf = half-word ho+2, in flight
@@ -1594,6 +1724,11 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     FMARK(4);
     // ---- command boundary: a block switch or refill goes to the general loop
     if (mbl <= 0 || cmd_blen == 0 || ho > 2030 - 8) break;
+    if (part && pos >= pub_next) {   // every output byte below pos is stored: publish
+      finish_copy();
+      part_publish(pos);
+      pub_next = U(s.pub_next);
+    }
     const uint64_t buf0 = buf;
     const uint32_t pf0 = pf;
     int bo0 = bo, ho0 = ho;
@@ -1714,6 +1849,14 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       max_dist = dmax;
       break;
     }
+    if (part && src < pstart) {   // the source reaches into earlier parts: wait until they wrote it
+      const int b = U(min(min(src + copy_len, pos), pstart));
+      if (!part_ready_near(src, b, plo, phi, pseen, cover_lo)) {
+        finish_copy();
+        if (part_wait(src, b) < 0) return kPartFail;
+        pseen = g_lds.part_seen[lane];
+      }
+    }
     mbl -= insert_len;
     if (dist_code >= 0) dist_blen--;
     if (dc > 0) {
@@ -1816,6 +1959,7 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
     if (++s.guard > s.guard_limit) return MIB_E_NO_PROGRESS;
     switch (s.running) {
       case ST_BLOCK_START:
+        if (s.pos >= s.part_end) return 3;   // part mode: the next part starts here
         if (s.mbl < 0) return ERR(s, -10);
         if ((r = read_next_mb_header(s)) < 0) return r;
         fence = s.ring_size;
@@ -1829,6 +1973,7 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
       case ST_MAIN_LOOP:
       case ST_INSERT_LOOP:
       case ST_COPY_LOOP: {
+        if (s.running == ST_MAIN_LOOP && s.pos >= s.part_end) return 3;
         {
           int rr;
           if (s.tab16) {
@@ -1844,6 +1989,7 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
           }
           if (rr < 0) return rr;
         }
+        if (s.part && s.pos >= s.pub_next) part_publish(s.pos);
         continue;
       }
       case ST_USE_DICTIONARY:
@@ -1890,6 +2036,10 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
         continue;
       }
       case ST_INIT_WRITE:
+        if (s.part) {   // part mode decodes into the output itself: nothing to flush
+          s.running = s.next_running;
+          continue;
+        }
         s.rb_ready = s.pos < s.ring_size ? s.pos : s.ring_size;
         s.running = ST_WRITE;
         continue;
@@ -1926,6 +2076,85 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
   return 1;
 }
 
+// A fresh decoder state for one job (initState, engine.ts:160-178), in LDS.
+__device__ void dec_init(DecS &s, const DecJob &job, uint8_t *ring, int32_t *tables, uint8_t *ctx, int32_t *block_trees) {
+  const int lane = LANE;
+    s.l = &g_lds;
+  s.in = job.in;
+  s.in_len = job.in_len;
+  s.in_off = 0;
+  s.acc = 0;
+  s.bo = 32;
+  s.ho = 2048;
+  s.tail = 0;
+  s.eos = 0;
+  s.running = 0;
+  s.next_running = 0;
+  s.ring = ring;
+  s.ring_cap = 0;
+  s.ring_size = 0;
+  s.max_ring = 0;
+  s.max_back = 0;
+  s.max_dist = 0;
+  s.expected_total = 0;
+  s.pos = 0;
+  s.mbl = 0;
+  s.input_end = 0;
+  s.is_uncompressed = 0;
+  s.is_metadata = 0;
+  s.lit_blen = s.n_lit_types = s.cmd_blen = s.n_cmd_types = s.dist_blen = s.n_dist_types = 0;
+  for (int i = 0; i < 10; i++) s.rings[i] = 0;
+  s.rings[0] = 16; s.rings[1] = 15; s.rings[2] = 11; s.rings[3] = 4;
+  s.dist_rb_idx = 3;
+  s.ring_scratch = ring;
+  s.direct = 0;
+  s.tab_lds = g_ltab;
+  s.tab16 = s.cmd_base = s.dist_base = 0;
+  s.bt = block_trees;
+  s.tab_hbm = tables;
+  s.lit_group = tables;
+  s.cmd_group = tables;
+  s.dist_group = tables;
+  s.ctx_modes = ctx + 256 * 64 + 256 * 4;
+  s.ctx_map = ctx;
+  s.dist_ctx_map = ctx + 256 * 64;
+  s.trivial_lit_ctx = s.lit_tree_idx = s.cmd_tree_idx = 0;
+  s.j = s.insert_len = s.copy_len = s.dist_code = s.distance = 0;
+  s.ctx_map_slice = s.dist_ctx_map_slice = s.clo1 = s.clo2 = 0;
+  s.npostfix = s.ndirect = 0;
+  s.out = job.out;
+  s.out_cap = (int64_t)job.out_cap;
+  s.out_flushed = 0;
+  s.known_size = job.out_size > 0;
+  s.chunk_start = 0;
+  s.chunk_size = s.known_size ? job.out_size : 16384;
+  s.rb_written = s.rb_ready = 0;
+  s.cd = job.dict;
+  s.cd_total = (int)job.dict_len;
+  s.cd_br_offset = s.cd_br_length = s.cd_br_copied = s.cd_br_index = 0;
+  // iteration guard: far above what any stream can need (each iteration consumes input
+  // bits or produces output), low enough that a bug cannot spin a GPU forever
+  s.guard = 0;
+  s.guard_limit = 64ull * (job.in_len + 64) * 8 + 4ull * job.out_cap + (1ull << 26);
+  // initState (:160-178): fresh zeroed byteBuffer (its stale tail is observable) and block trees
+  for (int i = lane; i < (int)sizeof(g_lds.win); i += 64) g_lds.win[i] = 0;
+  for (int i = lane; i <= kBlockTreesCap; i += 64) block_trees[i] = 0;
+  __syncthreads();
+  if (lane == 0) block_trees[0] = 7;
+  __syncthreads();
+  s.win_base = -4096;
+  s.mb_bit = 0;
+  s.mb_pos = s.mb_len = 0;
+  s.part = 0;
+  s.part_start = 0;
+  s.part_end = 0x7FFFFFFF;
+  s.pub_next = 0x7FFFFFFF;
+  s.pidx = 0;
+  s.cover_lo = 0;
+  s.prog = nullptr;
+  s.ppos = nullptr;
+}
+
 // Persistent grid: block b decodes jobs b, b + grid, ...  Scratch per block:
 //   [ring: ring_bytes][tables: kDecodeTableInts int32][ctx maps: kDecodeCtxBytes][dist luts]
 __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int njobs, uint8_t *scratch,
@@ -1942,69 +2171,7 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
   for (int jb = blockIdx.x; jb < njobs; jb += gridDim.x) {
     DecJob job = jobs[jb];
     DecS &s = *(DecS *)&g_dec;
-    s.l = &g_lds;
-    s.in = job.in;
-    s.in_len = job.in_len;
-    s.in_off = 0;
-    s.acc = 0;
-    s.bo = 32;
-    s.ho = 2048;
-    s.tail = 0;
-    s.eos = 0;
-    s.running = 0;
-    s.next_running = 0;
-    s.ring = ring;
-    s.ring_cap = 0;
-    s.ring_size = 0;
-    s.max_ring = 0;
-    s.max_back = 0;
-    s.max_dist = 0;
-    s.expected_total = 0;
-    s.pos = 0;
-    s.mbl = 0;
-    s.input_end = 0;
-    s.is_uncompressed = 0;
-    s.is_metadata = 0;
-    s.lit_blen = s.n_lit_types = s.cmd_blen = s.n_cmd_types = s.dist_blen = s.n_dist_types = 0;
-    for (int i = 0; i < 10; i++) s.rings[i] = 0;
-    s.rings[0] = 16; s.rings[1] = 15; s.rings[2] = 11; s.rings[3] = 4;
-    s.dist_rb_idx = 3;
-    s.ring_scratch = ring;
-    s.direct = 0;
-    s.tab_lds = g_ltab;
-    s.tab16 = s.cmd_base = s.dist_base = 0;
-    s.bt = block_trees;
-    s.tab_hbm = tables;
-    s.lit_group = tables;
-    s.cmd_group = tables;
-    s.dist_group = tables;
-    s.ctx_modes = ctx + 256 * 64 + 256 * 4;
-    s.ctx_map = ctx;
-    s.dist_ctx_map = ctx + 256 * 64;
-    s.trivial_lit_ctx = s.lit_tree_idx = s.cmd_tree_idx = 0;
-    s.j = s.insert_len = s.copy_len = s.dist_code = s.distance = 0;
-    s.ctx_map_slice = s.dist_ctx_map_slice = s.clo1 = s.clo2 = 0;
-    s.npostfix = s.ndirect = 0;
-    s.out = job.out;
-    s.out_cap = (int64_t)job.out_cap;
-    s.out_flushed = 0;
-    s.known_size = job.out_size > 0;
-    s.chunk_start = 0;
-    s.chunk_size = s.known_size ? job.out_size : 16384;
-    s.rb_written = s.rb_ready = 0;
-    s.cd = job.dict;
-    s.cd_total = (int)job.dict_len;
-    s.cd_br_offset = s.cd_br_length = s.cd_br_copied = s.cd_br_index = 0;
-    // iteration guard: far above what any stream can need (each iteration consumes input
-    // bits or produces output), low enough that a bug cannot spin a GPU forever
-    s.guard = 0;
-    s.guard_limit = 64ull * (job.in_len + 64) * 8 + 4ull * job.out_cap + (1ull << 26);
-    // initState (:160-178): fresh zeroed byteBuffer (its stale tail is observable) and block trees
-    for (int i = lane; i < (int)sizeof(g_lds.win); i += 64) g_lds.win[i] = 0;
-    for (int i = lane; i <= kBlockTreesCap; i += 64) block_trees[i] = 0;
-    __syncthreads();
-    if (lane == 0) block_trees[0] = 7;
-    __syncthreads();
+    dec_init(s, job, ring, tables, ctx, block_trees);
     int rc = prepare(s);
     if (rc >= 0) {
       s.running = ST_INITED;
@@ -2030,12 +2197,153 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
   }
 }
 
+// ---------------------------------------------------------------- part decoding
+// One part of an indexed stream: decode its metablock's header, jump to the entry, run the
+// state machine to the next entry, then check that the state matches it exactly.
+__device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
+  const PartEntry e = *(const PartEntry *)job.part_entry;
+  const bool last = job.next_entry == nullptr;
+  const int lane = LANE;
+  if (job.total <= 0 || job.total >= (1ll << 30) || e.pos > (uint64_t)job.total) return kPartFail;
+  s.part = 1;
+  s.pidx = job.pidx;
+  s.prog = job.prog;
+  s.ppos = job.ppos;
+  s.part_start = (int)e.pos;
+  s.part_end = last ? 0x7FFFFFFF : (int)job.ppos[job.pidx + 1];
+  s.pub_next = s.part_start + (int)kPartPublish;
+  {
+    const int w = job.pidx - 1 - lane;
+    g_lds.part_lo[lane] = w >= 0 ? (int)job.ppos[w] : 0;
+    g_lds.part_hi[lane] = w >= 0 ? (int)job.ppos[w + 1] : 0;
+    g_lds.part_seen[lane] = 0;
+    s.cover_lo = job.pidx >= 64 ? (int)job.ppos[job.pidx - 64] : 0;
+  }
+  // the output is the ring: no wrap, no flush
+  int rs = 1 << job.max_ring_log;
+  while (rs < job.total + 64) rs <<= 1;
+  s.max_ring = 1 << job.max_ring_log;
+  s.max_back = s.max_ring - 16;
+  s.ring = job.out;
+  s.direct = 1;
+  s.ring_size = rs;
+  s.ring_cap = rs + 37;
+  s.expected_total = (int)job.total;
+  s.known_size = 1;
+  int r;
+  if (e.flags & kPartAtMb) {
+    if ((r = part_seek(s, (int64_t)e.bit)) < 0) return kPartFail;
+    s.pos = (int)e.pos;
+    s.running = ST_BLOCK_START;
+  } else {
+    if ((r = part_seek(s, (int64_t)e.mb_bit)) < 0) return kPartFail;
+    s.pos = (int)e.mb_pos;
+    if ((r = read_next_mb_header(s)) < 0 || s.running != ST_COMPRESSED_BLOCK_START) return kPartFail;
+    if ((r = read_codes_and_maps(s, dist_extra, dist_offset, ctxmap_table)) < 0) return kPartFail;
+    if (s.mb_pos + s.mb_len < (int)e.pos) return kPartFail;
+    if ((r = part_seek(s, (int64_t)e.bit)) < 0) return kPartFail;
+    s.mbl = s.mb_pos + s.mb_len - (int)e.pos;
+    s.pos = (int)e.pos;
+    if (e.type[0] >= s.n_lit_types || e.type[1] >= s.n_cmd_types || e.type[2] >= s.n_dist_types) return kPartFail;
+    s.rings[4] = e.prev[0]; s.rings[5] = e.type[0]; s.lit_blen = (int)e.blen[0];
+    s.rings[6] = e.prev[1]; s.rings[7] = e.type[1]; s.cmd_blen = (int)e.blen[1];
+    s.rings[8] = e.prev[2]; s.rings[9] = e.type[2]; s.dist_blen = (int)e.blen[2];
+    s.ctx_map_slice = e.type[0] << 6;
+    s.lit_tree_idx = s.ctx_map[s.ctx_map_slice];
+    s.clo1 = s.ctx_modes[e.type[0]] << 9;
+    s.clo2 = s.clo1 + 256;
+    build_ctx_tree_base(s);
+    s.cmd_tree_idx = e.type[1];
+    s.dist_ctx_map_slice = e.type[2] << 2;
+    s.running = ST_MAIN_LOOP;
+  }
+  s.rings[0] = (int)e.ring[3]; s.rings[1] = (int)e.ring[2]; s.rings[2] = (int)e.ring[1]; s.rings[3] = (int)e.ring[0];
+  s.dist_rb_idx = 3;
+  s.max_dist = s.pos < s.max_back ? s.pos : s.max_back;
+  // the literal context: the two bytes before the part (the previous part writes the same)
+  if (lane == 0 && s.pos >= 1) s.ring[s.pos - 1] = e.p1;
+  if (lane == 1 && s.pos >= 2) s.ring[s.pos - 2] = e.p2;
+  wave_sync();
+  r = decompress(s, dist_extra, dist_offset, ctxmap_table);
+  if (last) return (r == 1 && s.pos == (int)job.total) ? 0 : kPartFail;
+  if (r != 3) return kPartFail;
+  const PartEntry n = *(const PartEntry *)job.next_entry;
+  if (n.flags & kPartAtMb) {
+    // a streaming chunk ends in a byte-aligning empty metadata block and the next one starts
+    // with its own index block: step over metadata blocks up to the next part's header
+    for (int guard = 0; abs_bit(s) < (int64_t)n.bit && guard < 64; guard++) {
+      if (s.mbl > 0 || (r = read_next_mb_header(s)) < 0 || !s.is_metadata) return kPartFail;
+      if ((r = part_seek(s, abs_bit(s) + 8 * (int64_t)s.mbl)) < 0) return kPartFail;
+      s.mbl = 0;
+      s.running = ST_BLOCK_START;
+    }
+  }
+  const int idx = s.dist_rb_idx;
+  bool ok = abs_bit(s) == (int64_t)n.bit && s.pos == (int)n.pos &&
+            s.rings[idx & 3] == (int)n.ring[0] && s.rings[(idx - 1) & 3] == (int)n.ring[1] &&
+            s.rings[(idx - 2) & 3] == (int)n.ring[2] && s.rings[(idx - 3) & 3] == (int)n.ring[3];
+  if (n.flags & kPartAtMb) {
+    ok = ok && s.mbl == 0;
+  } else {
+    ok = ok && s.running == ST_MAIN_LOOP && s.mb_bit == (int64_t)n.mb_bit && s.mb_pos == (int)n.mb_pos &&
+         s.rings[5] == n.type[0] && s.rings[4] == n.prev[0] && s.lit_blen == (int)n.blen[0] &&
+         s.rings[7] == n.type[1] && s.rings[6] == n.prev[1] && s.cmd_blen == (int)n.blen[1] &&
+         s.rings[9] == n.type[2] && s.rings[8] == n.prev[2] && s.dist_blen == (int)n.blen[2];
+  }
+  if (ok && s.pos >= 2) {
+    ok = s.ring[s.pos - 1] == n.p1 && s.ring[s.pos - 2] == n.p2;
+  }
+  return ok ? 0 : kPartFail;
+}
+
+// Parts are taken in order from a ticket counter, so every part a wave may wait on has
+// already been taken by a running wave: a part only waits on earlier parts of its stream.
+__global__ __launch_bounds__(64) void decode_parts_kernel(DecJob *jobs, int njobs, uint8_t *scratch, uint64_t per_block,
+                                                          unsigned *ticket) {
+  uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
+  int32_t *tables = reinterpret_cast<int32_t *>(base);
+  uint8_t *ctx = reinterpret_cast<uint8_t *>(tables + kDecodeTableInts);
+  int8_t *dist_extra = reinterpret_cast<int8_t *>(ctx + kDecodeCtxBytes);
+  int32_t *dist_offset = reinterpret_cast<int32_t *>(dist_extra + 1152);
+  int32_t *ctxmap_table = dist_offset + 1152;
+  int32_t *block_trees = ctxmap_table + 1100;
+  const int lane = threadIdx.x;
+  for (;;) {
+    int jb = 0;
+    if (lane == 0) jb = (int)atomicAdd(ticket, 1u);
+    jb = __shfl(jb, 0);
+    if (jb >= njobs) break;
+    const DecJob job = jobs[jb];
+    DecS &s = *(DecS *)&g_dec;
+    dec_init(s, job, job.out, tables, ctx, block_trees);
+    int rc = part_run(s, job, dist_extra, dist_offset, ctxmap_table);
+    if (rc == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (!job.next_entry) part_publish(0x7FFFFFFF);
+      else part_publish(s.pos);
+    } else {
+      part_fail();
+    }
+    if (lane == 0) {
+      jobs[jb].status = rc;
+      jobs[jb].result_len = rc == 0 ? s.pos : 0;
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace mib
 
 extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
                                         uint64_t ring_bytes, int grid, hipStream_t stream) {
   hipLaunchKernelGGL(mib::decode_streams_kernel, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block,
                      ring_bytes);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t mib_decode_parts_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
+                                              unsigned *d_ticket, int grid, hipStream_t stream) {
+  hipLaunchKernelGGL(mib::decode_parts_kernel, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block, d_ticket);
   return hipGetLastError();
 }
 
@@ -2048,8 +2356,7 @@ namespace mib {
 __global__ void peek_heads_kernel(const uint8_t *in, const uint64_t *offsets, int k, uint8_t *heads) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < k; i += gridDim.x * blockDim.x) {
     uint64_t a = offsets[i], n = offsets[i + 1] - a;
-    heads[2 * i] = n > 0 ? in[a] : 0;
-    heads[2 * i + 1] = n > 1 ? in[a + 1] : 0;
+    for (int q = 0; q < 16; q++) heads[16 * i + q] = (uint64_t)q < n ? in[a + q] : 0;
   }
 }
 }  // namespace mib

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "common.h"
+#include "parts.h"
 
 #ifndef RFC_CONST
 #define RFC_CONST static __device__ const
@@ -68,7 +69,10 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint32_t hist;            // streaming: bytes of the stream before data[0] that copies may reach
   uint32_t abs_base;        // streaming: stream position of data[0] (mod 2^32)
   uint32_t *hist_tab;       // streaming: the encoder's bucket table of earlier positions, or null
-  uint32_t pad_;
+  uint32_t parts;           // 1: part index (parts.h) -- external copy sources lag, index block first
+  uint32_t idx_payload;     // part index: metadata payload bytes
+  uint64_t idx_bits;        // part index: bits before the first metablock (window bits + index block)
+  uint64_t out_base;        // streaming: stream bytes emitted before this chunk
   uint64_t out_off;         // byte offset of its scratch output slice
   uint64_t out_cap;
   uint64_t total_bits;      // written by offsets / stored
@@ -206,6 +210,17 @@ __device__ __forceinline__ uint32_t pack_match(uint32_t dist, uint32_t len) {
 }
 __device__ __forceinline__ uint32_t match_dist(uint32_t m) { return m & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t match_length(uint32_t m) { return m >> 24; }
+
+// Part index (parts.h): a copy whose source lies in an earlier 64 KiB segment must end
+// kPartLag bytes before the destination's offset in its own segment, so the wave decoding
+// that earlier part has (in lockstep) already written it.  The longest allowed length of a
+// copy at stream position A from distance d (~0u: no limit).
+__device__ __forceinline__ uint32_t part_cap(uint32_t A, uint32_t d) {
+  const uint32_t q = A - d;
+  if ((q >> kSegBits) == (A >> kSegBits)) return ~0u;
+  const uint32_t x = A & (kSeg - 1), ql = q & (kSeg - 1);
+  return x >= ql + kPartLag ? x - kPartLag - ql : 0u;
+}
 
 __device__ __forceinline__ uint32_t load_u32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
@@ -366,6 +381,10 @@ void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const
                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint8_t *trees, const uint8_t *hdr,
                  uint8_t *out);
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out);
+struct PushSum;
+void launch_part_index(hipStream_t st, const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, int nsegs,
+                       const Cmd *cmds, const Unit *units, PushSum *push, uint8_t *out);
+size_t part_push_bytes();
 void launch_pack(hipStream_t st, const Job *jobs, int njobs, const uint64_t *dst_off, const uint8_t *src, uint8_t *dst);
 
 }  // namespace enc

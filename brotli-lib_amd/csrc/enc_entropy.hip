@@ -1220,7 +1220,7 @@ __global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hd
   uint8_t *hb = hdr + (size_t)m * kHdrBytes;
   for (int i = 0; i < kHdrBytes; i++) hb[i] = 0;
   BitW w{hb, 0};
-  if (mb.start == 0 && jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
+  if (mb.start == 0 && jb.hdr_lgwin && !jb.parts) put_window_bits(w, (int)jb.hdr_lgwin);   // (else: part_index_kernel)
   const uint32_t length = mb.end - mb.start;
   w.put(1, mb.is_last);
   if (mb.is_last) w.put(1, 0);
@@ -1304,7 +1304,7 @@ __global__ void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t
   if (j >= njobs) return;
   Job &jb = jobs[j];
   if (jb.uncompressed) return;
-  uint64_t pos = 0;
+  uint64_t pos = jb.parts ? jb.idx_bits : 0;   // window bits + part index block first
   for (uint32_t m = 0; m < jb.nmb; m++) {
     Mb &mb = mbs[jb.mb_base + m];
     mb.bit_off = pos;

@@ -109,6 +109,8 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
         if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
         const uint32_t d = g - spos[e];
         if (d > max_dist || best >= limit) break;
+        const uint32_t pc = jb.parts ? part_cap(jb.abs_base + p, d) : ~0u;   // part index: lagging source
+        if (pc <= best) continue;
         const uint64_t x0 = mine0 ^ spre[0][e];
         uint32_t len;
         if (x0) {
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
             if (lim > len) len += match_len(cur + len, (cur - d) + len, lim - len);
           }
         }
-        len = min(len, limit);
+        len = min(min(len, limit), pc);
         if (len > best) {
           best = len;
           if (cnt == kMaxMatches) {   // keep the longest ones: drop the shortest
@@ -154,7 +156,8 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       // DONE: no longer candidate can matter (the parse measures a long copy itself)
 #define TAKE(d_, len_, DONE)                                               \
     do {                                                                     \
-      const uint32_t l_ = min((len_), limit);                                \
+      const uint32_t l_ = min(min((len_), limit),                            \
+                              jb.parts ? part_cap(jb.abs_base + p, (d_)) : ~0u); \
       if (l_ > best) {                                                       \
         best = l_;                                                           \
         if (cnt == kMaxMatches) {                                            \

@@ -141,6 +141,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
   const uint8_t *data = nullptr;
   int ndirect = 0, npostfix = 0;
+  uint32_t parts = 0, abs0 = 0;
   if (sgi < nsegs) {
     const Seg &sg = segs[sgi];
     const Job &jb = jobs[sg.job];
@@ -151,6 +152,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     data = jb.data;
     ndirect = (int)jb.ndirect;
     npostfix = (int)jb.npostfix;
+    parts = jb.parts;
+    abs0 = jb.abs_base;
   }
   if (__ballot(a < b) == 0) return;
   // literal costs from the stream's order-0 histogram (zopfli-cost-model.ts:163-189)
@@ -289,6 +292,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
             break;
           }
           fl = min(fl, cap);
+          if (parts) fl = min(fl, part_cap(abs0 + i, fd));   // (>= the record's length)
         }
         const int cc = copy_code(fl);
         const bool last = fd == ld;

@@ -1,0 +1,147 @@
+// The part index (parts.h) of a stream: the decoder state at the first command of every
+// 64 KiB parse segment, written as an RFC 7932 metadata metablock after the window bits.
+// Everything it records is known once the commands are coded and the bit offsets are laid
+// out: distance pushes per segment (part_push_kernel), then one walk per stream over its
+// metablocks, segments and block-split units (part_index_kernel).
+#include "enc_common.h"
+
+namespace mib {
+namespace enc {
+
+struct PushSum {          // the explicit distances a segment pushes on the decoder's ring
+  uint32_t n;             // how many
+  uint32_t d[4];          // the last (up to) four, most recent first
+};
+
+// Wave per segment: walk the commands back to front 64 at a time; a command pushes its
+// distance when it has a copy with an explicit distance code (code 0 = last distance and the
+// implicit-distance commands do not push: engine.ts distance ring update).
+__global__ __launch_bounds__(64) void part_push_kernel(const Job *jobs, const Seg *segs, const Cmd *cmds, PushSum *out) {
+  const Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  const int lane = threadIdx.x;
+  PushSum ps;
+  ps.n = 0;
+  for (int q = 0; q < 4; q++) ps.d[q] = 0;
+  if (!jb.parts || jb.uncompressed) {
+    if (lane == 0) out[blockIdx.x] = ps;
+    return;
+  }
+  const Cmd *c = cmds + sg.cmd_off;
+  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  uint32_t got = 0, total = 0;
+  for (int64_t hi = (int64_t)n; hi > 0; hi -= 64) {
+    const int64_t q = hi - 64 + lane;
+    bool push = false;
+    uint32_t d = 0;
+    if (q >= 0) {
+      const Cmd cc = c[q];
+      push = cc.copy != 0 && (cc.dist_prefix & 0x3FF) != 0;
+      d = cc.dist;
+    }
+    uint64_t m = __ballot(push);
+    total += (uint32_t)__popcll(m);
+    while (m && got < 4) {
+      const int l = 63 - __clzll((long long)m);
+      ps.d[got++] = (uint32_t)__builtin_amdgcn_readlane((int)d, l);
+      m &= ~(1ull << l);
+    }
+  }
+  ps.n = total;
+  if (lane == 0) out[blockIdx.x] = ps;
+}
+
+// Lane per stream: the entries in stream order, then the metadata block (window bits, header,
+// payload) at the front of the stream's output slice.
+__global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, const Unit *units,
+                                  const PushSum *push, uint8_t *out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const Job &jb = jobs[j];
+  if (!jb.parts || jb.uncompressed) return;
+  uint8_t *o = out + jb.out_off;
+  const int wb = jb.hdr_lgwin ? window_bits_len((int)jb.hdr_lgwin) : 0;
+  const int nb = part_skip_bytes(jb.idx_payload);
+  BitW w{o, 0};
+  if (jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
+  w.put(1, 0);                       // ISLAST
+  w.put(2, 3);                       // MNIBBLES: metadata
+  w.put(1, 0);                       // reserved
+  w.put(2, (uint32_t)nb);            // MSKIPBYTES
+  w.put(8 * nb, jb.idx_payload - 1);   // MSKIPLEN - 1 (then zero bits to the byte boundary)
+  uint8_t *pay = o + ((uint64_t)(wb + 6 + 8 * nb) + 7) / 8;
+  PartHead h;
+  h.magic = kPartMagic;
+  h.version = 1;
+  h.entry_bytes = (uint16_t)sizeof(PartEntry);
+  h.nentries = jb.nseg;
+  h.lgwin = jb.lgwin;
+  h.next_byte = jb.final_ ? 0 : jb.out_base + ((jb.total_bits + 7) >> 3);
+  h.total = (uint64_t)jb.abs_base + jb.n;
+  const uint8_t *hb = reinterpret_cast<const uint8_t *>(&h);
+  for (int i = 0; i < (int)sizeof(h); i++) pay[i] = hb[i];
+  uint8_t *ent = pay + sizeof(PartHead);
+  uint32_t ring[4];
+  for (int q = 0; q < 4; q++) ring[q] = (uint32_t)jb.dc_in[q];
+  const uint64_t bit0 = 8 * jb.out_base;
+  for (uint32_t m = 0; m < jb.nmb; m++) {
+    const Mb &mb = mbs[jb.mb_base + m];
+    uint32_t type[3] = {0, 0, 0}, prev[3] = {1, 1, 1}, blen[3];
+    for (int c = 0; c < 3; c++) blen[c] = mb.nbt[c] > 1 ? mb.first_count[c] : (1u << 28);
+    for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
+      const Seg &sg = segs[s];
+      PartEntry e;
+      const bool at_mb = s == mb.first_seg;
+      const bool has_cmd = sg.ncmd + (sg.extra_ins ? 1 : 0) > 0;
+      const uint32_t p = at_mb ? mb.start : sg.start - sg.carry_in;
+      e.flags = at_mb ? (kPartValid | kPartAtMb) : has_cmd ? kPartValid : 0u;
+      e.bit = bit0 + (at_mb ? mb.bit_off : sg.bit_off);
+      e.pos = (uint64_t)jb.abs_base + p;
+      e.mb_bit = bit0 + mb.bit_off;
+      e.mb_pos = (uint64_t)jb.abs_base + mb.start;
+      for (int q = 0; q < 4; q++) e.ring[q] = ring[q];
+      for (int c = 0; c < 3; c++) {
+        e.blen[c] = at_mb ? 0 : blen[c];
+        e.type[c] = (uint8_t)(at_mb ? 0 : type[c]);
+        e.prev[c] = (uint8_t)(at_mb ? 0 : prev[c]);
+      }
+      const uint32_t p12 = prev2(jb, p);
+      e.p1 = (uint8_t)(p12 & 0xFF);
+      e.p2 = (uint8_t)(p12 >> 8);
+      const uint8_t *eb = reinterpret_cast<const uint8_t *>(&e);
+      uint8_t *dst = ent + (size_t)(s - jb.seg_base) * sizeof(PartEntry);
+      for (int i = 0; i < (int)sizeof(e); i++) dst[i] = eb[i];
+      // the segment's distance pushes and block-split units, in stream order
+      const PushSum &ps = push[s];
+      if (ps.n >= 4) {
+        for (int q = 0; q < 4; q++) ring[q] = ps.d[q];
+      } else if (ps.n) {
+        uint32_t r[4];
+        for (uint32_t q = 0; q < 4; q++) r[q] = q < ps.n ? ps.d[q] : ring[q - ps.n];
+        for (int q = 0; q < 4; q++) ring[q] = r[q];
+      }
+      for (int u = 0; u < kSubPerSeg; u++) {
+        const Unit &un = units[(size_t)s * kSubPerSeg + u];
+        for (int c = 0; c < 3; c++) {
+          if (un.sw_count[c]) {
+            prev[c] = type[c];
+            type[c] = un.type[c];
+            blen[c] = un.sw_count[c];
+          }
+          blen[c] -= un.nsym[c];
+        }
+      }
+    }
+  }
+}
+
+void launch_part_index(hipStream_t st, const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, int nsegs,
+                       const Cmd *cmds, const Unit *units, PushSum *push, uint8_t *out) {
+  hipLaunchKernelGGL(part_push_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, cmds, push);
+  hipLaunchKernelGGL(part_index_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, units, push, out);
+}
+
+size_t part_push_bytes() { return sizeof(PushSum); }
+
+}  // namespace enc
+}  // namespace mib

@@ -126,7 +126,25 @@ struct StreamDesc {
   uint32_t hist;         // streaming: history bytes before data[0] (device-resident, contiguous)
   uint32_t abs_base;     // streaming: stream position of data[0]
   uint32_t *hist_tab;    // streaming: the encoder's bucket table (null: none)
+  uint64_t out_base;     // streaming: stream bytes emitted before this chunk
+  bool streaming;        // a BrotliEncoder chunk (part index whenever it has segments to split)
 };
+
+// Streams that get a part index (parts.h): one-shot streams of at least kPartMinStream bytes
+// and streaming chunks, when they have more than one parse segment.  MIB_PART_MIN (bytes)
+// overrides the one-shot threshold (0 disables the index).
+uint64_t part_min_stream() {
+  static uint64_t v = [] {
+    const char *e = getenv("MIB_PART_MIN");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) : kPartMinStream;
+  }();
+  return v;
+}
+bool wants_parts(const StreamDesc &d) {
+  const uint64_t lim = part_min_stream();
+  if (lim == 0 || d.n <= kSeg) return false;
+  return d.streaming || d.n >= lim;
+}
 
 struct Params {
   int quality, lgwin, npostfix, ndirect;
@@ -172,6 +190,15 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.abs_base = sd[j].abs_base;
     jb.hist_tab = sd[j].hist_tab;
     if (jb.hist_tab) any_hist = true;
+    jb.out_base = sd[j].out_base;
+    jb.parts = (!jb.uncompressed && wants_parts(sd[j])) ? 1 : 0;
+    uint64_t idx_extra = 0;
+    if (jb.parts) {
+      const uint64_t nseg_j = (n + kSeg - 1) / kSeg;
+      jb.idx_payload = (uint32_t)(sizeof(PartHead) + nseg_j * sizeof(PartEntry));
+      jb.idx_bits = part_index_bits(jb.hdr_lgwin ? window_bits_len((int)jb.hdr_lgwin) : 0, jb.idx_payload);
+      idx_extra = jb.idx_payload + 16;
+    }
     jb.pos_base = (uint32_t)pos_total;
     jb.seg_base = (uint32_t)segs.size();
     jb.mb_base = (uint32_t)mbs.size();
@@ -205,7 +232,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     for (uint64_t q = 0; q < span / kSeg; q++) seg_job.push_back((uint32_t)j);
     pos_total += span;
     jb.out_off = out_scratch;
-    jb.out_cap = n + n / 8 + 4096;
+    jb.out_cap = n + n / 8 + 4096 + idx_extra;
     out_scratch += (jb.out_cap + 255) & ~255ull;
   }
   if (pos_total >= (1ull << 31)) return MIB_E_INVALID_ARG;
@@ -230,6 +257,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + kTreeSlots * kTreeBytes + 4 * (kLitSlots * 256 + kMaxBT * 704 + kMaxBT * kDistCtx * 128));
   need += ns1 * kSubPerSeg * (sizeof(Unit) + kSubHist * 4);
   need += out_scratch + 64;
+  need += ns1 * part_push_bytes();
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
   if (!ws) {
@@ -268,6 +296,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   uint8_t *trees = ar.take<uint8_t>(nm1 * kTreeSlots * kTreeBytes);
   uint64_t *d_dst_off = ar.take<uint64_t>(k + 1);
   uint8_t *oscr = ar.take<uint8_t>(out_scratch + 64);
+  PushSum *push = reinterpret_cast<PushSum *>(ar.take<uint8_t>(ns1 * part_push_bytes()));
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
   Timer tm{ctx, st, mib_ctx_profiling(ctx) != 0, {}};
@@ -326,6 +355,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.stop();
     tm.start("emit");
     launch_emit(st, d_jobs, d_mbs, nmbs, d_segs, nsegs, cmds, cmd_pos, codes, units, trees, hdr, oscr);
+    tm.stop();
+    tm.start("part_index");
+    launch_part_index(st, d_jobs, (int)k, d_mbs, d_segs, nsegs, cmds, units, push, oscr);
     tm.stop();
   }
   tm.start("stored");
@@ -412,6 +444,8 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
   d.hist = 0;
   d.abs_base = 0;
   d.hist_tab = nullptr;
+  d.out_base = 0;
+  d.streaming = !one_shot;
   if (!one_shot) {
     d.hdr_lgwin = (uint32_t)prm.lgwin;
   } else if (n == 0) {
@@ -429,7 +463,7 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
   }
 }
 
-uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096; }
+uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096 + 16 + sizeof(PartHead) + ((n + kSeg - 1) / kSeg) * sizeof(PartEntry); }
 
 }  // namespace
 
@@ -451,6 +485,7 @@ struct mib_encoder {
   int cur = 0;
   uint64_t hist = 0;              // history bytes at buf[cur][0, hist)
   uint64_t abs = 0;               // stream bytes encoded so far
+  uint64_t obytes = 0;            // compressed bytes returned so far (part index offsets)
   uint32_t *tab = nullptr;
 };
 extern "C" {
@@ -583,6 +618,7 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
     sd[i].hist = (uint32_t)e->hist;
     sd[i].abs_base = (uint32_t)e->abs;
     sd[i].hist_tab = e->tab;
+    sd[i].out_base = e->obytes;
   }
   std::vector<uint64_t> ooff(k + 1, 0);
   std::vector<int32_t> dcs(4 * std::max<size_t>(k, 1));
@@ -593,6 +629,7 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
     for (size_t i = 0; rc == 0 && i < k; i++) {
       mib_encoder *e = es[i];
       accs[i].insert(accs[i].end(), host.data() + ooff[i], host.data() + ooff[i + 1]);
+      e->obytes += ooff[i + 1] - ooff[i];
       for (int q = 0; q < 4; q++) e->dc[q] = dcs[4 * i + q];
       const uint64_t n = ns[i];
       for (uint64_t q = n - std::min<uint64_t>(n, 2); q < n; q++)   // the chunk's last bytes

@@ -15,7 +15,10 @@
 #include <vector>
 
 #include "common.h"
+#include "parts.h"
 
+extern "C" hipError_t mib_decode_parts_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
+                                              unsigned *d_ticket, int grid, hipStream_t stream);
 extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
                                         uint64_t ring_bytes, int grid, hipStream_t stream);
 extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut);
@@ -109,6 +112,145 @@ int peek_window_bits(const uint8_t *b, size_t n) {
   return 17;
 }
 
+// ---------------------------------------------------------------- part index (parts.h)
+// A stream's part plan: every valid entry of its index chain, in stream order.
+struct PartPlan {
+  std::vector<mib::PartEntry> ent;
+  int64_t total = -1;
+  int lgwin = 0;
+};
+
+// LSB-first bit reader over bytes fetched on demand (host memory or the device)
+template <class Fetch>
+struct HdrBits {
+  Fetch &fetch;
+  uint64_t bit;
+  bool ok = true;
+  uint32_t get(int n) {
+    uint32_t v = 0;
+    for (int i = 0; i < n; i++, bit++) {
+      int byte = 0;
+      if (!fetch(bit >> 3, 1, (uint8_t *)&byte)) {
+        ok = false;
+        return 0;
+      }
+      v |= (uint32_t)((byte >> (bit & 7)) & 1) << i;
+    }
+    return v;
+  }
+};
+
+// The index block at byte `at` (with the stream's window bits first when at == 0).
+// fetch(offset, length, dst) copies stream bytes; false past the end.
+template <class Fetch>
+bool read_part_index(Fetch &fetch, uint64_t at, PartPlan &plan, uint64_t *next) {
+  HdrBits<Fetch> r{fetch, at * 8};
+  if (at == 0) {   // decodeWindowBits (engine.ts:91-124)
+    int lg;
+    if (r.get(1) == 0) lg = 16;
+    else {
+      const int m = (int)r.get(3);
+      if (m) lg = 17 + m;
+      else {
+        const int k = (int)r.get(3);
+        if (k == 1) return false;
+        lg = k ? 8 + k : 17;
+      }
+    }
+    plan.lgwin = lg;
+  }
+  if (r.get(1) != 0 || r.get(2) != 3 || r.get(1) != 0) return false;   // ISLAST 0, metadata, reserved 0
+  const int nb = (int)r.get(2);
+  if (nb == 0) return false;
+  const uint64_t len = (uint64_t)r.get(8 * nb) + 1;
+  if (!r.ok || len < sizeof(mib::PartHead)) return false;
+  const uint64_t pay = (r.bit + 7) >> 3;
+  mib::PartHead h;
+  if (!fetch(pay, sizeof(h), (uint8_t *)&h)) return false;
+  if (h.magic != mib::kPartMagic || h.version != 1 || h.entry_bytes != sizeof(mib::PartEntry)) return false;
+  if (sizeof(h) + (uint64_t)h.nentries * sizeof(mib::PartEntry) > len || h.nentries == 0 || h.nentries > (1u << 20)) return false;
+  if (at == 0 && (int)h.lgwin != plan.lgwin) return false;
+  std::vector<mib::PartEntry> e(h.nentries);
+  if (!fetch(pay + sizeof(h), sizeof(mib::PartEntry) * e.size(), (uint8_t *)e.data())) return false;
+  for (auto &x : e)
+    if (x.flags & mib::kPartValid) plan.ent.push_back(x);
+  plan.total = (int64_t)h.total;
+  *next = h.next_byte;
+  return true;
+}
+
+// The whole chain of a stream of n bytes; false if it has none or it does not hold together.
+template <class Fetch>
+bool plan_parts(Fetch &fetch, uint64_t n, PartPlan &plan) {
+  uint64_t at = 0, next = 0;
+  for (int guard = 0; guard < (1 << 16); guard++) {
+    if (!read_part_index(fetch, at, plan, &next)) {
+      if (at == 0) return false;
+      break;   // a chunk without an index: the last part decodes through it
+    }
+    if (next == 0) break;
+    if (next <= at || next >= n) return false;
+    at = next;
+  }
+  if (next != 0) return false;   // the stream's total is only known from the final chunk's head
+  if (plan.ent.size() < 2 || plan.total <= 0 || plan.total >= (1ll << 30)) return false;
+  if (plan.ent[0].pos != 0 || !(plan.ent[0].flags & mib::kPartAtMb)) return false;
+  for (size_t i = 0; i < plan.ent.size(); i++) {
+    const mib::PartEntry &x = plan.ent[i];
+    if (x.bit >= 8 * n || x.mb_bit > x.bit || x.mb_pos > x.pos || x.pos >= (uint64_t)plan.total) return false;
+    if (i && (x.pos <= plan.ent[i - 1].pos || x.bit <= plan.ent[i - 1].bit)) return false;
+  }
+  return true;
+}
+
+struct HostFetch {   // stream bytes in host memory
+  const uint8_t *b;
+  uint64_t n;
+  bool operator()(uint64_t off, uint64_t len, uint8_t *dst) const {
+    if (off > n || len > n - off) return false;
+    memcpy(dst, b + off, len);
+    return true;
+  }
+};
+// The first 16 bytes of a stream: window bits then an index block with our magic?
+bool looks_indexed(const uint8_t *head, uint64_t n) {
+  HostFetch f{head, std::min<uint64_t>(n, 16)};
+  HdrBits<HostFetch> r{f, 0};
+  if (r.get(1) != 0) {
+    if (r.get(3) == 0 && r.get(3) == 1) return false;
+  }
+  if (r.get(1) != 0 || r.get(2) != 3 || r.get(1) != 0) return false;
+  const int nb = (int)r.get(2);
+  if (nb == 0) return false;
+  r.get(8 * nb);
+  const uint64_t pay = (r.bit + 7) >> 3;
+  uint32_t magic = 0;
+  return r.ok && f(pay, 4, (uint8_t *)&magic) && magic == mib::kPartMagic;
+}
+
+struct DeviceFetch {   // stream bytes on the device (small reads: index heads and entries)
+  const uint8_t *d;
+  uint64_t n;
+  hipStream_t st;
+  uint64_t cache_off = ~0ull;
+  uint8_t cache[64];
+  bool operator()(uint64_t off, uint64_t len, uint8_t *dst) {
+    if (off > n || len > n - off) return false;
+    if (len == 1) {   // header bits: one cached 64-byte line at a time
+      if (cache_off == ~0ull || off < cache_off || off >= cache_off + 64) {
+        cache_off = off & ~63ull;
+        const uint64_t m = std::min<uint64_t>(64, n - cache_off);
+        if (hipMemcpyAsync(cache, d + cache_off, m, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+          return false;
+      }
+      *dst = cache[off - cache_off];
+      return true;
+    }
+    return hipMemcpyAsync(dst, d + off, len, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
+  }
+};
+
 }  // namespace
 
 struct mib_ctx {
@@ -121,8 +263,13 @@ struct mib_ctx {
   size_t jobs_cap = 0;
   uint8_t *d_aux = nullptr;   // small per-call staging (offsets, header peeks)
   uint64_t aux_bytes = 0;
+  // part decoding: entries, positions, progress words, ticket (one allocation)
+  uint8_t *d_parts = nullptr;
+  uint64_t parts_bytes = 0;
   // encode workspace (encode.hip)
   void *enc_ws = nullptr;
+  // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
+  uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
   bool profiling = false;
   std::vector<mib_kernel_time> times;
@@ -276,12 +423,19 @@ void mib_ctx_free(mib_ctx *c) {
   if (c->d_scratch) hipFree(c->d_scratch);
   if (c->d_jobs) hipFree(c->d_jobs);
   if (c->d_aux) hipFree(c->d_aux);
+  if (c->d_parts) hipFree(c->d_parts);
   if (c->enc_ws) mib_encode_ws_free(c->enc_ws);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
 }
 
 void mib_ctx_set_profiling(mib_ctx *c, int on) { c->profiling = on != 0; }
+
+void mib_part_stats(mib_ctx *c, uint64_t *parallel, uint64_t *fallback) {
+  if (!c) c = default_ctx();
+  if (parallel) *parallel = c ? c->parts_used : 0;
+  if (fallback) *fallback = c ? c->parts_fallback : 0;
+}
 
 // internal (encode.hip)
 mib_ctx *mib_default_ctx(void) { return default_ctx(); }
@@ -341,22 +495,126 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
   return 0;
 }
 
+// Decode indexed streams part-parallel.  streams[i] = (device input, length, device output,
+// plan); ok[i] = 1 when every part of stream i checked out (its output is then complete:
+// plan.total bytes), else the caller decodes it serially.
+struct PartStream {
+  const uint8_t *in;
+  uint64_t in_len;
+  uint8_t *out;
+  const PartPlan *plan;
+};
+static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vector<int> &ok, hipStream_t stream) {
+  size_t nj = 0, ne = 0;
+  for (auto &p : ps) {
+    nj += p.plan->ent.size();
+    ne += p.plan->ent.size();
+  }
+  ok.assign(ps.size(), 0);
+  if (nj == 0) return 0;
+  // device layout: entries | positions (nparts + 1 per stream) | progress | ticket
+  const uint64_t ent_b = ((ne * sizeof(mib::PartEntry)) + 255) & ~255ull;
+  const uint64_t pos_b = (((ne + ps.size()) * 8) + 255) & ~255ull;
+  const uint64_t prog_b = ((ne * 8) + 255) & ~255ull;
+  int rc;
+  if ((rc = grow((void **)&c->d_parts, &c->parts_bytes, ent_b + pos_b + prog_b + 256)) != 0) return rc;
+  mib::PartEntry *d_ent = reinterpret_cast<mib::PartEntry *>(c->d_parts);
+  int64_t *d_pos = reinterpret_cast<int64_t *>(c->d_parts + ent_b);
+  uint64_t *d_prog = reinterpret_cast<uint64_t *>(c->d_parts + ent_b + pos_b);
+  unsigned *d_ticket = reinterpret_cast<unsigned *>(c->d_parts + ent_b + pos_b + prog_b);
+  std::vector<mib::PartEntry> ents;
+  std::vector<int64_t> pos;
+  std::vector<mib::DecJob> jobs;
+  ents.reserve(ne);
+  pos.reserve(ne + ps.size());
+  jobs.reserve(nj);
+  for (auto &p : ps) {
+    const size_t e0 = ents.size(), p0 = pos.size();
+    const size_t np = p.plan->ent.size();
+    for (auto &x : p.plan->ent) {
+      ents.push_back(x);
+      pos.push_back((int64_t)x.pos);
+    }
+    pos.push_back(p.plan->total);
+    for (size_t i = 0; i < np; i++) {
+      mib::DecJob j;
+      memset(&j, 0, sizeof(j));
+      j.in = p.in;
+      j.in_len = p.in_len;
+      j.out = p.out;
+      j.out_cap = (uint64_t)p.plan->total;
+      j.out_size = p.plan->total;
+      j.max_ring_log = p.plan->lgwin;
+      j.part_entry = d_ent + e0 + i;
+      j.next_entry = i + 1 < np ? d_ent + e0 + i + 1 : nullptr;
+      j.ppos = d_pos + p0;
+      j.prog = d_prog + e0;
+      j.pidx = (int32_t)i;
+      j.nparts = (int32_t)np;
+      j.total = p.plan->total;
+      jobs.push_back(j);
+    }
+  }
+  uint64_t per_block = mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4 + 3092 * 4;
+  per_block = (per_block + 255) & ~(uint64_t)255;
+  const int grid = (int)std::min<size_t>(nj, 2048);
+  if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
+  if (nj > c->jobs_cap) {
+    if (c->d_jobs) hipFree(c->d_jobs);
+    c->d_jobs = nullptr;
+    c->jobs_cap = 0;
+    if (hipMalloc(&c->d_jobs, sizeof(mib::DecJob) * nj) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+    c->jobs_cap = nj;
+  }
+  HIP_OK(hipMemcpyAsync(d_ent, ents.data(), sizeof(mib::PartEntry) * ne, hipMemcpyHostToDevice, stream));
+  HIP_OK(hipMemcpyAsync(d_pos, pos.data(), 8 * pos.size(), hipMemcpyHostToDevice, stream));
+  HIP_OK(hipMemsetAsync(d_prog, 0, prog_b + 256, stream));   // progress words and the ticket
+  HIP_OK(hipMemcpyAsync(c->d_jobs, jobs.data(), sizeof(mib::DecJob) * nj, hipMemcpyHostToDevice, stream));
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->profiling) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipEventRecord(e0, stream);
+  }
+  HIP_OK(mib_decode_parts_launch(c->d_jobs, (int)nj, c->d_scratch, per_block, d_ticket, grid, stream));
+  if (c->profiling) hipEventRecord(e1, stream);
+  HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * nj, hipMemcpyDeviceToHost, stream));
+  HIP_OK(hipStreamSynchronize(stream));
+  if (c->profiling) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    c->add_time("decode_parts_kernel", ms);
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  }
+  size_t q = 0;
+  for (size_t i = 0; i < ps.size(); i++) {
+    int good = 1;
+    for (size_t k = 0; k < ps[i].plan->ent.size(); k++, q++)
+      if (jobs[q].status != 0) good = 0;
+    ok[i] = good;
+  }
+  c->parts_used += ps.size();
+  for (int v : ok) c->parts_fallback += v ? 0 : 1;
+  return 0;
+}
+
 int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, size_t k, uint8_t *d_out,
                    const uint64_t *out_offsets, int64_t *out_sizes, int *status, void *stream) {
   if (!c || (k && (!d_in || !in_offsets || !d_out || !out_offsets))) return MIB_E_INVALID_ARG;
   if (ensure_device(c->device) != 0) return MIB_E_NO_DEVICE;
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   c->times.clear();
-  std::vector<uint8_t> heads(2 * k + 2);
+  std::vector<uint8_t> heads(16 * k + 16);
   std::vector<mib::DecJob> jobs(k);
-  if (k) {   // window bits of every stream, gathered on the device in one launch
-    int rc = grow((void **)&c->d_aux, &c->aux_bytes, (k + 1) * 8 + 2 * k + 256);
+  if (k) {   // window bits (and part index magic) of every stream, gathered in one launch
+    int rc = grow((void **)&c->d_aux, &c->aux_bytes, (k + 1) * 8 + 16 * k + 256);
     if (rc) return rc;
     uint64_t *d_off = reinterpret_cast<uint64_t *>(c->d_aux);
     uint8_t *d_heads = c->d_aux + ((k + 1) * 8 + 255) / 256 * 256;
     HIP_OK(hipMemcpyAsync(d_off, in_offsets, (k + 1) * 8, hipMemcpyHostToDevice, st));
     HIP_OK(mib_decode_peek_heads(d_in, d_off, (int)k, d_heads, st));
-    HIP_OK(hipMemcpyAsync(heads.data(), d_heads, 2 * k, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(heads.data(), d_heads, 16 * k, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
   }
   for (size_t i = 0; i < k; i++) {
@@ -367,10 +625,45 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
     j.out = d_out + out_offsets[i];
     j.out_cap = out_offsets[i + 1] - out_offsets[i];
     j.out_size = -1;
-    j.max_ring_log = peek_window_bits(&heads[2 * i], (size_t)std::min<uint64_t>(j.in_len, 2));
+    j.max_ring_log = peek_window_bits(&heads[16 * i], (size_t)std::min<uint64_t>(j.in_len, 2));
   }
-  int rc = decode_jobs(c, jobs, st);
+  // streams with a part index decode part-parallel; the rest (and any part stream that does
+  // not check out) one wave per stream
+  std::vector<PartPlan> plans(k);
+  std::vector<PartStream> ps;
+  std::vector<size_t> ps_idx;
+  std::vector<mib::DecJob> serial;
+  std::vector<size_t> serial_idx;
+  for (size_t i = 0; i < k; i++) {
+    bool part = false;
+    if (looks_indexed(&heads[16 * i], jobs[i].in_len)) {
+      DeviceFetch f{jobs[i].in, jobs[i].in_len, st};
+      part = plan_parts(f, jobs[i].in_len, plans[i]) && (uint64_t)plans[i].total + 64 <= jobs[i].out_cap;
+    }
+    if (part) {
+      ps.push_back(PartStream{jobs[i].in, jobs[i].in_len, jobs[i].out, &plans[i]});
+      ps_idx.push_back(i);
+    } else {
+      serial.push_back(jobs[i]);
+      serial_idx.push_back(i);
+    }
+  }
+  std::vector<int> ok;
+  int rc = decode_parts(c, ps, ok, st);
   if (rc) return rc;
+  for (size_t q = 0; q < ps.size(); q++) {
+    const size_t i = ps_idx[q];
+    if (ok[q]) {
+      jobs[i].status = 0;
+      jobs[i].result_len = plans[i].total;
+    } else {
+      serial.push_back(jobs[i]);
+      serial_idx.push_back(i);
+    }
+  }
+  rc = decode_jobs(c, serial, st);
+  if (rc) return rc;
+  for (size_t q = 0; q < serial.size(); q++) jobs[serial_idx[q]] = serial[q];
   int worst = 0;
   for (size_t i = 0; i < k; i++) {
     out_sizes[i] = jobs[i].result_len;
@@ -413,6 +706,37 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
       return MIB_E_OUT_OF_MEMORY;
     }
     if (dict_n) hipMemcpy(d_dict, dict, dict_n, hipMemcpyHostToDevice);
+  }
+  if (!dict && exact_out < 0) {   // a stream with a part index: part-parallel, checked
+    PartPlan plan;
+    HostFetch f{in, n};
+    if (plan_parts(f, n, plan)) {
+      std::vector<PartStream> ps(1);
+      std::vector<int> ok;
+      if (hipMalloc(&d_out, (uint64_t)plan.total + 4096) != hipSuccess) {
+        hipFree(d_in);
+        return MIB_E_OUT_OF_MEMORY;
+      }
+      ps[0] = PartStream{d_in, n, d_out, &plan};
+      rc = decode_parts(c, ps, ok, c->stream);
+      if (rc == 0 && ok[0]) {
+        const uint64_t len = (uint64_t)plan.total;
+        if (max_out >= 0 && (int64_t)len > max_out) {   // decode.ts:57-62
+          out->size = len;
+          rc = MIB_E_OUTPUT_LIMIT;
+        } else {
+          out->data = (uint8_t *)malloc(len);
+          out->size = len;
+          if (hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
+        }
+        hipFree(d_out);
+        hipFree(d_in);
+        return rc;
+      }
+      hipFree(d_out);
+      d_out = nullptr;
+      rc = 0;
+    }
   }
   for (;;) {
     // room for the ring of a one-metablock stream (a power of two >= its size, + slack), so

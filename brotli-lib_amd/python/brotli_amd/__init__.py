@@ -104,6 +104,7 @@ def _L():
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
         lib.mib_ctx_kernel_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(_KTime), ctypes.c_int]
         lib.mib_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.mib_part_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         _lib = lib
     return _lib
 
@@ -251,6 +252,14 @@ def decode_batch(buffers):
     if rc:
         raise _err(rc)
     return [(_take(outs[i]) if st[i] == 0 else _err(st[i])) for i in range(k)]
+
+
+def part_stats(ctx=None):
+    """(streams decoded part-parallel, of those sent back to the serial decoder) for a
+    DeviceContext, or the host API's default context"""
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    _L().mib_part_stats(ctx._c if ctx is not None else None, ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
 
 
 class DeviceContext:

@@ -111,6 +111,10 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
 typedef struct { char name[32]; double ms; uint32_t launches; } mib_kernel_time;
 int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max);
 void mib_ctx_set_profiling(mib_ctx *c, int on);
+/* Part-parallel decoding (streams this encoder marked with a part index):
+ * how many streams a context (NULL: the default one) decoded part-parallel, and how many of
+ * those it sent back to the serial decoder because a part did not check out. Diagnostic. */
+void mib_part_stats(mib_ctx *c, uint64_t *parallel, uint64_t *fallback);
 
 #ifdef __cplusplus
 }

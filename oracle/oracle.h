@@ -19,6 +19,9 @@ int64_t oracle_peek_decoded_size(const uint8_t *in, size_t n);
  * reference's negative error code; *out is malloc'ed (free with oracle_free). */
 int oracle_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n,
                   int64_t out_size, uint8_t **out, size_t *out_n);
+/* decode and record the decoder state (parts.h PartEntry layout, 72 bytes each) at the
+ * command boundaries / metablock headers at the ascending output positions pos[0..npos) */
+int oracle_decode_probe(const uint8_t *in, size_t n, const uint64_t *pos, size_t npos, void *states);
 
 /* encode.ts:50 brotliEncode (bugs A,B fixed = the survey's "ref-fixed"; C,E fixed too).
  * quality 0..11, lgwin 10..24, mode 0 GENERIC / 1 TEXT / 2 FONT. */

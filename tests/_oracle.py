@@ -73,3 +73,21 @@ def decode(data, out_size=None, dictionary=None):
     r = ctypes.string_at(o, n.value)
     lib().oracle_free(o)
     return r
+
+
+PROBE_DTYPE = None
+
+
+def probe(data, positions):
+    """decoder states (parts.h PartEntry layout) at the given ascending output positions:
+    the command starting there, or the metablock header starting there (flags bit 2)."""
+    import numpy as np
+    from _parts import ENTRY_DTYPE
+    pos = np.ascontiguousarray(np.asarray(positions, dtype=np.uint64))
+    out = np.zeros(len(pos), dtype=ENTRY_DTYPE)
+    f = lib().oracle_decode_probe
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    rc = f(data, len(data), pos.ctypes.data, len(pos), out.ctypes.data)
+    if rc:
+        raise RuntimeError('oracle_decode_probe rc=%d' % rc)
+    return out

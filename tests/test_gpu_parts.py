@@ -1,0 +1,150 @@
+"""Part-parallel decoding of one stream (brotli-lib_amd/csrc/parts.h).
+
+Streams of >= 2 MiB from this encoder carry, in a metadata metablock, the decoder's state at
+the first command of every 64 KiB segment, so one stream decodes on many waves.  What must
+hold:
+  * the stream stays an RFC 7932 stream whose decoded bytes are the input, for the oracle
+    (the reference decoder restated: it skips the metadata block) and for native brotli;
+  * every index entry IS the reference decoder's state at that point -- the oracle records
+    its own state at each entry's position (oracle_decode_probe) and the test compares;
+  * the HIP decoder takes the part-parallel path and returns the same bytes; when the index
+    is corrupted it notices (a part's end state differs from the next entry) and decodes
+    serially; corrupted stream bytes give exactly the oracle's error code.
+"""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import _oracle
+import _parts
+import brotli_amd
+from brotli_amd import datagen
+
+pytestmark = pytest.mark.gpu
+
+_CACHE = {}
+
+
+def _enwik_stream(n, seed, quality=11, lgwin=22):
+    key = (n, seed, quality, lgwin)
+    if key not in _CACHE:
+        data = datagen.enwik_text(n, seed)
+        _CACHE[key] = (data, brotli_amd.brotliEncode(data, {'quality': quality, 'lgwin': lgwin}))
+    return _CACHE[key]
+
+
+def _check_entries_against_oracle(enc, ents):
+    got = _oracle.probe(enc, ents['pos'])
+    assert np.all(got['flags'] & 1), 'oracle never reached some entries at a command boundary'
+    for f in ('bit', 'pos', 'mb_bit', 'mb_pos', 'ring', 'p1', 'p2'):
+        assert np.array_equal(got[f], ents[f]), f
+    at_mb = (ents['flags'] & _parts.AT_MB) != 0
+    assert np.array_equal(at_mb, (got['flags'] & 2) != 0)
+    mid = ~at_mb
+    for f in ('blen', 'type', 'prev'):
+        assert np.array_equal(got[f][mid], ents[f][mid]), f
+
+
+def test_index_is_the_reference_decoder_state():
+    data, enc = _enwik_stream(3 << 20, 2)
+    chain = _parts.read_chain(enc)
+    assert chain is not None, 'a 3 MiB stream must carry a part index'
+    ents, total = chain
+    assert total == len(data)
+    assert len(ents) == 48 and ents['pos'][0] == 0
+    assert _oracle.decode(enc) == data
+    _check_entries_against_oracle(enc, ents)
+
+
+def test_part_parallel_decode():
+    data, enc = _enwik_stream(3 << 20, 2)
+    p0, f0 = brotli_amd.part_stats()
+    assert brotli_amd.brotliDecode(enc) == data
+    p1, f1 = brotli_amd.part_stats()
+    assert p1 == p0 + 1 and f1 == f0, 'the stream was not decoded part-parallel'
+    # device-resident batch (the bench path): two indexed streams and a plain one
+    import torch
+    other = datagen.enwik_text(200000, 5)
+    enc2 = brotli_amd.brotliEncode(other, {'quality': 11})
+    assert _parts.read_chain(enc2) is None   # below the index threshold
+    streams = [enc, enc2, enc]
+    dev = torch.device('cuda', 0)
+    src = torch.tensor(np.frombuffer(b''.join(streams), dtype=np.uint8), device=dev)
+    ioff = [0]
+    for s_ in streams:
+        ioff.append(ioff[-1] + len(s_))
+    sizes = [len(data), len(other), len(data)]
+    ooff = [0]
+    for n in sizes:
+        ooff.append(ooff[-1] + n + 4096)
+    out = torch.zeros(ooff[-1], dtype=torch.uint8, device=dev)
+    ctx = brotli_amd.DeviceContext(0)
+    got, st = ctx.decode(src.data_ptr(), ioff, out.data_ptr(), ooff)
+    assert st == [0, 0, 0] and got == sizes
+    host = out.cpu().numpy().tobytes()
+    assert host[ooff[0]:ooff[0] + sizes[0]] == data
+    assert host[ooff[1]:ooff[1] + sizes[1]] == other
+    assert host[ooff[2]:ooff[2] + sizes[2]] == data
+    assert brotli_amd.part_stats(ctx) == (2, 0)
+
+
+def test_corrupt_index_falls_back_to_serial():
+    data, enc = _enwik_stream(3 << 20, 2)
+    ents, _ = _parts.read_chain(enc)
+    # locate entry 5's `bit` field in the payload and move it by one bit
+    b = bytearray(enc)
+    raw = bytes(ents[5:6].tobytes())
+    at = bytes(b).find(raw)
+    assert at > 0
+    bad = ents[5:6].copy()
+    bad['bit'] += 1
+    b[at:at + 72] = bad.tobytes()
+    p0, f0 = brotli_amd.part_stats()
+    assert brotli_amd.brotliDecode(bytes(b)) == data   # metadata is skipped: same stream content
+    p1, f1 = brotli_amd.part_stats()
+    assert p1 == p0 + 1 and f1 == f0 + 1
+    # a corrupted data byte: the part path must not hide the reference's error
+    c = bytearray(enc)
+    c[len(c) // 2] ^= 0x5A
+    want = _oracle.decode(bytes(c))
+    try:
+        got = brotli_amd.brotliDecode(bytes(c))
+    except brotli_amd.BrotliError as e:
+        got = e.code
+    if isinstance(want, bytes):
+        assert got == want
+    else:
+        assert got == want, (got, want)
+
+
+def test_streaming_chunks_carry_chained_indexes():
+    data = datagen.enwik_text(20 << 20, 9)
+    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24})
+    parts = [e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)]
+    parts.append(e.finish())
+    enc = b''.join(parts)
+    chain = _parts.read_chain(enc)
+    assert chain is not None
+    ents, total = chain
+    assert total == len(data) and len(ents) >= 300
+    assert _oracle.decode(enc) == data
+    _check_entries_against_oracle(enc, ents)
+    p0, f0 = brotli_amd.part_stats()
+    assert brotli_amd.brotliDecode(enc) == data
+    assert brotli_amd.part_stats() == (p0 + 1, f0)
+
+
+@pytest.mark.skipif(shutil.which('node') is None, reason='node not installed')
+def test_native_brotli_decodes_indexed_stream(tmp_path):
+    data, enc = _enwik_stream(3 << 20, 2)
+    p = tmp_path / 's.br'
+    p.write_bytes(enc)
+    js = ("const z=require('zlib'),fs=require('fs');const o=z.brotliDecompressSync(fs.readFileSync(process.argv[1]));"
+          "process.stdout.write(require('crypto').createHash('sha256').update(o).digest('hex'))")
+    out = subprocess.run(['node', '-e', js, str(p)], capture_output=True, text=True, timeout=120)
+    import hashlib
+    assert out.returncode == 0, out.stderr
+    assert out.stdout == hashlib.sha256(data).hexdigest()
