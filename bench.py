@@ -357,8 +357,9 @@ def main():
     if rank == 0:
         ms_step = dt * 1e3 / args.steps
         mb = world * total / 1e6
-        enc_ms = sum(v[0] for n, v in times.items() if n != 'decode_streams_kernel') / args.steps
-        dec_ms = times.get('decode_streams_kernel', [0.0, 1])[0] / args.steps
+        dec_names = ('decode_streams_kernel', 'decode_parts_kernel')
+        enc_ms = sum(v[0] for n, v in times.items() if n not in dec_names) / args.steps
+        dec_ms = sum(times.get(n, [0.0, 1])[0] for n in dec_names) / args.steps
         dom_name, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
         # a kernel launched L times per step covers 1/L of the batch per launch
         launches_per_step = max(1, dom_n // args.steps)

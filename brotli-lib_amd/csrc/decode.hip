@@ -1089,8 +1089,10 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
         const int pstart = __builtin_amdgcn_readfirstlane(s.part_start), cover_lo = __builtin_amdgcn_readfirstlane(s.cover_lo);
         // The last two output bytes (the literal context) live in registers: reading them
         // back from the ring would wait for every outstanding ring store (vmcnt is in order).
-        int c1 = __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 1) & rmask]);
-        int c2b = __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 2) & rmask]);
+        // (part mode: absolute positions -- before the stream start the context bytes are 0;
+        // the ring's last bytes would lie past the output buffer)
+        int c1 = (s.part && s.pos < 1) ? 0 : __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 1) & rmask]);
+        int c2b = (s.part && s.pos < 2) ? 0 : __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 2) & rmask]);
         int dr0, dr1, dr2, dr3, dridx;   // the distance ring (rings[0..3], dist_rb_idx)
         uint32_t acc;
         int bo, ho, pos, j, mbl, insert_len, copy_len, dist_code, distance, cmd_blen, lit_blen, dist_blen, max_dist;
@@ -1608,7 +1610,7 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
 //  * copies of <= 64 bytes: the source load is issued and the command loop goes on; the
 //    stores and the new (p1, p2) are completed when first needed (the next literals, the
 //    next copy, or the exit), so the load's latency overlaps the next command's header.
-template <bool kTrivial>
+template <bool kTrivial, bool kPart>
 __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
 #define U(x) __builtin_amdgcn_readfirstlane(x)
   DecS &s = *(DecS *)&g_dec;
@@ -1621,10 +1623,12 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   const int lane = LANE;
   const int rmask = U(rmask_in);
   // positions stay below lim: no fence, flush or wrap inside a command
-  const int lim = U(min(min(fence_in, rmask), s.part_end));
-  // part mode: publishing, and the 64 earlier parts' ranges / acquired progress (lane l)
-  const int part = U(s.part), pstart = U(s.part_start), cover_lo = U(s.cover_lo);
-  int pub_next = U(s.pub_next);
+  const int lim = kPart ? U(min(min(fence_in, rmask), s.part_end)) : U(min(fence_in, rmask));
+  // part mode (a build of its own): publishing, and the 64 earlier parts' ranges / acquired
+  // progress (lane l)
+  constexpr bool part = kPart;
+  const int pstart = kPart ? U(s.part_start) : 0, cover_lo = kPart ? U(s.cover_lo) : 0;
+  int pub_next = kPart ? U(s.pub_next) : 0x7FFFFFFF;
   int plo = 0, phi = 0, pseen = 0;
   if (part) {
     plo = g_lds.part_lo[LANE];
@@ -1639,7 +1643,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   uint32_t pf = win16[ho + 2];
   int cmd_blen = U(s.cmd_blen), lit_blen = U(s.lit_blen), dist_blen = U(s.dist_blen), max_dist = U(s.max_dist);
   int dr0 = U(s.rings[0]), dr1 = U(s.rings[1]), dr2 = U(s.rings[2]), dr3 = U(s.rings[3]), dridx = U(s.dist_rb_idx);
-  int c1 = U((int)s.ring[(pos - 1) & rmask]), c2b = U((int)s.ring[(pos - 2) & rmask]);
+  int c1 = (kPart && pos < 1) ? 0 : U((int)s.ring[(pos - 1) & rmask]);
+  int c2b = (kPart && pos < 2) ? 0 : U((int)s.ring[(pos - 2) & rmask]);
   const int cmd_root = U((int)t16[s.cmd_base + s.cmd_tree_idx]);
   const int lit_root = kTrivial ? U((int)t16[s.lit_tree_idx]) : 0;
   // lut1 of the literal context mode, packed: lane l holds entries l, l + 64, l + 128, l + 192
@@ -1978,7 +1983,8 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
           int rr;
           if (s.tab16) {
             if (s.running == ST_MAIN_LOOP) {
-              rr = s.trivial_lit_ctx ? fast_loop<true>(fence, rmask) : fast_loop<false>(fence, rmask);
+              if (s.part) rr = s.trivial_lit_ctx ? fast_loop<true, true>(fence, rmask) : fast_loop<false, true>(fence, rmask);
+              else rr = s.trivial_lit_ctx ? fast_loop<true, false>(fence, rmask) : fast_loop<false, false>(fence, rmask);
               if (rr < 0) return rr;
             }
             // what the fast loop left (a block switch, a refill, a dictionary word, a wrap,

@@ -71,6 +71,8 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint32_t *hist_tab;       // streaming: the encoder's bucket table of earlier positions, or null
   uint32_t parts;           // 1: part index (parts.h) -- external copy sources lag, index block first
   uint32_t idx_payload;     // part index: metadata payload bytes
+  uint32_t part_bits;       // part index: log2 of the part size (>= kSegBits)
+  uint32_t part_lag;        // part index: how far an external copy source lags (bytes)
   uint64_t idx_bits;        // part index: bits before the first metablock (window bits + index block)
   uint64_t out_base;        // streaming: stream bytes emitted before this chunk
   uint64_t out_off;         // byte offset of its scratch output slice
@@ -211,15 +213,15 @@ __device__ __forceinline__ uint32_t pack_match(uint32_t dist, uint32_t len) {
 __device__ __forceinline__ uint32_t match_dist(uint32_t m) { return m & 0xFFFFFFu; }
 __device__ __forceinline__ uint32_t match_length(uint32_t m) { return m >> 24; }
 
-// Part index (parts.h): a copy whose source lies in an earlier 64 KiB segment must end
-// kPartLag bytes before the destination's offset in its own segment, so the wave decoding
-// that earlier part has (in lockstep) already written it.  The longest allowed length of a
-// copy at stream position A from distance d (~0u: no limit).
-__device__ __forceinline__ uint32_t part_cap(uint32_t A, uint32_t d) {
+// Part index (parts.h): a copy whose source lies in an earlier part (2^bits aligned) must
+// end `lag` bytes before the destination's offset in its own part, so the wave decoding that
+// earlier part has (in lockstep) already written it.  The longest allowed length of a copy
+// at stream position A from distance d (~0u: no limit).
+__device__ __forceinline__ uint32_t part_cap(uint32_t A, uint32_t d, uint32_t bits, uint32_t lag) {
   const uint32_t q = A - d;
-  if ((q >> kSegBits) == (A >> kSegBits)) return ~0u;
-  const uint32_t x = A & (kSeg - 1), ql = q & (kSeg - 1);
-  return x >= ql + kPartLag ? x - kPartLag - ql : 0u;
+  if ((q >> bits) == (A >> bits)) return ~0u;
+  const uint32_t m = (1u << bits) - 1u, x = A & m, ql = q & m;
+  return x >= ql + lag ? x - lag - ql : 0u;
 }
 
 __device__ __forceinline__ uint32_t load_u32(const uint8_t *p) {
@@ -356,7 +358,7 @@ struct ItemMap {
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals);
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
-                         const uint32_t *svals, uint32_t total, int depth, bool hist, uint32_t *matches);
+                         const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total);

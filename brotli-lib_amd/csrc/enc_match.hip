@@ -60,7 +60,9 @@ __device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, 
   for (uint32_t i = 0; i < avail && i < 8 * kPreW; i++) o[i >> 3] |= (uint64_t)p[i] << (8 * (i & 7));
 }
 
-template <bool kHist>   // streaming chunks with a history table (a separate build of the walk)
+// kHist: streaming chunks with a history table; kParts: some stream carries a part index
+// (lagging external sources) -- separate builds of the walk
+template <bool kHist, bool kParts>
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
                                                              const uint32_t *sorted_vals, uint32_t total, int depth,
                                                              uint32_t *matches) {
@@ -99,6 +101,8 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     const uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
     const uint32_t limit = seg_end - p;   // copies never cross a parse segment
     const uint8_t *cur = jb.data + p;
+    const bool parts = kParts && jb.parts;
+    const uint32_t pA = jb.abs_base + p, pbits = kParts ? jb.part_bits : 16u, plag = kParts ? jb.part_lag : 0u;
     uint32_t best = 3;
     uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
     if constexpr (!kHist) {
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
         if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
         const uint32_t d = g - spos[e];
         if (d > max_dist || best >= limit) break;
-        const uint32_t pc = jb.parts ? part_cap(jb.abs_base + p, d) : ~0u;   // part index: lagging source
+        const uint32_t pc = parts ? part_cap(pA, d, pbits, plag) : ~0u;   // part index: lagging source
         if (pc <= best) continue;
         const uint64_t x0 = mine0 ^ spre[0][e];
         uint32_t len;
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
 #define TAKE(d_, len_, DONE)                                               \
     do {                                                                     \
       const uint32_t l_ = min(min((len_), limit),                            \
-                              jb.parts ? part_cap(jb.abs_base + p, (d_)) : ~0u); \
+                              parts ? part_cap(pA, (d_), pbits, plag) : ~0u);   \
       if (l_ > best) {                                                       \
         best = l_;                                                           \
         if (cnt == kMaxMatches) {                                            \
@@ -286,13 +290,16 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, keys, vals);
 }
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
-                         const uint32_t *svals, uint32_t total, int depth, bool hist, uint32_t *matches) {
-  if (hist)
-    hipLaunchKernelGGL(find_matches_kernel<true>, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, pos_job, skeys,
-                       svals, total, depth, matches);
+                         const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches) {
+  const dim3 g((total + kTile - 1) / kTile), b(kTile);
+  if (hist && parts)
+    hipLaunchKernelGGL((find_matches_kernel<true, true>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
+  else if (hist)
+    hipLaunchKernelGGL((find_matches_kernel<true, false>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
+  else if (parts)
+    hipLaunchKernelGGL((find_matches_kernel<false, true>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
   else
-    hipLaunchKernelGGL(find_matches_kernel<false>, dim3((total + kTile - 1) / kTile), dim3(kTile), 0, st, jobs, pos_job, skeys,
-                       svals, total, depth, matches);
+    hipLaunchKernelGGL((find_matches_kernel<false, false>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
 }
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total) {

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
   const uint8_t *data = nullptr;
   int ndirect = 0, npostfix = 0;
-  uint32_t parts = 0, abs0 = 0;
+  uint32_t parts = 0, abs0 = 0, pbits = 16, plag = 0;
   if (sgi < nsegs) {
     const Seg &sg = segs[sgi];
     const Job &jb = jobs[sg.job];
@@ -154,6 +154,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     npostfix = (int)jb.npostfix;
     parts = jb.parts;
     abs0 = jb.abs_base;
+    pbits = jb.part_bits;
+    plag = jb.part_lag;
   }
   if (__ballot(a < b) == 0) return;
   // literal costs from the stream's order-0 histogram (zopfli-cost-model.ts:163-189)
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
             break;
           }
           fl = min(fl, cap);
-          if (parts) fl = min(fl, part_cap(abs0 + i, fd));   // (>= the record's length)
+          if (parts) fl = min(fl, part_cap(abs0 + i, fd, pbits, plag));   // (>= the record's length)
         }
         const int cc = copy_code(fl);
         const bool last = fd == ld;

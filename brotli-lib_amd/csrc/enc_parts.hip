@@ -74,7 +74,8 @@ __global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, con
   h.magic = kPartMagic;
   h.version = 1;
   h.entry_bytes = (uint16_t)sizeof(PartEntry);
-  h.nentries = jb.nseg;
+  const uint32_t every = 1u << (jb.part_bits - kSegBits);   // segments per part
+  h.nentries = (jb.nseg + every - 1) / every;
   h.lgwin = jb.lgwin;
   h.next_byte = jb.final_ ? 0 : jb.out_base + ((jb.total_bits + 7) >> 3);
   h.total = (uint64_t)jb.abs_base + jb.n;
@@ -108,9 +109,11 @@ __global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, con
       const uint32_t p12 = prev2(jb, p);
       e.p1 = (uint8_t)(p12 & 0xFF);
       e.p2 = (uint8_t)(p12 >> 8);
-      const uint8_t *eb = reinterpret_cast<const uint8_t *>(&e);
-      uint8_t *dst = ent + (size_t)(s - jb.seg_base) * sizeof(PartEntry);
-      for (int i = 0; i < (int)sizeof(e); i++) dst[i] = eb[i];
+      if ((s - jb.seg_base) % every == 0) {   // a part starts at this segment
+        const uint8_t *eb = reinterpret_cast<const uint8_t *>(&e);
+        uint8_t *dst = ent + (size_t)((s - jb.seg_base) / every) * sizeof(PartEntry);
+        for (int i = 0; i < (int)sizeof(e); i++) dst[i] = eb[i];
+      }
       // the segment's distance pushes and block-split units, in stream order
       const PushSum &ps = push[s];
       if (ps.n >= 4) {

@@ -140,6 +140,21 @@ uint64_t part_min_stream() {
   }();
   return v;
 }
+uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
+  const char *e = getenv(name);
+  if (!e) return dflt;
+  const unsigned long v = strtoul(e, nullptr, 10);
+  return (uint32_t)std::max<unsigned long>(lo, std::min<unsigned long>(hi, v));
+}
+// part size (log2) and source lag (MIB_PART_BITS / MIB_PART_LAG override, for experiments)
+uint32_t part_bits() {
+  static uint32_t v = env_u32("MIB_PART_BITS", kPartBits, kSegBits, 22);
+  return v;
+}
+uint32_t part_lag() {
+  static uint32_t v = env_u32("MIB_PART_LAG", kPartLag, 0, 1u << 20);
+  return v;
+}
 bool wants_parts(const StreamDesc &d) {
   const uint64_t lim = part_min_stream();
   if (lim == 0 || d.n <= kSeg) return false;
@@ -171,7 +186,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   std::vector<Mb> mbs;
   std::vector<uint32_t> seg_job;   // per 64 KiB of global positions: its stream
   uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0;
-  bool any_hist = false;
+  bool any_hist = false, any_parts = false;
   for (size_t j = 0; j < k; j++) {
     Job &jb = jobs[j];
     memset(&jb, 0, sizeof(jb));
@@ -192,9 +207,12 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     if (jb.hist_tab) any_hist = true;
     jb.out_base = sd[j].out_base;
     jb.parts = (!jb.uncompressed && wants_parts(sd[j])) ? 1 : 0;
+    if (jb.parts) any_parts = true;
     uint64_t idx_extra = 0;
     if (jb.parts) {
-      const uint64_t nseg_j = (n + kSeg - 1) / kSeg;
+      jb.part_bits = part_bits();
+      jb.part_lag = part_lag();
+      const uint64_t nseg_j = (n + (1ull << jb.part_bits) - 1) >> jb.part_bits;
       jb.idx_payload = (uint32_t)(sizeof(PartHead) + nseg_j * sizeof(PartEntry));
       jb.idx_bits = part_index_bits(jb.hdr_lgwin ? window_bits_len((int)jb.hdr_lgwin) : 0, jb.idx_payload);
       idx_extra = jb.idx_payload + 16;
@@ -319,7 +337,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, key_bits, st));
     tm.stop();
     tm.start("find_matches");
-    launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, any_hist, matches);
+    launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, any_hist, any_parts, matches);
     if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
     tm.stop();
     tm.start("lit_histo");

@@ -26,7 +26,7 @@
 namespace mib {
 
 constexpr uint32_t kPartMagic = 0x3170424Du;     // "MBp1"
-constexpr uint32_t kPartSeg = 1u << 16;          // part granularity: the encoder's parse segment
+constexpr uint32_t kPartBits = 18;               // part size: 256 KiB (a multiple of the encoder's 64 KiB parse segment)
 constexpr uint32_t kPartLag = 4096;              // an external copy source ends this far behind
                                                  // the destination's offset in its segment
 constexpr uint32_t kPartPublish = 2048;          // a part publishes its progress this often (bytes)
