@@ -91,6 +91,7 @@ struct Seg {
   uint32_t prev_dist;         // carry: the decoder's last distance when the segment starts
   uint32_t extra_ins;         // carry: trailing insert-only command of the metablock (0: none)
   uint32_t pad;
+  uint32_t ring_in[4];        // ring_scan: the decoder's distance ring at the segment start, most recent first
   uint64_t bit_off;           // offsets: stream-relative bit position
   uint64_t bits;              // sizes
 };
@@ -205,6 +206,19 @@ __device__ __forceinline__ uint32_t dist_prefix(uint32_t dcode, int ndirect, int
   uint32_t nbits = (uint32_t)(bucket - npostfix);
   *extra = (dist - offset) >> npostfix;
   return (nbits << 10) | (16 + (uint32_t)ndirect + ((2 * (nbits - 1) + prefix) << npostfix) + postfix);
+}
+
+// The distance code of a copy at distance d given the decoder's ring r (most recent first)
+// when d is not the last distance: a short code 1-15 when d is in the ring or within 3 of its
+// first two entries (RFC 7932 section 4; engine.ts DISTANCE_SHORT_CODE_*), else d + 15.
+__device__ __forceinline__ uint32_t short_code(uint32_t d, const uint32_t *r) {
+  if (d == r[1]) return 1;
+  if (d == r[2]) return 2;
+  if (d == r[3]) return 3;
+  const int64_t a = (int64_t)d - (int64_t)r[0], b = (int64_t)d - (int64_t)r[1];
+  if (a >= -3 && a <= 3 && a != 0) return a < 0 ? (uint32_t)(4 + 2 * (-a - 1)) : (uint32_t)(5 + 2 * (a - 1));
+  if (b >= -3 && b <= 3 && b != 0) return b < 0 ? (uint32_t)(10 + 2 * (-b - 1)) : (uint32_t)(11 + 2 * (b - 1));
+  return d + 15;
 }
 
 __device__ __forceinline__ uint32_t pack_match(uint32_t dist, uint32_t len) {
@@ -384,6 +398,7 @@ void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const
                  uint8_t *out);
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out);
 struct PushSum;
+void launch_ring_scan(hipStream_t st, Job *jobs, int njobs, Seg *segs, int nsegs, const RawCmd *raw, PushSum *push);
 void launch_part_index(hipStream_t st, const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, int nsegs,
                        const Cmd *cmds, const Unit *units, PushSum *push, uint8_t *out);
 size_t part_push_bytes();

@@ -95,6 +95,8 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
   __shared__ ItemMap<kBlock> map;
   __shared__ uint32_t sh_pos[kBlock];
   __shared__ uint8_t sh_unit[kBlock];
+  __shared__ uint32_t sh_push[kBlock];   // the batch's pushed distances, by rank
+  __shared__ uint32_t sh_ring[4];        // the ring before the batch, most recent first
   const Seg sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
@@ -105,6 +107,7 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
     sh_first[t / 3][t % 3] = ~0u;
   }
   if (t == 0) sh_run = sg.start - sg.carry_in;
+  if (t < 4) sh_ring[t] = sg.ring_in[t];
   __syncthreads();
   const RawCmd *r = raw + sg.cmd_off;
   Cmd *out = cmds + sg.cmd_off;
@@ -125,7 +128,21 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
     uint32_t off, total;
     Scan(scan_tmp).ExclusiveSum(ins + len, off, total);
     const uint32_t pos = sh_run + off;
+    // the decoder's distance ring before this command: pushes of the batch before it (by
+    // rank), then the ring the batch started with
+    const uint32_t push = (q < nraw && d != prevd) ? 1u : 0u;
+    uint32_t rank, npush;
     __syncthreads();
+    Scan(scan_tmp).ExclusiveSum(push, rank, npush);
+    if (push) sh_push[rank] = d;
+    __syncthreads();
+    uint32_t ring[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) ring[k] = (int)rank - 1 - k >= 0 ? sh_push[rank - 1 - k] : sh_ring[k - rank];
+    uint32_t ring_after = 0;   // the ring after the batch
+    if (t < 4) ring_after = (int)npush - 1 - t >= 0 ? sh_push[npush - 1 - t] : sh_ring[t - npush];
+    __syncthreads();
+    if (t < 4) sh_ring[t] = ring_after;
     if (t == 0) sh_run += total;
     if (q < n) {
       Cmd c;
@@ -138,7 +155,7 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
       const uint32_t u = unit_of(sg, pos);
       uint32_t *hu = sh_h + u * kSubHist;
       if (len) {
-        const uint32_t dcode = d == prevd ? 0 : d + 15;
+        const uint32_t dcode = d == prevd ? 0 : short_code(d, ring);
         uint32_t extra;
         const uint32_t dp = dist_prefix(dcode, (int)jb.ndirect, (int)jb.npostfix, &extra);
         c.dist_extra = extra;

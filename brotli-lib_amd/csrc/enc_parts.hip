@@ -51,6 +51,68 @@ __global__ __launch_bounds__(64) void part_push_kernel(const Job *jobs, const Se
   if (lane == 0) out[blockIdx.x] = ps;
 }
 
+// The decoder's distance ring at every segment start (codes_kernel then picks short distance
+// codes 1-15 from it, RFC 7932 section 4): the raw commands' pushes per segment -- a copy
+// pushes its distance unless it equals the previous copy's (code 0) -- then a lane per stream
+// walks its segments.  Every non-zero distance code pushes, so the ring does not depend on
+// which of them a command ends up with.
+__global__ __launch_bounds__(64) void raw_push_kernel(const Job *jobs, const Seg *segs, const RawCmd *raw, PushSum *out) {
+  const Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  const int lane = threadIdx.x;
+  PushSum ps;
+  ps.n = 0;
+  for (int q = 0; q < 4; q++) ps.d[q] = 0;
+  if (jb.uncompressed) {
+    if (lane == 0) out[blockIdx.x] = ps;
+    return;
+  }
+  const RawCmd *c = raw + sg.cmd_off;
+  const int64_t n = sg.ncmd;
+  uint32_t got = 0, total = 0;
+  for (int64_t hi = n; hi > 0; hi -= 64) {
+    const int64_t q = hi - 64 + lane;
+    bool push = false;
+    uint32_t d = 0;
+    if (q >= 0) {
+      d = c[q].dist;
+      push = d != (q ? c[q - 1].dist : sg.prev_dist);
+    }
+    uint64_t m = __ballot(push);
+    total += (uint32_t)__popcll(m);
+    while (m && got < 4) {
+      const int l = 63 - __clzll((long long)m);
+      ps.d[got++] = (uint32_t)__builtin_amdgcn_readlane((int)d, l);
+      m &= ~(1ull << l);
+    }
+  }
+  ps.n = total;
+  if (lane == 0) out[blockIdx.x] = ps;
+}
+__global__ void ring_scan_kernel(Job *jobs, int njobs, Seg *segs, const PushSum *push) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= njobs) return;
+  const Job &jb = jobs[j];
+  if (jb.uncompressed) return;
+  uint32_t ring[4];
+  for (int q = 0; q < 4; q++) ring[q] = (uint32_t)jb.dc_in[q];
+  for (uint32_t s = jb.seg_base; s < jb.seg_base + jb.nseg; s++) {
+    for (int q = 0; q < 4; q++) segs[s].ring_in[q] = ring[q];
+    const PushSum &ps = push[s];
+    if (ps.n >= 4) {
+      for (int q = 0; q < 4; q++) ring[q] = ps.d[q];
+    } else if (ps.n) {
+      uint32_t r[4];
+      for (uint32_t q = 0; q < 4; q++) r[q] = q < ps.n ? ps.d[q] : ring[q - ps.n];
+      for (int q = 0; q < 4; q++) ring[q] = r[q];
+    }
+  }
+}
+void launch_ring_scan(hipStream_t st, Job *jobs, int njobs, Seg *segs, int nsegs, const RawCmd *raw, PushSum *push) {
+  hipLaunchKernelGGL(raw_push_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, raw, push);
+  hipLaunchKernelGGL(ring_scan_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, push);
+}
+
 // Lane per stream: the entries in stream order, then the metadata block (window bits, header,
 // payload) at the front of the stream's output slice.
 __global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, const Unit *units,

@@ -351,6 +351,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.stop();
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
+    launch_ring_scan(st, d_jobs, (int)k, d_segs, nsegs, raw, push);
     launch_context_mode(st, d_jobs, d_mbs, nmbs);
     launch_codes(st, d_jobs, d_segs, d_mbs, nsegs, raw, cmds, cmd_pos, units, unit_h);
     launch_dist_ring(st, d_jobs, (int)k, d_segs, cmds);
