@@ -11,6 +11,8 @@ resident in HBM when the timed region starts):
   c5            C5's shape per GPU: one stream streamed through BrotliEncoder.update() in 1 MiB
                 chunks (history window carried on the device), q9 lgwin 24 TEXT, then decoded
                 (64 MiB by default: --size for more).
+  ref           decode of the reference's own bench streams (noto-tc etc.), one stream per
+                call: the single-stream latency case of the reference's README.
 A step encodes the batch (mib_ctx_encode: packed compressed streams in HBM), gathers the
 compressed shards to rank 0 over RCCL (N > 1, c3/c4; the only collective)
 and decodes them back (mib_ctx_decode) into HBM.  The round trip is checked bit-exact on
@@ -62,7 +64,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--workload', default='c4', choices=sorted(WORKLOADS))
+    ap.add_argument('--workload', default='c4', choices=sorted(WORKLOADS) + ['ref'])
     ap.add_argument('--streams', type=int, default=-1, help='buffers per GPU (-1: the workload\'s)')
     ap.add_argument('--size', type=int, default=-1, help='bytes per buffer (-1: the workload\'s)')
     ap.add_argument('--quality', type=int, default=11)
@@ -250,6 +252,87 @@ def run_stream(args, rank, world, local):
         dist.destroy_process_group()
 
 
+# The reference's own bench streams (tests/golden/bench, bench/fixtures of the reference) and
+# its decode times: README.md:79-82 (Apple M2 Max, Node 22) and SURVEY.md §6 (the survey
+# host: Xeon, Node 12, 1 thread).
+REF_STREAMS = [('enc-ttf', 2.3, 5.6), ('enc-otf', 2.2, 4.2), ('enc-var-ttf', 5.8, 10.6), ('noto-tc', 47.0, 85.9),
+               ('html-content', None, None), ('random-binary', None, None)]
+
+
+def run_ref(args):
+    """ref leg: decode each of the reference's bench streams ALONE (one stream per call, input
+    and output in HBM: single-stream latency, the case the reference's README times), then all
+    of them in one call; the oracle decodes the same streams on one host core."""
+    import torch
+    import brotli_amd
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    dev = torch.device('cuda', 0)
+    ctx = brotli_amd.DeviceContext(0, profiling=True)
+    gold = os.path.join(ROOT, 'tests', 'golden', 'bench')
+    streams = []
+    for name, m2, host in REF_STREAMS:
+        with open(os.path.join(gold, name + '.br'), 'rb') as f:
+            enc = f.read()
+        n = brotli_amd.brotliDecodedSize(enc)
+        if n <= 0:
+            n = len(brotli_amd.brotliDecode(enc))
+        streams.append((name, m2, host, enc, n))
+    per = []
+    tot_out, tot_s = 0, 0.0
+    for name, m2, host, enc, n in streams:
+        src = torch.tensor(list(enc), dtype=torch.uint8, device=dev)
+        out = torch.empty(n + 4096, dtype=torch.uint8, device=dev)
+        for _ in range(max(1, args.warmup)):
+            sizes, st = ctx.decode(src.data_ptr(), [0, len(enc)], out.data_ptr(), [0, n + 4096])
+        assert st == [0] and sizes == [n], (name, st, sizes)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        kern = 0.0
+        for _ in range(args.steps):
+            ctx.decode(src.data_ptr(), [0, len(enc)], out.data_ptr(), [0, n + 4096])
+            kern += sum(ms for nm, (ms, c) in ctx.kernel_times().items() if nm.startswith('decode'))
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / args.steps
+        tot_out += n
+        tot_s += dt
+        per.append({'stream': name, 'out_bytes': n, 'in_bytes': len(enc), 'ms': round(dt * 1e3, 3),
+                    'kernel_ms': round(kern / args.steps, 3), 'MBps': round(n / dt / 1e6, 2),
+                    'ref_ms_m2max': m2, 'ref_ms_survey_host': host})
+    # all streams in one call (one wave each)
+    cat = b''.join(s[3] for s in streams)
+    ioff, ooff = [0], [0]
+    for s_ in streams:
+        ioff.append(ioff[-1] + len(s_[3]))
+        ooff.append(ooff[-1] + s_[4] + 4096)
+    src = torch.tensor(list(cat), dtype=torch.uint8, device=dev)
+    out = torch.empty(ooff[-1], dtype=torch.uint8, device=dev)
+    ctx.decode(src.data_ptr(), ioff, out.data_ptr(), ooff)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.decode(src.data_ptr(), ioff, out.data_ptr(), ooff)
+    torch.cuda.synchronize()
+    batch_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    cpu = None
+    if not args.no_cpu_baseline:
+        import _oracle
+        t0 = time.perf_counter()
+        for s_ in streams:
+            assert isinstance(_oracle.decode(s_[3]), bytes)
+        ct = time.perf_counter() - t0
+        cpu = {'value': round(tot_out / ct / 1e6, 3), 'unit': 'MB/s', 'cores': 1, 'kind': 'port',
+               'sample': 'the same %d streams, oracle decoder (reference decoder restated), one host thread, %.2f s'
+                         % (len(streams), ct)}
+    print(json.dumps({
+        'metric': 'decode MB/s of the reference bench streams (single stream per call)', 'value': round(tot_out / tot_s / 1e6, 3),
+        'unit': 'MB/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(tot_s * 1e3, 3),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'reference fixtures',
+        'config': {'workload': 'decode of the reference bench streams (tests/golden/bench/*.br), one stream per call, '
+                               'input/output in HBM', 'name': 'ref', 'parallelism': 'replicas1'},
+        'streams': per, 'all_streams_one_call_ms': round(batch_ms, 3), 'roofline': None, 'cpu_baseline': cpu}),
+          flush=True)
+
+
 def datagen_device(total, seed, dev):
     from brotli_amd import datagen
     return datagen.enwik_device(total, seed, dev)
@@ -258,6 +341,8 @@ def datagen_device(total, seed, dev):
 def main():
     args = parse()
     wl = args.workload
+    if wl == 'ref':
+        return run_ref(args)
     if wl == 'c5':
         return run_stream(args, int(os.environ.get('RANK', '0')), int(os.environ.get('WORLD_SIZE', '1')),
                           int(os.environ.get('LOCAL_RANK', '0')))

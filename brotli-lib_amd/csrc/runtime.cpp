@@ -186,7 +186,11 @@ bool plan_parts(Fetch &fetch, uint64_t n, PartPlan &plan) {
   for (int guard = 0; guard < (1 << 16); guard++) {
     if (!read_part_index(fetch, at, plan, &next)) {
       if (at == 0) return false;
-      break;   // a chunk without an index: the last part decodes through it
+      // BrotliEncoder.finish() with nothing pending adds only the final empty metablock
+      // (ISLAST, ISLASTEMPTY: one byte 0x03): the chain is complete
+      uint8_t b = 0;
+      if (n - at == 1 && fetch(at, 1, &b) && b == 0x03) next = 0;
+      break;
     }
     if (next == 0) break;
     if (next <= at || next >= n) return false;

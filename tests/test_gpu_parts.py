@@ -137,6 +137,20 @@ def test_streaming_chunks_carry_chained_indexes():
     assert brotli_amd.part_stats() == (p0 + 1, f0)
 
 
+def test_streaming_exact_chunks_then_empty_finish():
+    # the chunks use up the input exactly: finish() only adds the final empty metablock
+    data = datagen.enwik_text(16 << 20, 11)
+    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'mode': 1})
+    parts = [e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)]
+    tail = e.finish()
+    assert tail == b'\x03'
+    enc = b''.join(parts) + tail
+    p0, f0 = brotli_amd.part_stats()
+    assert brotli_amd.brotliDecode(enc) == data
+    assert brotli_amd.part_stats() == (p0 + 1, f0)
+    assert _oracle.decode(enc) == data
+
+
 @pytest.mark.skipif(shutil.which('node') is None, reason='node not installed')
 def test_native_brotli_decodes_indexed_stream(tmp_path):
     data, enc = _enwik_stream(3 << 20, 2)
