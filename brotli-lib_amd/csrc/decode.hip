@@ -1763,14 +1763,20 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       int fl0 = pos;
       uint32_t ob = 0;
       const int end = pos + insert_len;
+      // literals are gathered one per lane (lane pos & 63) and stored a
+      // 64-byte line at a time; the inner loops run to the next line end, so the line check
+      // is not paid per literal
       if (kTrivial) {
         while (pos < end) {
-          fill();
-          const int val = sym16(lit_root);
-          ob = lane == (pos & 63) ? (uint32_t)val : ob;
-          pos++;
-          c2b = c1;
-          c1 = val;
+          const int seg_end = U(min(end, (pos | 63) + 1));
+          while (pos < seg_end) {
+            fill();
+            const int val = sym16(lit_root);
+            ob = lane == (pos & 63) ? (uint32_t)val : ob;
+            pos++;
+            c2b = c1;
+            c1 = val;
+          }
           if ((pos & 63) == 0) {
             const int p = (fl0 & ~63) + lane;
             if (p >= fl0) ring[p] = (uint8_t)ob;
@@ -1780,15 +1786,18 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       } else {
         int root = U((int)g_lds.ctx_root[(lut1_of(c2b) << 8) | c1]);
         while (pos < end) {
-          // the root row of the next literal (its p2 is the current c1), 4 entries per lane
-          const uint64_t row = croot64[(lut1_of(c1) << 6) | lane];
-          fill();
-          c2b = c1;
-          c1 = U(sym16(root));
-          const uint64_t e = c1 & 2 ? row >> 32 : row;   // lane c1 >> 2 holds entries 4 (c1 >> 2) ..
-          root = __builtin_amdgcn_readlane((int)(uint32_t)(e >> (16 * (c1 & 1))), c1 >> 2) & 0xFFFF;
-          ob = lane == (pos & 63) ? (uint32_t)c1 : ob;
-          pos++;
+          const int seg_end = U(min(end, (pos | 63) + 1));
+          while (pos < seg_end) {
+            // the root row of the next literal (its p2 is the current c1), 4 entries per lane
+            const uint64_t row = croot64[(lut1_of(c1) << 6) | lane];
+            fill();
+            c2b = c1;
+            c1 = U(sym16(root));
+            const uint64_t e = c1 & 2 ? row >> 32 : row;   // lane c1 >> 2 holds entries 4 (c1 >> 2) ..
+            root = __builtin_amdgcn_readlane((int)(uint32_t)(e >> (16 * (c1 & 1))), c1 >> 2) & 0xFFFF;
+            ob = lane == (pos & 63) ? (uint32_t)c1 : ob;
+            pos++;
+          }
           if ((pos & 63) == 0) {
             const int p = (fl0 & ~63) + lane;
             if (p >= fl0) ring[p] = (uint8_t)ob;

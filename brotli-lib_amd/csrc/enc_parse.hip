@@ -46,14 +46,14 @@ __device__ unsigned long long g_dp_prof[8];
 #define DPMARK(slot) do {} while (0)
 #define DPCOUNT(slot, v) do {} while (0)
 #endif
-constexpr int kS = 2;                 // segments per wave
-constexpr int kL = 64 / kS;           // lanes per segment
-constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
+// kS is a template parameter: 2 segments per wave (32 lanes each) for batches with enough
+// segments to fill the chip, 1 (64 lanes) when there are fewer waves than SIMDs (one long
+// stream): a step then relaxes twice the lengths per instruction on a wave that would
+// otherwise share its SIMD with nothing.
 constexpr int kDpWaves = 4;           // waves per workgroup, sharing the length table
 constexpr int kLenTab = kLongCopy + 1;
 constexpr float kInf = 3.0e38f;
 constexpr uint32_t kCostLast = 255;   // cost code of a match at the path's last distance
-static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
 
 typedef const __attribute__((address_space(1))) uint8_t GCU8;
 
@@ -114,9 +114,15 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lane_src << 2), (int)v);
 }
 
+template <int KS>
 __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const uint32_t *matches,
                                                            uint64_t *choice /* per position+1 */) {
+  constexpr int kS = KS;                // segments per wave
+  constexpr int kL = 64 / kS;           // lanes per segment
+  constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
+  static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
+  constexpr uint64_t kLaneMask = kL == 64 ? ~0ull : ((1ull << kL) - 1);
   __shared__ uint32_t lentab[24 * kLenTab];   // (insert code, length) -> fp16 (explicit distance) | fp16 (short code 0) << 16
   __shared__ float litc_all[kDpWaves * kS][256];
   __shared__ StageEnt stg_all[kDpWaves][64];
@@ -285,12 +291,12 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
           for (;;) {
             const uint32_t x = fl + hl;
             const uint64_t okb = __ballot(x < cap && cp[x] == sp[x]);
-            const uint32_t ok = (uint32_t)(okb >> hbase) & (uint32_t)((1ull << kL) - 1);
-            if (ok == (uint32_t)((1ull << kL) - 1)) {
+            const uint64_t ok = (okb >> hbase) & kLaneMask;
+            if (ok == kLaneMask) {
               fl += kL;
               continue;
             }
-            fl += (uint32_t)__ffs(~ok) - 1;
+            fl += (uint32_t)__ffsll((unsigned long long)~ok) - 1;
             break;
           }
           fl = min(fl, cap);
@@ -492,8 +498,13 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 #endif
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                const uint32_t *matches, uint64_t *choice) {
-  hipLaunchKernelGGL(dp_kernel, dim3((nsegs + kDpWaves * kS - 1) / (kDpWaves * kS)), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h, matches,
-                     choice);
+  // 1024 SIMDs (256 CUs x 4): with fewer than two segments per SIMD a wave takes one segment
+  if (nsegs < 2048)
+    hipLaunchKernelGGL(dp_kernel<1>, dim3((nsegs + kDpWaves - 1) / kDpWaves), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs,
+                       lit_h, matches, choice);
+  else
+    hipLaunchKernelGGL(dp_kernel<2>, dim3((nsegs + kDpWaves * 2 - 1) / (kDpWaves * 2)), dim3(64 * kDpWaves), 0, st, jobs,
+                       segs, nsegs, lit_h, matches, choice);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {
   hipLaunchKernelGGL(backtrack_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, nsegs, choice, raw);

@@ -104,6 +104,7 @@ def _L():
                                        ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int), ctypes.c_void_p]
         lib.mib_ctx_kernel_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(_KTime), ctypes.c_int]
         lib.mib_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        lib.mib_woff2_transform_glyf.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
         lib.mib_part_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         _lib = lib
     return _lib
@@ -252,6 +253,17 @@ def decode_batch(buffers):
     if rc:
         raise _err(rc)
     return [(_take(outs[i]) if st[i] == 0 else _err(st[i])) for i in range(k)]
+
+
+def woff2_transform_glyf(ttf):
+    """The WOFF2-transformed 'glyf' table of a TrueType font (W3C WOFF2 section 5.1), computed on
+    the GPU: the FONT-mode input of brotliEncode for a WOFF2 writer (reference README.md:63)."""
+    data = _bytes(ttf)
+    buf = _Buf()
+    rc = _L().mib_woff2_transform_glyf(data, len(data), ctypes.byref(buf))
+    if rc:
+        raise _err(rc)
+    return _take(buf)
 
 
 def part_stats(ctx=None):

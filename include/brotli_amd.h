@@ -111,6 +111,13 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
 typedef struct { char name[32]; double ms; uint32_t launches; } mib_kernel_time;
 int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max);
 void mib_ctx_set_profiling(mib_ctx *c, int on);
+/* WOFF2 'glyf' transform (the FONT-mode caller, reference README.md:63;
+ * W3C WOFF2 section 5.1): the glyf + loca tables of the TrueType font `ttf` become the
+ * transformed glyf table (header, the seven streams, the overlap-simple bitmap), byte for
+ * byte what fontTools' WOFF2GlyfTable.transform produces.  MIB_E_INVALID_ARG for a font
+ * without glyf / loca / head / maxp or with a malformed glyph. */
+int mib_woff2_transform_glyf(const uint8_t *ttf, size_t n, mib_buf *out);
+
 /* Part-parallel decoding (streams this encoder marked with a part index):
  * how many streams a context (NULL: the default one) decoded part-parallel, and how many of
  * those it sent back to the serial decoder because a part did not check out. Diagnostic. */
