@@ -131,6 +131,15 @@ struct Cmd {                  // one command with its prefix codes (command.ts:2
 
 struct RawCmd { uint32_t ins, len, dist; };
 
+// The parse's second-iteration prices (ZopfliCostModel.setFromCommands,
+// zopfli-cost-model.ts:68-159): bits per literal, command code and distance code from the
+// first parse's commands, one model per stream
+struct CostModel {
+  float lit[256];
+  float cmd[704];
+  float dist[128];
+};
+
 struct Codes {   // per metablock Huffman codes by slot, and the block-switch codes
   uint8_t ld[kLitSlots][256];
   uint16_t lc[kLitSlots][256];
@@ -376,7 +385,10 @@ void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_jo
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total);
-void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
+size_t cost_model_hist_bytes(int njobs);
+void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,
+                       uint32_t *hist, CostModel *model);
+void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
                const uint32_t *matches, uint64_t *choice);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);

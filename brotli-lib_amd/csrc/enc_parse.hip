@@ -27,9 +27,9 @@ namespace enc {
 // Node i is fetched with ds_bpermute from its lane; at a batch end the segment's chunks move
 // down by one (chunk 0 is all consumed nodes).
 //
-// The length-dependent half of a copy's price (copy code, its extra bits, the command
-// code it forms with the insert code, with and without short code 0) comes from an LDS
-// table indexed by (insert code, length), fp16 pairs, built once per workgroup.
+// The length-dependent half of a copy's price (its copy code's extra bits, the command code
+// it forms with the insert code, with and without short code 0) comes from a per-segment LDS
+// table indexed by (insert code, copy code), fp16 pairs, and a length -> copy code table.
 // Per-position inputs (matches, distance-cost codes, literal cost) are staged one lane per
 // position into LDS, loaded a batch ahead, and read back with one broadcast read per
 // segment; the batch's choices are collected per lane and stored as one coalesced write.
@@ -65,12 +65,16 @@ __device__ __forceinline__ uint32_t ins_extra(int ic) {
 // iteration-0 cost model (zopfli-cost-model.ts: costCmd = log2(11 + code), costDist = log2(20 + code))
 __device__ __forceinline__ float cmd_cost(int cmd) { return __builtin_amdgcn_logf(11.f + (float)cmd); }
 __device__ __forceinline__ float dist_sym_cost(uint32_t code) { return __builtin_amdgcn_logf(20.f + (float)min(code, 127u)); }
-// the length-dependent price of a copy of length l after insert code ic: with an explicit
-// distance (its symbol cost added by the caller), and with short code 0 (complete)
-__device__ __forceinline__ float copy_price(int ic, uint32_t l, bool last, float dist0) {
-  const int cc = copy_code(l);
+// the second iteration's prices come from the workgroup's CostModel (null: iteration 0)
+__device__ __forceinline__ float cmd_price(int cmd, const CostModel *cm) { return cm ? cm->cmd[cmd] : cmd_cost(cmd); }
+__device__ __forceinline__ float dist_price(uint32_t code, const CostModel *cm) {
+  return cm ? cm->dist[min(code, 127u)] : dist_sym_cost(code);
+}
+// the length-dependent price of a copy with copy code cc after insert code ic: with an
+// explicit distance (its symbol cost added by the caller), and with short code 0 (complete)
+__device__ __forceinline__ float copy_price(int ic, int cc, bool last, float dist0, const CostModel *cm) {
   const int cmd = combine_codes(ic, cc, last);
-  return (float)copy_extra(cc) + cmd_cost(cmd) + (last && cmd >= 128 ? dist0 : 0.f);
+  return (float)copy_extra(cc) + cmd_price(cmd, cm) + (last && cmd >= 128 ? dist0 : 0.f);
 }
 
 // ins_code / ins_extra (command.ts:29-64) without branches: the node's insert length is
@@ -116,33 +120,26 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
 
 template <int KS>
 __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
-                                                           const uint32_t *lit_histo, const uint32_t *matches,
+                                                           const uint32_t *lit_histo, const CostModel *model,
+                                                           const uint32_t *matches,
                                                            uint64_t *choice /* per position+1 */) {
   constexpr int kS = KS;                // segments per wave
   constexpr int kL = 64 / kS;           // lanes per segment
   constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
   static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
   constexpr uint64_t kLaneMask = kL == 64 ? ~0ull : ((1ull << kL) - 1);
-  __shared__ uint32_t lentab[24 * kLenTab];   // (insert code, length) -> fp16 (explicit distance) | fp16 (short code 0) << 16
+  __shared__ uint32_t ptab_all[kDpWaves * kS][24 * 24];   // per segment: (insert code, copy code) -> fp16 (explicit distance) | fp16 (short code 0) << 16
+  __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
   __shared__ float litc_all[kDpWaves * kS][256];
   __shared__ StageEnt stg_all[kDpWaves][64];
-  const float dist0 = dist_sym_cost(0);
-  for (int t = threadIdx.x; t < 24 * kLenTab; t += 64 * kDpWaves) {
-    const int ic = t / kLenTab;
-    const uint32_t l = (uint32_t)(t % kLenTab);
-    uint32_t v = 0;
-    if (l >= 4) {
-      const _Float16 a = (_Float16)copy_price(ic, l, false, dist0), b = (_Float16)copy_price(ic, l, true, dist0);
-      v = (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
-    }
-    lentab[t] = v;
-  }
+  for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 4 ? copy_code((uint32_t)t) : 0);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t h = lane / kL, hl = lane % kL, hbase = h * kL;
   const int sgi = (blockIdx.x * kDpWaves + (int)w) * kS + (int)h;
   StageEnt *stg = stg_all[w];
   float *litc = litc_all[w * kS + h];
+  uint32_t *ptab = ptab_all[w * kS + h];
   // this lane group's segment (a = b: nothing to parse)
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
   const uint8_t *data = nullptr;
@@ -164,8 +161,23 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     plag = jb.part_lag;
   }
   if (__ballot(a < b) == 0) return;
-  // literal costs from the stream's order-0 histogram (zopfli-cost-model.ts:163-189)
-  {
+  // prices: iteration 0 from zopfli-cost-model.ts's initial model, iteration 1 from the
+  // stream's CostModel (per segment tables: a wave's segments may be different streams)
+  const CostModel *cm = (model && a < b) ? model + job : nullptr;
+  const float dist0 = dist_price(0, cm);
+  if (a < b)
+    for (uint32_t t = hl; t < 24 * 24; t += kL) {
+      const int ic = (int)(t / 24), cc = (int)(t % 24);
+      const _Float16 x = (_Float16)copy_price(ic, cc, false, dist0, cm), y = (_Float16)copy_price(ic, cc, true, dist0, cm);
+      ptab[t] = (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+    }
+  // literal costs: iteration 0 from the stream's order-0 histogram (zopfli-cost-model.ts:
+  // 163-189), iteration 1 from the model
+  if (cm) {
+    if (a < b)
+      for (uint32_t k = hl; k < 256; k += kL)
+        litc[k] = (float)(uint32_t)(fminf(fmaxf(cm->lit[k], 1.f), 255.f) * 256.f) * (1.f / 256.f);
+  } else {
     uint32_t part = 0;
     if (a < b)
       for (uint32_t k = hl; k < 256; k += kL) part += lit_histo[job * 256 + k];
@@ -225,7 +237,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         const uint32_t ln = min(match_length(cur.m[q]), b - p);
         const uint32_t dp = dist_prefix(match_dist(cur.m[q]) + 15, ndirect, npostfix, &extra);
         e.m[q] = (ln << 24) | match_dist(cur.m[q]);
-        const float dc = (float)(dp >> 10) + dist_sym_cost(dp & 0x3FFu);
+        const float dc = (float)(dp >> 10) + dist_price(dp & 0x3FFu, cm);
         e.mc[q] = match_dist(cur.m[q]) | (min((uint32_t)(dc * 4.f + 0.5f), kCostLast - 1) << 24);
         maxlen = ln;
       }
@@ -305,7 +317,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         const int cc = copy_code(fl);
         const bool last = fd == ld;
         const int cmd = combine_codes(ic, cc, last);
-        const float fc = base + (float)copy_extra(cc) + cmd_cost(cmd) + (last ? (cmd < 128 ? 0.f : dist0) : fdc);
+        const float fc = base + (float)copy_extra(cc) + cmd_price(cmd, cm) + (last ? (cmd < 128 ? 0.f : dist0) : fdc);
         {
           const uint32_t p = i0 + hl;
           if (p <= i && p != a) choice[gbase + p] = choice_of(chd, chm);
@@ -337,7 +349,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
       vpk[q] = match_dist(pk) == ld ? (pk | (kCostLast << 24)) : pk;
     }
     const uint32_t maxrel = max(1u, maxlen);
-    const uint32_t *trow = lentab + ic * kLenTab;
+    const uint32_t *trow = ptab + ic * 24;
     // relax every edge out of i: lane j of chunk k takes length kL k + j - off
 #pragma unroll
     for (int c = 0; c < kC; c++) {
@@ -352,7 +364,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
 #pragma unroll
         for (int q = kMaxMatches - 1; q >= 0; q--)
           x = l <= mL[q] ? vpk[q] : x;   // mL = 0 past nm
-        const uint32_t tv = trow[l];
+        const uint32_t tv = trow[cctab[l]];
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
         const uint32_t cc = x >> 24;
@@ -488,6 +500,103 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
 }
 
 
+// ---------------------------------------------------------------- 5. second-iteration prices
+// ZopfliCostModel.setFromCommands + setCostFromHistogram (zopfli-cost-model.ts:68-159):
+// histograms of the first parse's literals, command codes and distance codes of a stream
+// (block per segment, merged into the stream's histogram), turned into bits per symbol
+// (missing symbols: log2 of the sum plus the number of missing symbols, + 2; present ones at
+// least 1 bit).  "Last distance" is the parse's notion: the previous copy of the segment.
+// A stream's model depends on its own bytes only, so a batch encodes each stream exactly as
+// a call of its own does.
+constexpr int kHistLen = 256 + 704 + 128;   // literals | commands | distances
+__global__ __launch_bounds__(256) void cmd_stats_kernel(const Job *jobs, const Seg *segs, const RawCmd *raw,
+                                                        uint32_t *hist /* kHistLen per job */) {
+  __shared__ uint32_t hs[kHistLen], scan[256];
+  uint32_t *hl = hs, *hc = hs + 256, *hd = hs + 256 + 704;
+  const uint32_t t = threadIdx.x;
+  for (uint32_t i = t; i < kHistLen; i += 256) hs[i] = 0;
+  __syncthreads();
+  const Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  const RawCmd *rc = raw + sg.cmd_off;
+  const uint32_t n = sg.ncmd;
+  uint32_t base = sg.start;
+  for (uint32_t q0 = 0; q0 < n; q0 += 256) {
+    const uint32_t q = q0 + t;
+    RawCmd c{0, 0, 0};
+    uint32_t prevd = 0;
+    if (q < n) {
+      c = rc[q];
+      prevd = q ? rc[q - 1].dist : 0u;
+    }
+    const uint32_t span = c.ins + c.len;
+    scan[t] = span;
+    __syncthreads();
+    for (uint32_t o = 1; o < 256; o <<= 1) {
+      const uint32_t v = t >= o ? scan[t - o] : 0u;
+      __syncthreads();
+      scan[t] += v;
+      __syncthreads();
+    }
+    const uint32_t pos = base + scan[t] - span, tot = scan[255];
+    __syncthreads();
+    if (q < n) {
+      const bool last = c.dist == prevd;
+      const int cmd = combine_codes(ins_code(c.ins), copy_code(c.len), last);
+      atomicAdd(&hc[cmd], 1u);
+      if (cmd >= 128) {
+        uint32_t extra;
+        const uint32_t code = last ? 0u : (dist_prefix(c.dist + 15, (int)jb.ndirect, (int)jb.npostfix, &extra) & 0x3FFu);
+        atomicAdd(&hd[min(code, 127u)], 1u);
+      }
+      for (uint32_t j = 0; j < c.ins; j++) atomicAdd(&hl[jb.data[pos + j]], 1u);
+    }
+    base += tot;
+  }
+  for (uint32_t p = sg.end - sg.tail_lits + t; p < sg.end; p += 256) atomicAdd(&hl[jb.data[p]], 1u);
+  __syncthreads();
+  for (uint32_t i = t; i < kHistLen; i += 256)
+    if (hs[i]) atomicAdd(&hist[(size_t)sg.job * kHistLen + i], hs[i]);
+}
+__global__ __launch_bounds__(256) void cost_model_kernel(const uint32_t *hist, CostModel *model) {
+  __shared__ uint32_t sums[5];   // literals, commands, distances, missing commands, missing distances
+  const uint32_t t = threadIdx.x;
+  const uint32_t *hl = hist + (size_t)blockIdx.x * kHistLen, *hc = hl + 256, *hd = hl + 256 + 704;
+  if (t < 5) sums[t] = 0;
+  __syncthreads();
+  {
+    uint32_t sc = 0, mc = 0, sd = 0, md = 0;
+    for (uint32_t i = t; i < 704; i += 256) {
+      sc += hc[i];
+      mc += hc[i] == 0;
+    }
+    if (t < 128) {
+      sd = hd[t];
+      md = hd[t] == 0;
+    }
+    atomicAdd(&sums[0], hl[t]);
+    atomicAdd(&sums[1], sc);
+    atomicAdd(&sums[2], sd);
+    atomicAdd(&sums[3], mc);
+    atomicAdd(&sums[4], md);
+  }
+  __syncthreads();
+  CostModel &m = model[blockIdx.x];
+  auto price = [](uint32_t h, float log2sum, float missing) { return h ? fmaxf(1.f, log2sum - log2f((float)h)) : missing; };
+  {
+    const float ls = log2f((float)max(sums[0], 1u));
+    m.lit[t] = price(hl[t], ls, ls + 2.f);
+  }
+  {
+    const float ls = log2f((float)max(sums[1], 1u)), miss = log2f((float)max(sums[1] + sums[3], 1u)) + 2.f;
+    for (uint32_t i = t; i < 704; i += 256) m.cmd[i] = price(hc[i], ls, miss);
+  }
+  if (t < 128) {
+    const float ls = log2f((float)max(sums[2], 1u)), miss = log2f((float)max(sums[2] + sums[4], 1u)) + 2.f;
+    m.dist[t] = price(hd[t], ls, miss);
+  }
+}
+
 #ifdef MIB_PROF
 extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dp_prof), sizeof(unsigned long long) * 8);
@@ -496,15 +605,28 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
   return 0;
 }
 #endif
-void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
+// dp_kernel<2> when there are enough segments to fill the chip (1024 SIMDs: 256 CUs x 4),
+// else dp_kernel<1>
+static int dp_ks(int nsegs) { return nsegs < 2048 ? 1 : 2; }
+static int dp_workgroups(int nsegs) {
+  const int spw = kDpWaves * dp_ks(nsegs);
+  return (nsegs + spw - 1) / spw;
+}
+void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
                const uint32_t *matches, uint64_t *choice) {
-  // 1024 SIMDs (256 CUs x 4): with fewer than two segments per SIMD a wave takes one segment
-  if (nsegs < 2048)
-    hipLaunchKernelGGL(dp_kernel<1>, dim3((nsegs + kDpWaves - 1) / kDpWaves), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs,
-                       lit_h, matches, choice);
+  if (dp_ks(nsegs) == 1)
+    hipLaunchKernelGGL(dp_kernel<1>, dim3(dp_workgroups(nsegs)), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h,
+                       model, matches, choice);
   else
-    hipLaunchKernelGGL(dp_kernel<2>, dim3((nsegs + kDpWaves * 2 - 1) / (kDpWaves * 2)), dim3(64 * kDpWaves), 0, st, jobs,
-                       segs, nsegs, lit_h, matches, choice);
+    hipLaunchKernelGGL(dp_kernel<2>, dim3(dp_workgroups(nsegs)), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h,
+                       model, matches, choice);
+}
+size_t cost_model_hist_bytes(int njobs) { return (size_t)njobs * kHistLen * 4; }
+void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,
+                       uint32_t *hist, CostModel *model) {
+  hipMemsetAsync(hist, 0, cost_model_hist_bytes(njobs), st);
+  hipLaunchKernelGGL(cmd_stats_kernel, dim3(nsegs), dim3(256), 0, st, jobs, segs, raw, hist);
+  hipLaunchKernelGGL(cost_model_kernel, dim3(njobs), dim3(256), 0, st, hist, model);
 }
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw) {
   hipLaunchKernelGGL(backtrack_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, nsegs, choice, raw);

@@ -155,6 +155,17 @@ uint32_t part_lag() {
   static uint32_t v = env_u32("MIB_PART_LAG", kPartLag, 0, 1u << 20);
   return v;
 }
+// zopfli iterations at quality 11 (MIB_ZOPFLI_ITERS overrides, for experiments)
+uint32_t zopfli_iterations() {
+  static uint32_t v = env_u32("MIB_ZOPFLI_ITERS", 2, 1, 2);
+  return v;
+}
+// bytes at the start of each segment the first iteration parses when it only feeds the
+// model (MIB_ZOPFLI_SAMPLE; >= 64 KiB parses whole segments)
+uint32_t zopfli_sample() {
+  static uint32_t v = env_u32("MIB_ZOPFLI_SAMPLE", 4096, 1024, kSeg);
+  return v;
+}
 bool wants_parts(const StreamDesc &d) {
   const uint64_t lim = part_min_stream();
   if (lim == 0 || d.n <= kSeg) return false;
@@ -276,6 +287,8 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += ns1 * kSubPerSeg * (sizeof(Unit) + kSubHist * 4);
   need += out_scratch + 64;
   need += ns1 * part_push_bytes();
+  const bool two_pass = prm.quality >= 11 && zopfli_iterations() > 1;   // backward-references-hq.ts:562-605
+  need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
   if (!ws) {
@@ -315,12 +328,24 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   uint64_t *d_dst_off = ar.take<uint64_t>(k + 1);
   uint8_t *oscr = ar.take<uint8_t>(out_scratch + 64);
   PushSum *push = reinterpret_cast<PushSum *>(ar.take<uint8_t>(ns1 * part_push_bytes()));
+  CostModel *model = two_pass ? ar.take<CostModel>(k) : nullptr;
+  uint32_t *model_h = two_pass ? reinterpret_cast<uint32_t *>(ar.take<uint8_t>(cost_model_hist_bytes((int)k))) : nullptr;
+  // iteration 1 of a two-pass parse only feeds the model: it parses the first
+  // zopfli_sample() bytes of every segment (its own copy of the segment table)
+  const bool sampled = two_pass && zopfli_sample() < kSeg;
+  Seg *d_sample = sampled ? ar.take<Seg>(ns1) : nullptr;
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
   Timer tm{ctx, st, mib_ctx_profiling(ctx) != 0, {}};
   CK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(Job) * k, hipMemcpyHostToDevice, st));
   if (nsegs) CK(hipMemcpyAsync(d_segs, segs.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
   if (nmbs) CK(hipMemcpyAsync(d_mbs, mbs.data(), sizeof(Mb) * nmbs, hipMemcpyHostToDevice, st));
+  std::vector<Seg> sample;
+  if (sampled && nsegs) {
+    sample = segs;
+    for (Seg &sg : sample) sg.end = std::min(sg.end, sg.start + zopfli_sample());
+    CK(hipMemcpyAsync(d_sample, sample.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
+  }
   CK(hipMemcpyAsync(d_seg_job, seg_job.data(), seg_job.size() * 4, hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
   if (nsegs) {
@@ -329,7 +354,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipMemsetAsync(hc, 0, nm1 * kMaxBT * 704 * 4, st));
     CK(hipMemsetAsync(hd, 0, nm1 * kMaxBT * kDistCtx * 128 * 4, st));
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
-    const int depth = depth_for_quality(prm.quality);
+    const int depth = (int)env_u32("MIB_DEPTH", (uint32_t)depth_for_quality(prm.quality), 1, 64);   // override: experiments
     tm.start("hash_keys");
     launch_hash_keys(st, d_jobs, d_seg_job, total, gshift, keys, vals);
     tm.stop();
@@ -344,11 +369,23 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
     tm.stop();
     tm.start("dp_parse");
-    launch_dp(st, d_jobs, d_segs, nsegs, lit_h, matches, choice);
+    Seg *s1 = sampled ? d_sample : d_segs;
+    launch_dp(st, d_jobs, s1, nsegs, lit_h, nullptr, matches, choice);
     tm.stop();
     tm.start("backtrack");
-    launch_backtrack(st, d_jobs, d_segs, nsegs, choice, raw);
+    launch_backtrack(st, d_jobs, s1, nsegs, choice, raw);
     tm.stop();
+    if (two_pass) {   // iteration 2: prices from the first parse's commands
+      tm.start("cost_model");
+      launch_cost_model(st, d_jobs, (int)k, s1, nsegs, raw, model_h, model);
+      tm.stop();
+      tm.start("dp_parse");
+      launch_dp(st, d_jobs, d_segs, nsegs, lit_h, model, matches, choice);
+      tm.stop();
+      tm.start("backtrack");
+      launch_backtrack(st, d_jobs, d_segs, nsegs, choice, raw);
+      tm.stop();
+    }
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
     launch_ring_scan(st, d_jobs, (int)k, d_segs, nsegs, raw, push);
