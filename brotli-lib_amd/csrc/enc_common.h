@@ -114,8 +114,9 @@ struct Mb {                   // one metablock: block types per category, litera
 
 struct Unit {                 // one block-split unit: the commands of 8 KiB of a segment
   uint32_t nsym[3];           // symbols: literals, commands, distance codes
-  uint32_t first[3];          // segment-relative index of its first command with a literal /
-                              // any / with a distance code (~0u: none)
+  uint32_t first[3];          // literals: stream position of its first literal; commands /
+                              // distance codes: segment-relative index of its first command
+                              // (any / with a distance code) (~0u: none)
   uint32_t sw_count[3];       // block switch before that symbol: the new block's count (0: none)
   uint8_t type[3];            // block type per category
   uint8_t sw_code[3];         // the switch's block type code (RFC 7932 section 6)
@@ -319,7 +320,10 @@ __device__ __forceinline__ uint32_t switch_bits(const Codes &cd, int cat, const 
   const int bc = block_count_code(u.sw_count[cat]);
   return cd.btd[cat][u.sw_code[cat]] + cd.bcd[cat][bc] + kBlkBits[bc];
 }
+// command / distance block switches sit at a command; literal ones at a literal, so a literal
+// block can end inside a long insert (glyph data: a few copies, long literal runs)
 __device__ __forceinline__ bool switch_at(const Unit &u, int cat, uint32_t q) { return u.sw_count[cat] && q == u.first[cat]; }
+__device__ __forceinline__ bool lit_switch_at(const Unit &u, uint32_t lp) { return u.sw_count[0] && lp == u.first[0]; }
 
 // ---------------------------------------------------------------- command items
 // A command is coded as a sequence of ITEMS (storeCommandExtra / storeSymbolWithContext /
@@ -339,7 +343,6 @@ __device__ __forceinline__ uint32_t header_bits(const Codes &cd, const Cmd &c, c
   const int cc = copy_code(c.copy ? c.copy : 2);
   uint32_t bits = cd.cd[u.type[1]][c.cmd_prefix] + kInsExtra[ic] + kCopyExtra[cc];
   if (switch_at(u, 1, q)) bits += switch_bits(cd, 1, u);
-  if (switch_at(u, 0, q)) bits += switch_bits(cd, 0, u);
   return bits;
 }
 __device__ __forceinline__ int literal_tree(const Mb &mb, const uint8_t *lut, const Unit &u, uint32_t p12) {
@@ -351,13 +354,16 @@ __device__ __forceinline__ uint32_t dist_bits(const Codes &cd, const Mb &mb, con
   if (switch_at(u, 2, q)) bits += switch_bits(cd, 2, u);
   return bits;
 }
-// bits of item k of command c (insert at stream position p)
+// bits of item k of command c (insert at stream position p); su: the segment's units (the
+// command's header and distance go by the unit of p, each literal by its own position's)
 __device__ __forceinline__ uint32_t item_bits(const Codes &cd, const Mb &mb, const uint8_t *lut, const Job &jb,
-                                              const Cmd &c, uint32_t p, const Unit &u, uint32_t q, uint32_t k) {
-  if (k == 0) return header_bits(cd, c, u, q);
-  if (k > c.ins) return dist_bits(cd, mb, c, u, q);
+                                              const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q,
+                                              uint32_t k) {
+  if (k == 0) return header_bits(cd, c, su[unit_of(sg, p)], q);
+  if (k > c.ins) return dist_bits(cd, mb, c, su[unit_of(sg, p)], q);
   const uint32_t lp = p + k - 1;
-  return cd.ld[literal_tree(mb, lut, u, prev2(jb, lp))][jb.data[lp]];
+  const Unit &ul = su[unit_of(sg, lp)];
+  return (lit_switch_at(ul, lp) ? switch_bits(cd, 0, ul) : 0u) + cd.ld[literal_tree(mb, lut, ul, prev2(jb, lp))][jb.data[lp]];
 }
 
 // Load-balanced expansion of a batch of at most B commands into their items: off[j] is the

@@ -109,7 +109,8 @@ __device__ __forceinline__ void put_switch(W &wr, const Codes &cd, int cat, cons
 // item k of command q (see item_bits in enc_common.h: same bits, in stream order)
 template <class W>
 __device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb, const uint8_t *lut, const Job &jb,
-                                           const Cmd &c, uint32_t p, const Unit &u, uint32_t q, uint32_t k) {
+                                           const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q, uint32_t k) {
+  const Unit &u = su[unit_of(sg, p)];
   if (k == 0) {
     if (switch_at(u, 1, q)) put_switch(wr, cd, 1, u);
     const int ct = u.type[1];
@@ -119,11 +120,12 @@ __device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb,
     const uint32_t clen = c.copy ? c.copy : 2;
     const int cc = copy_code(clen);
     wr.put((int)kCopyExtra[cc], clen - kCopyBase[cc]);
-    if (switch_at(u, 0, q)) put_switch(wr, cd, 0, u);
   } else if (k <= c.ins) {
     const uint32_t lp = p + k - 1;
+    const Unit &ul = su[unit_of(sg, lp)];
+    if (lit_switch_at(ul, lp)) put_switch(wr, cd, 0, ul);
     const uint32_t lit = jb.data[lp];
-    const int tree = literal_tree(mb, lut, u, prev2(jb, lp));
+    const int tree = literal_tree(mb, lut, ul, prev2(jb, lp));
     wr.put(cd.ld[tree][lit], cd.lc[tree][lit]);
   } else if (c.copy && c.cmd_prefix >= 128) {
     if (switch_at(u, 2, q)) put_switch(wr, cd, 2, u);
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
           kk[e] = i - map.off[j];
           const Cmd &k = sh_c[j];
           const uint32_t p = sh_p[j];
-          bits[e] = item_bits(cd, mb, lut, jb, k, p, sh_u[unit_of(sg, p)], base + j, kk[e]);
+          bits[e] = item_bits(cd, mb, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
         }
       }
       uint32_t boff[kEmitItems], total;
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
         const uint32_t p = sh_p[jj];
         OrW<false> wr;
         wr.init(win, rel0 + boff[e]);
-        write_item(wr, cd, mb, lut, jb, k, p, sh_u[unit_of(sg, p)], base + jj, kk[e]);
+        write_item(wr, cd, mb, lut, jb, k, p, sg, sh_u, base + jj, kk[e]);
         wr.finish();
       }
       __syncthreads();

@@ -94,7 +94,6 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
   __shared__ uint32_t sh_run;
   __shared__ ItemMap<kBlock> map;
   __shared__ uint32_t sh_pos[kBlock];
-  __shared__ uint8_t sh_unit[kBlock];
   __shared__ uint32_t sh_push[kBlock];   // the batch's pushed distances, by rank
   __shared__ uint32_t sh_ring[4];        // the ring before the batch, most recent first
   const Seg sg = segs[blockIdx.x];
@@ -172,16 +171,20 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
       atomicAdd(&hu[256 + c.cmd_prefix], 1u);
       atomicAdd(&sh_n[u][1], 1u);
       atomicMin(&sh_first[u][1], q);
-      if (ins) {
-        atomicAdd(&sh_n[u][0], ins);
-        atomicMin(&sh_first[u][0], q);
+      if (ins) {   // literals count to the unit of their own position
+        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
+        for (uint32_t v = ulo; v <= uhi; v++) {
+          const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
+          const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
+          atomicAdd(&sh_n[v][0], s1 - s0);
+          atomicMin(&sh_first[v][0], s0);
+        }
       }
       out[q] = c;
       outp[q] = pos;
     }
     // the literals of the batch, spread over the lanes (items = inserts, see ItemMap)
     sh_pos[t] = pos;
-    sh_unit[t] = (uint8_t)unit_of(sg, pos);
     uint32_t loff, nlits;
     Scan(scan_tmp).ExclusiveSum(q < n ? ins : 0u, loff, nlits);
     const uint32_t nb = min((uint32_t)kBlock, n - base);
@@ -190,7 +193,8 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
     __syncthreads();
     for (uint32_t i = t; i < nlits; i += kBlock) {
       const uint32_t j = map.find(i, nb);
-      atomicAdd(&sh_h[sh_unit[j] * kSubHist + jb.data[sh_pos[j] + i - map.off[j]]], 1u);
+      const uint32_t lp = sh_pos[j] + i - map.off[j];
+      atomicAdd(&sh_h[unit_of(sg, lp) * kSubHist + jb.data[lp]], 1u);
     }
     __syncthreads();
   }
@@ -224,7 +228,7 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
   __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
   __shared__ uint8_t ut[kSubPerSeg][3];
   __shared__ ItemMap<kBlock> map;
-  __shared__ uint32_t sh_pos[kBlock];
+  __shared__ uint32_t sh_pos[kBlock], sh_ins[kBlock];
   uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
@@ -262,9 +266,17 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
     for (uint32_t base = 0; base < n; base += kBlock) {   // the literals of this type, spread over the lanes
       const uint32_t q = base + t, nb = min((uint32_t)kBlock, n - base);
       uint32_t cnt = 0;
-      if (q < n) {
-        sh_pos[t] = cp[q];
-        if (ut[unit_of(sg, cp[q])][0] == ty) cnt = c[q].ins;
+      if (q < n && c[q].ins) {   // the command's literals that lie in units of this type
+        const uint32_t pos = cp[q], ins = c[q].ins;
+        sh_pos[t] = pos;
+        sh_ins[t] = ins;
+        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
+        for (uint32_t v = ulo; v <= uhi; v++)
+          if (ut[v][0] == ty) {
+            const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
+            const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
+            cnt += s1 - s0;
+          }
       }
       uint32_t off, nlits;
       Scan(scan_tmp).ExclusiveSum(cnt, off, nlits);
@@ -273,7 +285,20 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
       __syncthreads();
       for (uint32_t i = t; i < nlits; i += kBlock) {
         const uint32_t j = map.find(i, nb);
-        const uint32_t lp = sh_pos[j] + i - map.off[j];
+        // the (i - off)-th of command j's literals in type-ty units (an insert spans few units)
+        const uint32_t pos = sh_pos[j], ins = sh_ins[j];
+        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
+        uint32_t k = i - map.off[j], lp = pos;
+        for (uint32_t v = ulo; v <= uhi; v++) {
+          if (ut[v][0] != ty) continue;
+          const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
+          const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
+          if (k < s1 - s0) {
+            lp = s0 + k;
+            break;
+          }
+          k -= s1 - s0;
+        }
         const uint32_t p12 = prev2(jb, lp);
         atomicAdd(&sh_l[(lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp]], 1u);
       }
@@ -1307,7 +1332,7 @@ __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *seg
     for (uint32_t i = t; i < nitems; i += kBlock) {
       const uint32_t j = map.find(i, nb);
       const uint32_t p = sh_p[j];
-      bits += item_bits(cd, mb, lut, jb, sh_c[j], p, sh_u[unit_of(sg, p)], base + j, i - map.off[j]);
+      bits += item_bits(cd, mb, lut, jb, sh_c[j], p, sg, sh_u, base + j, i - map.off[j]);
     }
     __syncthreads();
   }
