@@ -118,7 +118,9 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lane_src << 2), (int)v);
 }
 
-template <int KS>
+// KM: the second iteration (prices from the stream's CostModel; a separate build, so
+// profiles tell the two passes apart)
+template <int KS, bool KM>
 __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
@@ -163,7 +165,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   if (__ballot(a < b) == 0) return;
   // prices: iteration 0 from zopfli-cost-model.ts's initial model, iteration 1 from the
   // stream's CostModel (per segment tables: a wave's segments may be different streams)
-  const CostModel *cm = (model && a < b) ? model + job : nullptr;
+  const CostModel *cm = (KM && a < b) ? model + job : nullptr;
   const float dist0 = dist_price(0, cm);
   if (a < b)
     for (uint32_t t = hl; t < 24 * 24; t += kL) {
@@ -614,12 +616,18 @@ static int dp_workgroups(int nsegs) {
 }
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
                const uint32_t *matches, uint64_t *choice) {
-  if (dp_ks(nsegs) == 1)
-    hipLaunchKernelGGL(dp_kernel<1>, dim3(dp_workgroups(nsegs)), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h,
-                       model, matches, choice);
-  else
-    hipLaunchKernelGGL(dp_kernel<2>, dim3(dp_workgroups(nsegs)), dim3(64 * kDpWaves), 0, st, jobs, segs, nsegs, lit_h,
-                       model, matches, choice);
+  const dim3 g(dp_workgroups(nsegs)), b(64 * kDpWaves);
+  if (dp_ks(nsegs) == 1) {
+    if (model)
+      hipLaunchKernelGGL((dp_kernel<1, true>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+    else
+      hipLaunchKernelGGL((dp_kernel<1, false>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+  } else {
+    if (model)
+      hipLaunchKernelGGL((dp_kernel<2, true>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+    else
+      hipLaunchKernelGGL((dp_kernel<2, false>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+  }
 }
 size_t cost_model_hist_bytes(int njobs) { return (size_t)njobs * kHistLen * 4; }
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,

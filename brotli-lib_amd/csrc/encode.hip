@@ -368,7 +368,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.start("lit_histo");
     launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
     tm.stop();
-    tm.start("dp_parse");
+    tm.start(two_pass ? "dp_sample" : "dp_parse");
     Seg *s1 = sampled ? d_sample : d_segs;
     launch_dp(st, d_jobs, s1, nsegs, lit_h, nullptr, matches, choice);
     tm.stop();
