@@ -24,8 +24,9 @@ constexpr int kLongCopy = 200;                // copies longer than this are tak
                                               // reference's MAX_ZOPFLI_LEN is 325 at q11, 150 at q10,
                                               // enc-constants.ts:32-33)
 constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
-constexpr uint32_t kHashBits = 17;            // hashBytes4 (match.ts:162-172)
-constexpr uint32_t kInvalidKey = 1u << kHashBits;   // (within a stream group) positions without 4 bytes
+constexpr uint32_t kHashBits = 17;            // bucket hash bits (hashBytes4, match.ts:162-172)
+constexpr int kHashBytes = 6;                  // bytes a bucket key covers (see hashn)
+constexpr uint32_t kInvalidKey = 1u << kHashBits;   // (within a stream group) positions without kHashBytes bytes
 constexpr int kGroupKeyBits = 6;
 // Streaming history (BrotliEncoder across update() calls): per encoder, for every hash bucket
 // the stream positions of its kHistWays most recent earlier occurrences, newest first
@@ -252,6 +253,17 @@ __device__ __forceinline__ uint32_t load_u32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 __device__ __forceinline__ uint32_t hash4(const uint8_t *p) { return (load_u32(p) * 0x1E35A7BDu) >> 15; }
+// Bucket key over the first n bytes at p (n = kHashBytes; MIB_HASH_BYTES overrides, 4..7).
+// The candidate walk is depth-limited (64 at q11), so a longer key makes every candidate a
+// match of >= n bytes and lets the walk reach farther back: C4 0.3770 -> 0.3706 and
+// find_matches 75 -> 59 ms for 6 bytes (4: the reference's hashBytes4, match.ts:162-172;
+// 7: 0.3749); matches of 4-5 bytes are given up (fonts: +0.04 %).
+__device__ __forceinline__ uint32_t hashn(const uint8_t *p, int n) {
+  uint64_t v = load_u32(p);
+  for (int i = 4; i < n; i++) v |= (uint64_t)p[i] << (8 * i);
+  v <<= 64 - 8 * n;
+  return (uint32_t)((v * 0x1E35A7BD1E35A7BDull) >> (64 - kHashBits));
+}
 
 // length of the common prefix of a[] and b[], up to limit
 __device__ __forceinline__ uint32_t match_len(const uint8_t *a, const uint8_t *b, uint32_t limit) {

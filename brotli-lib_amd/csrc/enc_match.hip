@@ -1,6 +1,7 @@
 // Match finding: hash keys, the device radix sort that turns
 // every hash bucket into a flat chain, and the LDS-tiled candidate walk.
 #include <algorithm>
+#include <cstdlib>
 
 #include "enc_common.h"
 
@@ -9,19 +10,20 @@ namespace enc {
 
 // ---------------------------------------------------------------- 1. keys
 // Every global position (including the padding after each stream) gets the key
-// (stream group << 18 | hash4), the invalid hash 2^17 for padding and a stream's last 3
+// (stream group << 18 | hash of kHashBytes bytes), the invalid hash 2^17 for padding and a stream's last
 // bytes.  A stream group is 2^gshift consecutive streams (at most 64 groups a call, so keys
 // have at most 24 bits: three radix passes).  The sort is stable and global positions
 // ascend stream by stream, so within a bucket the entries of one stream are contiguous and
 // in position order -- a candidate walk stops where the stream changes -- and the entries a
 // wave of find_matches tiles touches stay within one group's streams (cache locality).
-__global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
+__global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
                                  uint32_t *vals) {
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
     uint32_t j = pos_job[g >> kSegBits];
     const Job &jb = jobs[j];
     uint32_t p = g - jb.pos_base;
-    keys[g] = ((j >> gshift) << (kHashBits + 1)) | ((p + 4 <= jb.n && !jb.uncompressed) ? hash4(jb.data + p) : kInvalidKey);
+    keys[g] = ((j >> gshift) << (kHashBits + 1)) |
+              ((p + (uint32_t)hb <= jb.n && !jb.uncompressed) ? (hb > 4 ? hashn(jb.data + p, hb) : hash4(jb.data + p)) : kInvalidKey);
     vals[g] = g;
   }
 }
@@ -287,7 +289,8 @@ __global__ void lit_histo_kernel(const Job *jobs, const Seg *segs, uint32_t *lit
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals) {
   const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total + 255) / 256);
-  hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, keys, vals);
+  static const int hb = getenv("MIB_HASH_BYTES") ? std::min(7, std::max(4, atoi(getenv("MIB_HASH_BYTES")))) : kHashBytes;
+  hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, hb, keys, vals);
 }
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                          const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches) {

@@ -52,6 +52,7 @@ __device__ unsigned long long g_dp_prof[8];
 // otherwise share its SIMD with nothing.
 constexpr int kDpWaves = 4;           // waves per workgroup, sharing the length table
 constexpr int kLenTab = kLongCopy + 1;
+constexpr int kInsTab = 256;            // insert lengths with a table entry
 constexpr float kInf = 3.0e38f;
 constexpr uint32_t kCostLast = 255;   // cost code of a match at the path's last distance
 
@@ -132,9 +133,14 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   constexpr uint64_t kLaneMask = kL == 64 ? ~0ull : ((1ull << kL) - 1);
   __shared__ uint32_t ptab_all[kDpWaves * kS][24 * 24];   // per segment: (insert code, copy code) -> fp16 (explicit distance) | fp16 (short code 0) << 16
   __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
+  __shared__ uint16_t itab[kInsTab];                       // insert length -> insert code | its extra bits << 8
   __shared__ float litc_all[kDpWaves * kS][256];
   __shared__ StageEnt stg_all[kDpWaves][64];
   for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 4 ? copy_code((uint32_t)t) : 0);
+  for (int t = threadIdx.x; t < kInsTab; t += 64 * kDpWaves) {
+    const int ic = ins_code((uint32_t)t);
+    itab[t] = (uint16_t)(ic | (ins_extra(ic) << 8));
+  }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t h = lane / kL, hl = lane % kL, hbase = h * kL;
@@ -274,8 +280,18 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? (info >> 8) : 0u;
     const float litcost = e.lc;
     const uint32_t ins = mm >> 16;
-    const int ic = ins_code_sel(ins);
-    const float base = ci + (float)ins_extra_sel(ic);
+    // insert code and extra bits: a table for short inserts, the closed form (rare) past it
+    int ic;
+    uint32_t iextra;
+    if (__builtin_expect(ins < (uint32_t)kInsTab, 1)) {
+      const uint32_t v = itab[ins];
+      ic = (int)(v & 0xFF);
+      iextra = v >> 8;
+    } else {
+      ic = ins_code_sel(ins);
+      iextra = ins_extra_sel(ic);
+    }
+    const float base = ci + (float)iextra;
     DPMARK(1);
     DPCOUNT(4, 1);
     const bool longc = maxlen > (uint32_t)kLongCopy;
