@@ -104,7 +104,7 @@ __device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches,
   st.m[0] = a.x; st.m[1] = a.y; st.m[2] = a.z; st.m[3] = a.w;
   st.nm = (a.x != 0u) + (a.y != 0u) + (a.z != 0u) + (a.w != 0u);
 }
-struct StageEnt {   // one position's parse inputs in LDS (48 B: two b128 reads and a b64)
+struct alignas(16) StageEnt {   // one position's parse inputs in LDS (48 B: two b128 reads and a b64)
   uint32_t m[kMaxMatches];   // (clipped length << 24) | distance, 0 = none
   uint32_t mc[kMaxMatches];  // distance | distance-cost code << 24 (quarter bits)
   uint32_t info;             // nm | maxlen << 8 (clipped to the segment)
@@ -356,16 +356,13 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
       DPMARK(2);
       continue;
     }
-    // the match staircase of i: lengths (clipped) and the packed (distance | cost code) words;
-    // a match at the path's last distance gets the code kCostLast (priced with short code 0)
-    uint32_t mL[kMaxMatches], vpk[kMaxMatches];
-#pragma unroll
-    for (int q = 0; q < kMaxMatches; q++) {
-      const uint32_t m = e.m[q];   // 0 past nm
-      mL[q] = act ? match_length(m) : 0u;
-      const uint32_t pk = e.mc[q];
-      vpk[q] = match_dist(pk) == ld ? (pk | (kCostLast << 24)) : pk;
-    }
+    // the match staircase of i: lengths (clipped) and the packed (distance | cost code) words
+    // (both read unconditionally: a masked load would be a branch and a wait per entry)
+    const uint4 em = *reinterpret_cast<const uint4 *>(e.m), emc = *reinterpret_cast<const uint4 *>(e.mc);
+    const uint32_t actm = 0u - (uint32_t)act;
+    const uint32_t mL[kMaxMatches] = {match_length(em.x) & actm, match_length(em.y) & actm, match_length(em.z) & actm,
+                                      match_length(em.w) & actm};   // 0 past nm
+    const uint32_t vpk[kMaxMatches] = {emc.x, emc.y, emc.z, emc.w};
     const uint32_t maxrel = max(1u, maxlen);
     const uint32_t *trow = ptab + ic * 24;
     // relax every edge out of i: lane j of chunk k takes length kL k + j - off
@@ -385,11 +382,11 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         const uint32_t tv = trow[cctab[l]];
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
-        const uint32_t cc = x >> 24;
-        const float alt = pn + (float)cc * 0.25f;
-        const uint32_t use_last = 0u - (uint32_t)(cc == kCostLast);   // a select, not a branch
-        cand = base + __uint_as_float((__float_as_uint(pl) & use_last) | (__float_as_uint(alt) & ~use_last));
         nd = match_dist(x);
+        const float alt = pn + (float)(x >> 24) * 0.25f;
+        // a match at the path's last distance is priced with short code 0
+        const uint32_t use_last = 0u - (uint32_t)(nd == ld);   // a select, not a branch
+        cand = base + __uint_as_float((__float_as_uint(pl) & use_last) | (__float_as_uint(alt) & ~use_last));
         nmeta = l;
       }
       if (cand < wc[c]) {
