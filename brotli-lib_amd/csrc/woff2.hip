@@ -370,6 +370,38 @@ __global__ void glyf_bitmaps_kernel(uint32_t n, const uint8_t *bits, uint8_t *bb
   }
 }
 
+
+// ---------------------------------------------------------------- hmtx (WOFF2 section 5.4)
+// fontTools WOFF2HmtxTable.transform: the proportional (i < numberOfHMetrics) and monospaced
+// glyphs' left side bearings are dropped when every one equals its glyph's xMin (0 for an
+// empty glyph).  Thread per glyph: a mismatch sets bit 0 (proportional) or 1 (monospaced).
+__global__ void hmtx_check_kernel(Font f, const uint8_t *hmtx, uint32_t nhm, uint32_t *mismatch) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= f.num_glyphs) return;
+  const uint32_t o0 = f.long_loca ? be32(f.loca + 4 * g) : 2 * be16(f.loca + 2 * g);
+  const uint32_t o1 = f.long_loca ? be32(f.loca + 4 * g + 4) : 2 * be16(f.loca + 2 * g + 2);
+  const int32_t xmin = (o1 > o0 && o0 + 10 <= f.glyf_len) ? sbe16(f.glyf + o0 + 2) : 0;
+  const int32_t lsb = g < nhm ? sbe16(hmtx + 4 * g + 2) : sbe16(hmtx + 4 * nhm + 2 * (g - nhm));
+  if (lsb != xmin) atomicOr(mismatch, g < nhm ? 1u : 2u);
+}
+// the transformed table: flags, advance widths, then the lsb array that is kept (if any)
+__global__ void hmtx_write_kernel(uint32_t ng, const uint8_t *hmtx, uint32_t nhm, uint32_t keep, uint8_t *out) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ng) return;
+  if (g < nhm) {
+    out[1 + 2 * g] = hmtx[4 * g];
+    out[2 + 2 * g] = hmtx[4 * g + 1];
+  }
+  const uint32_t lsb_at = 1 + 2 * nhm;
+  if (keep == 1 && g < nhm) {          // proportional glyphs' lsbs
+    out[lsb_at + 2 * g] = hmtx[4 * g + 2];
+    out[lsb_at + 2 * g + 1] = hmtx[4 * g + 3];
+  } else if (keep == 2 && g >= nhm) {  // monospaced glyphs' lsbs
+    out[lsb_at + 2 * (g - nhm)] = hmtx[4 * nhm + 2 * (g - nhm)];
+    out[lsb_at + 2 * (g - nhm) + 1] = hmtx[4 * nhm + 2 * (g - nhm) + 1];
+  }
+}
+
 }  // namespace woff2
 }  // namespace mib
 
@@ -526,6 +558,93 @@ extern "C" int mib_woff2_transform_glyf(const uint8_t *ttf, size_t n, mib_buf *o
   hipFree(d_base);
   hipFree(d_out);
   hipFree(d_tmp);
+  mib_default_lock(0);
+  return rc;
+}
+
+// WOFF2 hmtx transform (fontTools WOFF2HmtxTable.transform).  Returns 0 with out->size = 0
+// when no transform applies (both side-bearing arrays must be kept: the table stays as is).
+extern "C" int mib_woff2_transform_hmtx(const uint8_t *ttf, size_t n, mib_buf *out) {
+  if (!out || (!ttf && n)) return MIB_E_INVALID_ARG;
+  out->data = nullptr;
+  out->size = 0;
+  if (n < 12) return MIB_E_INVALID_ARG;
+  const uint32_t ntab = hbe16(ttf + 4);
+  if (12 + 16ull * ntab > n) return MIB_E_INVALID_ARG;
+  uint64_t off[6] = {0, 0, 0, 0, 0, 0}, len[6] = {0, 0, 0, 0, 0, 0};
+  bool have[6] = {false, false, false, false, false, false};
+  static const char *kTags[6] = {"glyf", "loca", "head", "maxp", "hhea", "hmtx"};
+  for (uint32_t i = 0; i < ntab; i++) {
+    const uint8_t *r = ttf + 12 + 16 * i;
+    const uint32_t o = hbe32(r + 8), l = hbe32(r + 12);
+    if ((uint64_t)o + l > n) return MIB_E_INVALID_ARG;
+    for (int t = 0; t < 6; t++)
+      if (!memcmp(r, kTags[t], 4)) off[t] = o, len[t] = l, have[t] = true;
+  }
+  for (int t = 0; t < 6; t++)
+    if (!have[t]) return MIB_E_INVALID_ARG;
+  if (len[2] < 54 || len[3] < 6 || len[4] < 36) return MIB_E_INVALID_ARG;
+  const int long_loca = (int16_t)hbe16(ttf + off[2] + 50) != 0 ? 1 : 0;
+  const uint32_t ng = hbe16(ttf + off[3] + 4), nhm = hbe16(ttf + off[4] + 34);
+  if (ng == 0 || nhm == 0 || nhm > ng || (uint64_t)(ng + 1) * (long_loca ? 4 : 2) > len[1] ||
+      4ull * nhm + 2ull * (ng - nhm) > len[5])
+    return MIB_E_INVALID_ARG;
+  mib_default_lock(1);
+  mib_ctx *c = mib_default_ctx();
+  if (!c) {
+    mib_default_lock(0);
+    return MIB_E_NO_DEVICE;
+  }
+  hipSetDevice(mib_ctx_device_of(c));
+  hipStream_t st = (hipStream_t)mib_ctx_stream_of(c);
+  int rc = 0;
+  uint8_t *d_font = nullptr, *d_out = nullptr;
+  uint32_t *d_mis = nullptr;
+  do {
+    const uint64_t gl = len[0], ll = len[1], hl = len[5];
+    if (hipMalloc(&d_font, gl + ll + hl + 16) != hipSuccess || hipMalloc(&d_mis, 4) != hipSuccess) {
+      rc = MIB_E_OUT_OF_MEMORY;
+      break;
+    }
+    hipMemcpyAsync(d_font, ttf + off[0], gl, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(d_font + gl, ttf + off[1], ll, hipMemcpyHostToDevice, st);
+    hipMemcpyAsync(d_font + gl + ll, ttf + off[5], hl, hipMemcpyHostToDevice, st);
+    hipMemsetAsync(d_mis, 0, 4, st);
+    Font f{d_font, (uint32_t)gl, d_font + gl, ng, long_loca};
+    const dim3 grid((ng + 255) / 256), block(256);
+    hipLaunchKernelGGL(hmtx_check_kernel, grid, block, 0, st, f, d_font + gl + ll, nhm, d_mis);
+    uint32_t mis = 0;
+    hipMemcpyAsync(&mis, d_mis, 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      rc = MIB_E_NO_DEVICE;
+      break;
+    }
+    if (mis == 3) break;   // both arrays needed: no transform
+    const uint32_t keep = mis;   // 0: none, 1: proportional lsbs, 2: monospaced lsbs
+    const uint64_t total = 1 + 2ull * nhm + (keep == 1 ? 2ull * nhm : keep == 2 ? 2ull * (ng - nhm) : 0);
+    if (hipMalloc(&d_out, total + 16) != hipSuccess) {
+      rc = MIB_E_OUT_OF_MEMORY;
+      break;
+    }
+    hipLaunchKernelGGL(hmtx_write_kernel, grid, block, 0, st, ng, d_font + gl + ll, nhm, keep, d_out);
+    out->data = (uint8_t *)malloc(total);
+    if (!out->data) {
+      rc = MIB_E_OUT_OF_MEMORY;
+      break;
+    }
+    hipMemcpyAsync(out->data, d_out, total, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      free(out->data);
+      out->data = nullptr;
+      rc = MIB_E_NO_DEVICE;
+      break;
+    }
+    out->data[0] = (uint8_t)((keep == 1 ? 0 : 1) | (keep == 2 ? 0 : 2));   // set: that array is absent
+    out->size = total;
+  } while (0);
+  hipFree(d_font);
+  hipFree(d_mis);
+  hipFree(d_out);
   mib_default_lock(0);
   return rc;
 }

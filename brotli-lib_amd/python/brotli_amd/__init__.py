@@ -105,6 +105,7 @@ def _L():
         lib.mib_ctx_kernel_times.argtypes = [ctypes.c_void_p, ctypes.POINTER(_KTime), ctypes.c_int]
         lib.mib_ctx_set_profiling.argtypes = [ctypes.c_void_p, ctypes.c_int]
         lib.mib_woff2_transform_glyf.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
+        lib.mib_woff2_transform_hmtx.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
         lib.mib_part_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         _lib = lib
     return _lib
@@ -263,6 +264,19 @@ def woff2_transform_glyf(ttf):
     rc = _L().mib_woff2_transform_glyf(data, len(data), ctypes.byref(buf))
     if rc:
         raise _err(rc)
+    return _take(buf)
+
+
+def woff2_transform_hmtx(ttf):
+    """The WOFF2-transformed 'hmtx' table (W3C WOFF2 section 5.4), computed on the GPU, or None
+    when no transform applies (both side-bearing arrays differ from the glyphs' xMin)."""
+    data = _bytes(ttf)
+    buf = _Buf()
+    rc = _L().mib_woff2_transform_hmtx(data, len(data), ctypes.byref(buf))
+    if rc:
+        raise _err(rc)
+    if not buf.size:
+        return None
     return _take(buf)
 
 

@@ -117,6 +117,11 @@ void mib_ctx_set_profiling(mib_ctx *c, int on);
  * byte what fontTools' WOFF2GlyfTable.transform produces.  MIB_E_INVALID_ARG for a font
  * without glyf / loca / head / maxp or with a malformed glyph. */
 int mib_woff2_transform_glyf(const uint8_t *ttf, size_t n, mib_buf *out);
+/* WOFF2 'hmtx' transform (W3C WOFF2 section 5.4; fontTools WOFF2HmtxTable.transform): flags,
+ * the advance widths and whichever left-side-bearing array does not equal the glyphs' xMin.
+ * Returns 0 with out->size = 0 when both arrays differ (no transform: the table is stored
+ * as is).  The transformed loca table is empty (WOFF2 section 5.3): nothing to compute. */
+int mib_woff2_transform_hmtx(const uint8_t *ttf, size_t n, mib_buf *out);
 
 /* Part-parallel decoding (streams this encoder marked with a part index):
  * how many streams a context (NULL: the default one) decoded part-parallel, and how many of

@@ -53,3 +53,24 @@ def test_malformed_fonts_are_rejected():
     for bad in (b'', ttf[:11], ttf[:200]):
         with pytest.raises(brotli_amd.BrotliError):
             brotli_amd.woff2_transform_glyf(bad)
+
+
+def test_hmtx_transform_matches_fonttools():
+    """WOFF2 section 5.4 on the GPU against fontTools' WOFF2HmtxTable.transform: the bench fonts
+    as they are (both side-bearing arrays dropped), with a proportional or the monospaced
+    glyph's lsb moved off its xMin (that array kept), and with both (no transform: None)."""
+    import make_golden
+    with open(os.path.join(HERE, 'hmtx_golden.json')) as f:
+        gold = json.load(f)['fonts']
+    seen = 0
+    for name, ttf in _fonts():
+        for tag, v in make_golden.hmtx_variants(ttf):
+            want = gold['%s/%s' % (name, tag)]
+            got = brotli_amd.woff2_transform_hmtx(v)
+            if want is None:
+                assert got is None, (name, tag)
+            else:
+                assert got is not None and got[0] == want['flags'] and len(got) == want['size'], (name, tag)
+                assert hashlib.sha256(got).hexdigest() == want['sha256'], (name, tag)
+            seen += 1
+    assert seen == 8
