@@ -383,7 +383,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
         nd = match_dist(x);
-        const float alt = pn + (float)(x >> 24) * 0.25f;
+        const float alt = __builtin_fmaf((float)(x >> 24), 0.25f, pn);   // (exact: code / 4 needs no rounding)
         // a match at the path's last distance is priced with short code 0
         const uint32_t use_last = 0u - (uint32_t)(nd == ld);   // a select, not a branch
         cand = base + __uint_as_float((__float_as_uint(pl) & use_last) | (__float_as_uint(alt) & ~use_last));
