@@ -327,14 +327,17 @@ __device__ __forceinline__ float hist_cost(float bits, int nnz) {
 // Block per (metablock, literal | distance, block type): the type's context histograms.  A
 // literal block type may keep at most kMaxLitTrees / (literal block types) codes: past that
 // cap the cheapest merge is taken even when it costs bits.
-__global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
+// 16 waves: the LDS working set (64 histograms) allows one block per CU, and a lone wave per
+// SIMD would leave every LDS round trip of the merge loop exposed
+constexpr int kCluT = 1024;
+__global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
   constexpr int kMaxH = kLitCtx;
   __shared__ uint32_t h[kMaxH][256];
   __shared__ float cost[kMaxH];
   __shared__ float save[kMaxH][kMaxH];
   __shared__ int alive[kMaxH], label[kMaxH];
-  __shared__ float red_v[256];
-  __shared__ int red_i[256];
+  __shared__ float red_v[kCluT];
+  __shared__ int red_i[kCluT];
   __shared__ int sh_best, sh_alive;
   const int m = blockIdx.x / (2 * kMaxBT), kind = (blockIdx.x / kMaxBT) & 1, ty = blockIdx.x % kMaxBT;
   Mb &mb = mbs[m];
@@ -355,13 +358,13 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
   const int stride = kind == 0 ? 256 : 128;
   uint32_t *src = kind == 0 ? hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256
                             : hd + ((size_t)m * kMaxBT * kDistCtx + ty * kDistCtx) * 128;
-  for (int i = t; i < nh * 256; i += 256) {
+  for (int i = t; i < nh * 256; i += kCluT) {
     const int a = i / 256, x = i % 256;
     h[a][x] = x < A ? src[a * stride + x] : 0u;
   }
   __syncthreads();
   // each histogram's cost, and which contexts are used at all
-  for (int a = t; a < nh; a += 256) {
+  for (int a = t; a < nh; a += kCluT) {
     float sum = 0.f, ent = 0.f;
     int nnz = 0;
     for (int x = 0; x < A; x++) {
@@ -398,7 +401,7 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
     if (sum > 0.f) ent += sum * __log2f(sum);
     return cost[a] + cost[b] - hist_cost(ent, nnz);
   };
-  for (int p = t; p < nh * nh; p += 256) {
+  for (int p = t; p < nh * nh; p += kCluT) {
     const int a = p / nh, b = p % nh;
     save[a][b] = (a < b && alive[a] && alive[b]) ? pair_saving(a, b) : -1e30f;
   }
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
     // best pair
     float bv = -1e30f;
     int bi = -1;
-    for (int p = t; p < nh * nh; p += 256) {
+    for (int p = t; p < nh * nh; p += kCluT) {
       const float v = save[p / nh][p % nh];
       if (v > bv) {
         bv = v;
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
     red_v[t] = bv;
     red_i[t] = bi;
     __syncthreads();
-    for (int o = 128; o; o >>= 1) {
+    for (int o = kCluT / 2; o; o >>= 1) {
       if (t < o && (red_v[t + o] > red_v[t] || (red_v[t + o] == red_v[t] && red_i[t + o] >= 0 &&
                                                  (red_i[t] < 0 || red_i[t + o] < red_i[t])))) {
         red_v[t] = red_v[t + o];
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
     const int best = sh_best;
     if (best < 0) break;
     const int a = best / nh, b = best % nh;   // merge b into a
-    for (int x = t; x < A; x += 256) h[a][x] += h[b][x];
+    for (int x = t; x < A; x += kCluT) h[a][x] += h[b][x];
     __syncthreads();
     if (t == 0) {
       cost[a] = cost[a] + cost[b] - save[a][b];
@@ -440,12 +443,34 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
         if (label[q] == b) label[q] = a;
     }
     __syncthreads();
-    // pairs with b die; pairs with a change
-    for (int q = t; q < nh; q += 256) {
-      save[min(q, b)][max(q, b)] = -1e30f;
-      if (q != a) {
-        const int lo = min(q, a), hi = max(q, a);
-        save[lo][hi] = alive[q] ? pair_saving(lo, hi) : -1e30f;
+    // pairs with b die; pairs with a change: a wave per pair, lanes over the symbols
+    for (int q = t; q < nh; q += kCluT) save[min(q, b)][max(q, b)] = -1e30f;
+    __syncthreads();
+    for (int q = t >> 6; q < nh; q += kCluT / 64) {
+      if (q == a || q == b) continue;
+      const int lo = min(q, a), hi = max(q, a);
+      if (!alive[q]) {
+        if ((t & 63) == 0) save[lo][hi] = -1e30f;
+        continue;
+      }
+      float sum = 0.f, ent = 0.f;
+      int nnz = 0;
+      for (int x = t & 63; x < A; x += 64) {
+        const float c = (float)(h[a][x] + h[q][x]);
+        if (c > 0.f) {
+          sum += c;
+          ent -= c * __log2f(c);
+          nnz++;
+        }
+      }
+      for (int o = 32; o; o >>= 1) {
+        sum += __shfl_xor(sum, o);
+        ent += __shfl_xor(ent, o);
+        nnz += __shfl_xor(nnz, o);
+      }
+      if ((t & 63) == 0) {
+        if (sum > 0.f) ent += sum * __log2f(sum);
+        save[lo][hi] = cost[lo] + cost[hi] - hist_cost(ent, nnz);
       }
     }
     __syncthreads();
@@ -468,9 +493,9 @@ __global__ __launch_bounds__(256) void cluster_kernel(const Job *jobs, Mb *mbs, 
   }
   __syncthreads();
   // clustered histograms, in place: cluster c <- its representative's merged histogram
-  for (int i = t; i < nh * stride; i += 256) src[i] = 0;
+  for (int i = t; i < nh * stride; i += kCluT) src[i] = 0;
   __syncthreads();
-  for (int i = t; i < nh * 256; i += 256) {
+  for (int i = t; i < nh * 256; i += kCluT) {
     const int a = i / 256, x = i % 256;
     const int c = alive[a] ? rep_id[a] : -1;
     if (c >= 0 && x < A) src[c * stride + x] = h[a][x];
@@ -1398,7 +1423,7 @@ void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
   hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs);
 }
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
-  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(256), 0, st, jobs, mbs, nmbs, hl, hd);
+  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd);
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
