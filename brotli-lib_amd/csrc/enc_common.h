@@ -70,6 +70,8 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint32_t hist;            // streaming: bytes of the stream before data[0] that copies may reach
   uint32_t abs_base;        // streaming: stream position of data[0] (mod 2^32)
   uint32_t *hist_tab;       // streaming: the encoder's bucket table of earlier positions, or null
+  uint32_t dict;            // 1: static-dictionary references allowed (one-shot, lgwin <= 22, q >= 10)
+  uint32_t dict_span;       // ... at stream positions below this (where the window is still short)
   uint32_t parts;           // 1: part index (parts.h) -- external copy sources lag, index block first
   uint32_t idx_payload;     // part index: metadata payload bytes
   uint32_t part_bits;       // part index: log2 of the part size (>= kSegBits)
@@ -80,6 +82,22 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint64_t out_cap;
   uint64_t total_bits;      // written by offsets / stored
 };
+
+// Static-dictionary references (RFC 7932 section 8, identity transform):
+// a copy whose distance exceeds the decoder's maximum backward distance names the word of
+// its length with index distance - (max distance + 1).  Encoder-side such a copy carries
+// kDictFlag in its distance (window distances stay below 2^22: dictionary words are only
+// used at lgwin <= 22): it never pushes on the distance ring and is always coded with an
+// explicit distance code; as a "previous distance" it equals no window distance, so the
+// copy after it never takes code 0 by mistake.
+constexpr uint32_t kDictFlag = 1u << 23;
+constexpr int kDictHashBits = 15;           // word table: buckets by the first 4 bytes
+constexpr int kDictWays = 8;                // words per bucket, longest first (length << 16 | index)
+__device__ __forceinline__ bool is_dict(uint32_t d) { return (d & kDictFlag) != 0; }
+__device__ __forceinline__ uint32_t dict_hash(uint32_t w4) { return (w4 * 0x1E35A7BDu) >> (32 - kDictHashBits); }
+
+// (only streams with dict set carry word references; at lgwin > 22 bit 23 is a distance bit)
+__device__ __forceinline__ bool is_word(const Job &jb, uint32_t d) { return jb.dict && is_dict(d); }
 
 struct Seg {
   uint32_t job, start, end;   // stream-local [start, end)
@@ -398,6 +416,8 @@ struct ItemMap {
 // ---------------------------------------------------------------- kernel launchers (host)
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals);
+void launch_dict_matches(hipStream_t st, const Job *jobs, int njobs, uint32_t span, const uint32_t *dict_tab,
+                         const uint8_t *dict_data, uint32_t *matches);
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                          const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);

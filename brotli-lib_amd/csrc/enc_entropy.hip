@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
     const uint32_t pos = sh_run + off;
     // the decoder's distance ring before this command: pushes of the batch before it (by
     // rank), then the ring the batch started with
-    const uint32_t push = (q < nraw && d != prevd) ? 1u : 0u;
+    const uint32_t push = (q < nraw && !is_word(jb, d) && d != prevd) ? 1u : 0u;   // dictionary words never push
     uint32_t rank, npush;
     __syncthreads();
     Scan(scan_tmp).ExclusiveSum(push, rank, npush);
@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
       const uint32_t u = unit_of(sg, pos);
       uint32_t *hu = sh_h + u * kSubHist;
       if (len) {
-        const uint32_t dcode = d == prevd ? 0 : short_code(d, ring);
+        const uint32_t dcode = is_word(jb, d) ? (d & ~kDictFlag) + 15 : d == prevd ? 0 : short_code(d, ring);
         uint32_t extra;
         const uint32_t dp = dist_prefix(dcode, (int)jb.ndirect, (int)jb.npostfix, &extra);
         c.dist_extra = extra;
@@ -516,7 +516,7 @@ __global__ void dist_ring_kernel(Job *jobs, int njobs, const Seg *segs, const Cm
     const Seg &sg = segs[s];
     const Cmd *c = cmds + sg.cmd_off;
     for (int q = (int)sg.ncmd - 1; q >= 0 && got < 4; q--)
-      if ((c[q].dist_prefix & 0x3FF) != 0) ring[got++] = (int32_t)c[q].dist;
+      if ((c[q].dist_prefix & 0x3FF) != 0 && !is_word(jb, c[q].dist)) ring[got++] = (int32_t)c[q].dist;
   }
   for (int q = 0; q < 4; q++) jb.dc_out[q] = q < got ? ring[q] : jb.dc_in[q - got];
 }

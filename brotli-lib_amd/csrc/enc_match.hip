@@ -286,6 +286,39 @@ __global__ void lit_histo_kernel(const Job *jobs, const Seg *segs, uint32_t *lit
 }
 
 
+// ---------------------------------------------------------------- static-dictionary words
+// After the window walk, over the first dict_span bytes of every stream (where the window is
+// short): a position with no window match gets the longest RFC 7932 word (identity
+// transform) of its bucket that the input repeats in full -- a word reference cannot be cut,
+// and it may not cross the parse segment.  Block = 256 consecutive positions of one stream.
+__global__ __launch_bounds__(256) void dict_matches_kernel(const Job *jobs, int njobs, const uint32_t *dict_tab,
+                                                           const uint8_t *dict_data, uint32_t *matches) {
+  for (int j = blockIdx.y; j < njobs; j += gridDim.y) {
+  const Job &jb = jobs[j];
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  if (!jb.dict || p >= min(jb.dict_span, jb.n) || p + 4 > jb.n) continue;
+  uint32_t *rec = matches + (uint64_t)(jb.pos_base + p) * kMatchRec;
+  if (rec[0] != 0) continue;   // the window has a match here
+  const uint32_t limit = min(((p >> kSegBits) + 1) << kSegBits, jb.n) - p;
+  const uint8_t *cur = jb.data + p;
+  const uint32_t *slot = dict_tab + (size_t)dict_hash(load_u32(cur)) * kDictWays;
+  for (int k = 0; k < kDictWays; k++) {
+    const uint32_t e = slot[k];
+    if (!e) break;
+    const uint32_t L = e >> 16, idx = e & 0x7FF;
+    if (L > limit) continue;
+    // dict_data: the word-list offsets per length (32 x u32), then the RFC 7932 words
+    const uint8_t *w = dict_data + 128 + reinterpret_cast<const uint32_t *>(dict_data)[L] + idx * L;
+    uint32_t i = 0;
+    while (i < L && w[i] == cur[i]) i++;
+    if (i == L) {
+      rec[0] = pack_match(kDictFlag | idx, L);
+      break;
+    }
+  }
+  }
+}
+
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals) {
   const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total + 255) / 256);
@@ -307,6 +340,12 @@ void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_jo
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total) {
   hipLaunchKernelGGL(hist_update_kernel, dim3((total + 255) / 256), dim3(256), 0, st, jobs, pos_job, skeys, svals, total);
+}
+void launch_dict_matches(hipStream_t st, const Job *jobs, int njobs, uint32_t span, const uint32_t *dict_tab,
+                         const uint8_t *dict_data, uint32_t *matches) {
+  if (!njobs || !span) return;
+  hipLaunchKernelGGL(dict_matches_kernel, dim3((span + 255) / 256, std::min(njobs, 65535)), dim3(256), 0, st, jobs, njobs, dict_tab,
+                     dict_data, matches);
 }
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h) {
   hipLaunchKernelGGL(lit_histo_kernel, dim3(nsegs), dim3(256), 0, st, jobs, segs, lit_h);

@@ -152,7 +152,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
   const uint8_t *data = nullptr;
   int ndirect = 0, npostfix = 0;
-  uint32_t parts = 0, abs0 = 0, pbits = 16, plag = 0;
+  uint32_t parts = 0, abs0 = 0, pbits = 16, plag = 0, maxback = 0;
+  bool words = false;
   if (sgi < nsegs) {
     const Seg &sg = segs[sgi];
     const Job &jb = jobs[sg.job];
@@ -167,6 +168,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     abs0 = jb.abs_base;
     pbits = jb.part_bits;
     plag = jb.part_lag;
+    maxback = (1u << jb.lgwin) - 16;
+    words = jb.dict != 0;
   }
   if (__ballot(a < b) == 0) return;
   // prices: iteration 0 from zopfli-cost-model.ts's initial model, iteration 1 from the
@@ -235,22 +238,29 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     const uint32_t nm = p < b ? cur.nm : 0u;
     StageEnt e;
     e.lc = p < b ? litc[cur.lit] : 0.f;
-    uint32_t maxlen = 0;
+    uint32_t maxlen = 0, word = 0;
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
       e.m[q] = 0;
       e.mc[q] = 0;
       if ((uint32_t)q < nm) {
         uint32_t extra;
-        const uint32_t ln = min(match_length(cur.m[q]), b - p);
-        const uint32_t dp = dist_prefix(match_dist(cur.m[q]) + 15, ndirect, npostfix, &extra);
-        e.m[q] = (ln << 24) | match_dist(cur.m[q]);
+        uint32_t md = match_dist(cur.m[q]), d = md;
+        uint32_t ln = min(match_length(cur.m[q]), b - p);
+        if (words && is_dict(md)) {   // a dictionary word (the only entry): its distance at p, its exact length
+          d = min(abs0 + p, maxback) + 1 + (md & 0x7FF);
+          md = d | kDictFlag;
+          word = ln == match_length(cur.m[q]) ? 1u : 0u;   // cut by the segment end: unusable
+          ln = word ? ln : 0u;
+        }
+        const uint32_t dp = dist_prefix(d + 15, ndirect, npostfix, &extra);
+        e.m[q] = (ln << 24) | md;
         const float dc = (float)(dp >> 10) + dist_price(dp & 0x3FFu, cm);
-        e.mc[q] = match_dist(cur.m[q]) | (min((uint32_t)(dc * 4.f + 0.5f), kCostLast - 1) << 24);
+        e.mc[q] = md | (min((uint32_t)(dc * 4.f + 0.5f), kCostLast - 1) << 24);
         maxlen = ln;
       }
     }
-    e.info = nm | (maxlen << 8);
+    e.info = (maxlen ? nm : 0u) | (maxlen << 8) | ((word ? maxlen : 4u) << 16);   // | the shortest usable length
     e.pad[0] = e.pad[1] = 0;
     stg[lane] = e;
     DPCOUNT(6, 1);
@@ -277,7 +287,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     const bool act = !done;
     const StageEnt &e = stg[src];
     const uint32_t info = e.info;
-    const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? (info >> 8) : 0u;
+    const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? ((info >> 8) & 0xFF) : 0u;
+    const uint32_t minlen = info >> 16;   // 4, or a dictionary word's length: that length only
     const float litcost = e.lc;
     const uint32_t ins = mm >> 16;
     // insert code and extra bits: a table for short inserts, the closed form (rare) past it
@@ -374,7 +385,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
       float cand = kInf;
       uint32_t nd = ld, nmeta = min(ins + 1, 65535u) << 16;
       if (l == 1 && act) cand = ci + litcost;
-      if (l >= 4 && l <= maxlen) {
+      if (l >= minlen && l <= maxlen) {
         uint32_t x = 0;
 #pragma unroll
         for (int q = kMaxMatches - 1; q >= 0; q--)
@@ -556,12 +567,13 @@ __global__ __launch_bounds__(256) void cmd_stats_kernel(const Job *jobs, const S
     const uint32_t pos = base + scan[t] - span, tot = scan[255];
     __syncthreads();
     if (q < n) {
-      const bool last = c.dist == prevd;
+      const bool last = !is_word(jb, c.dist) && c.dist == prevd;
       const int cmd = combine_codes(ins_code(c.ins), copy_code(c.len), last);
       atomicAdd(&hc[cmd], 1u);
       if (cmd >= 128) {
         uint32_t extra;
-        const uint32_t code = last ? 0u : (dist_prefix(c.dist + 15, (int)jb.ndirect, (int)jb.npostfix, &extra) & 0x3FFu);
+        const uint32_t code =
+            last ? 0u : (dist_prefix((is_word(jb, c.dist) ? c.dist & ~kDictFlag : c.dist) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra) & 0x3FFu);
         atomicAdd(&hd[min(code, 127u)], 1u);
       }
       for (uint32_t j = 0; j < c.ins; j++) atomicAdd(&hl[jb.data[pos + j]], 1u);

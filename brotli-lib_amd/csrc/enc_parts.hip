@@ -36,7 +36,7 @@ __global__ __launch_bounds__(64) void part_push_kernel(const Job *jobs, const Se
     uint32_t d = 0;
     if (q >= 0) {
       const Cmd cc = c[q];
-      push = cc.copy != 0 && (cc.dist_prefix & 0x3FF) != 0;
+      push = cc.copy != 0 && (cc.dist_prefix & 0x3FF) != 0 && !is_word(jb, cc.dist);
       d = cc.dist;
     }
     uint64_t m = __ballot(push);
@@ -76,7 +76,7 @@ __global__ __launch_bounds__(64) void raw_push_kernel(const Job *jobs, const Seg
     uint32_t d = 0;
     if (q >= 0) {
       d = c[q].dist;
-      push = d != (q ? c[q - 1].dist : sg.prev_dist);
+      push = !is_word(jb, d) && d != (q ? c[q - 1].dist : sg.prev_dist);
     }
     uint64_t m = __ballot(push);
     total += (uint32_t)__popcll(m);

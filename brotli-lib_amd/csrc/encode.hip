@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <memory>
+#include <mutex>
 #include <vector>
 
 #include "enc_common.h"
@@ -189,6 +190,76 @@ Params make_params(const mib_enc_opts *o) {
   return p;
 }
 
+// The static dictionary for the match finder (§8 f3), once per device: the word-list offsets
+// per length and the RFC 7932 words (dict_data), and buckets of kDictWays words by their first
+// four bytes, longest first (dict_tab: length << 16 | index, 0 = empty).
+const uint8_t kHostDict[] = {
+#include "rfc_dictionary.inc"
+};
+const uint8_t kHostDictSizeBits[25] = {0, 0, 0, 0, 10, 10, 11, 11, 10, 10, 10, 10, 10, 9, 9, 8, 7, 7, 8, 7, 7, 6, 6, 5, 5};
+struct DictDev {
+  uint8_t *data = nullptr;
+  uint32_t *tab = nullptr;
+};
+constexpr int kDictDevices = 64;
+DictDev g_dict[kDictDevices];
+std::mutex g_dict_mu;
+// MIB_DICT=0 turns the dictionary references off (experiments)
+bool dict_enabled() {
+  static bool v = [] {
+    const char *e = getenv("MIB_DICT");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+// stream positions where words are looked up (MIB_DICT_SPAN overrides): a word reference
+// pays where the window has little to offer, and each one costs the decoder a trip through
+// its general loop
+uint32_t dict_span() {
+  static uint32_t v = env_u32("MIB_DICT_SPAN", 1u << 16, 0, 1u << 30);
+  return v;
+}
+const DictDev *dict_device(int dev) {
+  if (dev < 0 || dev >= kDictDevices) return nullptr;
+  std::lock_guard<std::mutex> lk(g_dict_mu);
+  DictDev &d = g_dict[dev];
+  if (d.data) return &d;
+  std::vector<uint32_t> off(32, 0);
+  for (int L = 4; L < 25; L++) off[L + 1] = off[L] + ((uint32_t)L << kHostDictSizeBits[L]);
+  for (int L = 26; L < 32; L++) off[L] = off[25];
+  std::vector<uint8_t> blob(128 + sizeof(kHostDict));
+  memcpy(blob.data(), off.data(), 128);
+  memcpy(blob.data() + 128, kHostDict, sizeof(kHostDict));
+  std::vector<uint32_t> tab((size_t)kDictWays << kDictHashBits, 0u);
+  for (int L = 24; L >= 4; L--)
+    for (uint32_t i = 0; i < (1u << kHostDictSizeBits[L]); i++) {
+      const uint8_t *w = kHostDict + off[L] + i * L;
+      const uint32_t w4 = (uint32_t)w[0] | ((uint32_t)w[1] << 8) | ((uint32_t)w[2] << 16) | ((uint32_t)w[3] << 24);
+      uint32_t *slot = tab.data() + (size_t)((w4 * 0x1E35A7BDu) >> (32 - kDictHashBits)) * kDictWays;
+      for (int k = 0; k < kDictWays; k++)
+        if (!slot[k]) {
+          slot[k] = ((uint32_t)L << 16) | i;
+          break;
+        }
+    }
+  uint8_t *dd = nullptr;
+  uint32_t *dt = nullptr;
+  if (hipMalloc(&dd, blob.size()) != hipSuccess) return nullptr;
+  if (hipMalloc(&dt, tab.size() * 4) != hipSuccess) {
+    hipFree(dd);
+    return nullptr;
+  }
+  if (hipMemcpy(dd, blob.data(), blob.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dt, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(dd);
+    hipFree(dt);
+    return nullptr;
+  }
+  d.data = dd;
+  d.tab = dt;
+  return &d;
+}
+
 // Encode a group of streams into d_out (packed from out_pos; returns the per-stream sizes).
 int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k, uint8_t *d_out, uint64_t out_cap,
                  uint64_t out_pos, uint64_t *sizes, int32_t (*dc_out)[4], hipStream_t st) {
@@ -197,7 +268,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   std::vector<Mb> mbs;
   std::vector<uint32_t> seg_job;   // per 64 KiB of global positions: its stream
   uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0;
-  bool any_hist = false, any_parts = false;
+  bool any_hist = false, any_parts = false, any_dict = false;
   for (size_t j = 0; j < k; j++) {
     Job &jb = jobs[j];
     memset(&jb, 0, sizeof(jb));
@@ -218,6 +289,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     if (jb.hist_tab) any_hist = true;
     jb.out_base = sd[j].out_base;
     jb.parts = (!jb.uncompressed && wants_parts(sd[j])) ? 1 : 0;
+    jb.dict = (!jb.uncompressed && !sd[j].streaming && !sd[j].hist_tab && prm.quality >= 10 && prm.lgwin <= 22 &&
+               dict_enabled()) ? 1 : 0;
+    jb.dict_span = dict_span();
+    if (jb.dict) any_dict = true;
     if (jb.parts) any_parts = true;
     uint64_t idx_extra = 0;
     if (jb.parts) {
@@ -362,7 +437,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, key_bits, st));
     tm.stop();
     tm.start("find_matches");
+    const DictDev *dd = any_dict ? dict_device(mib_ctx_device_of(ctx)) : nullptr;
+    if (any_dict && !dd) return MIB_E_OUT_OF_MEMORY;
     launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, any_hist, any_parts, matches);
+    if (dd) launch_dict_matches(st, d_jobs, (int)k, dict_span(), dd->tab, dd->data, matches);
     if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
     tm.stop();
     tm.start("lit_histo");

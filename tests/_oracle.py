@@ -78,6 +78,12 @@ def decode(data, out_size=None, dictionary=None):
 PROBE_DTYPE = None
 
 
+def word_refs():
+    """static-dictionary word references the oracle decoder has met in this process"""
+    lib().oracle_word_refs.restype = ctypes.c_uint64
+    return lib().oracle_word_refs()
+
+
 def probe(data, positions):
     """decoder states (parts.h PartEntry layout) at the given ascending output positions:
     the command starting there, or the metablock header starting there (flags bit 2)."""
