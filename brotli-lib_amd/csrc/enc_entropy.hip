@@ -822,6 +822,8 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
 
 // Block (one wave) per (metablock, code slot): literal (block type, cluster), command (block
 // type), distance (block type, cluster); slots beyond the metablock's counts are empty.
+// blocks per metablock: the used codes only (literal codes are at most kMaxLitTrees in all)
+constexpr int kHuffBlocks = kMaxLitTrees + kMaxBT + kMaxBT * kDistCtx;
 __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                                                      const uint32_t *hc, const uint32_t *hd, Codes *codes,
                                                      uint8_t *trees) {
@@ -834,20 +836,38 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ uint16_t code[704];
   __shared__ uint8_t buf[kTreeBytes];
   __shared__ int sh_ok;
-  const int m = blockIdx.x / kTreeSlots, t = blockIdx.x % kTreeSlots;
+  const int m = blockIdx.x / kHuffBlocks, r = blockIdx.x % kHuffBlocks;
   const int lane = threadIdx.x;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
+  auto slot_used = [&](int q) {
+    const bool l = q < kCmdSlot, d = q >= kDistSlot;
+    const int c = l ? q : d ? q - kDistSlot : q - kCmdSlot;
+    return l ? (c / kLitCtx < (int)mb.nbt[0] && c % kLitCtx < (int)mb.nlit_t[c / kLitCtx])
+             : d ? (c / kDistCtx < (int)mb.nbt[2] && c % kDistCtx < (int)mb.ndist_t[c / kDistCtx]) : c < (int)mb.nbt[1];
+  };
+  // the unused slots' sizes are zeroed by the blocks in turn (each slot by one block)
+  if (lane == 0)
+    for (int q = r; q < kTreeSlots; q += kHuffBlocks)
+      if (!slot_used(q)) mb.tree_bits[q] = 0;
+  // block r builds the r-th used code: literal codes first (at most kMaxLitTrees of them,
+  // numbered per block type), then the command codes, then the distance codes
+  int t = -1;
+  if (r < kMaxLitTrees) {
+    int acc = 0;
+    for (int ty = 0; ty < (int)mb.nbt[0] && t < 0; ty++) {
+      if (r < acc + (int)mb.nlit_t[ty]) t = ty * kLitCtx + (r - acc);
+      acc += (int)mb.nlit_t[ty];
+    }
+  } else if (r < kMaxLitTrees + kMaxBT) {
+    t = kCmdSlot + (r - kMaxLitTrees);
+  } else {
+    t = kDistSlot + (r - kMaxLitTrees - kMaxBT);
+  }
+  if (t < 0 || !slot_used(t)) return;
   const bool lit = t < kCmdSlot, dist = t >= kDistSlot;
   const int cl = lit ? t : dist ? t - kDistSlot : t - kCmdSlot;   // slot within its alphabet
-  const bool used = lit ? (cl / kLitCtx < (int)mb.nbt[0] && cl % kLitCtx < (int)mb.nlit_t[cl / kLitCtx])
-                        : dist ? (cl / kDistCtx < (int)mb.nbt[2] && cl % kDistCtx < (int)mb.ndist_t[cl / kDistCtx])
-                               : cl < (int)mb.nbt[1];
-  if (!used) {
-    if (lane == 0) mb.tree_bits[t] = 0;
-    return;
-  }
   const int asize = lit ? 256 : !dist ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
   const uint32_t *src = lit ? hl + ((size_t)m * kLitSlots + cl) * 256 : !dist ? hc + ((size_t)m * kMaxBT + cl) * 704
                                                                           : hd + ((size_t)m * kMaxBT * kDistCtx + cl) * 128;
@@ -1427,7 +1447,7 @@ void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
-  hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * kTreeSlots), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees);
+  hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * kHuffBlocks), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees);
   hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
