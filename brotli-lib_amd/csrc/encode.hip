@@ -609,7 +609,8 @@ struct mib_encoder {
   int32_t dc[4] = {4, 11, 15, 16};
   uint32_t prev_bytes = 0;        // the last two bytes handed to the engine (literal contexts)
   uint64_t block = 1 << 16;       // the reference's 2^lgblock (enc-constants.ts:129-147)
-  uint64_t chunk = 8ull << 20;    // input per device encode: whole blocks, at least this much
+  uint64_t chunk = 32ull << 20;   // input per device encode: whole blocks, at least this much
+                                  // (512 parse segments: 8 MiB left 7/8 of the chip idle in the DP)
   // device state (the default context's device): the window of history plus the chunk,
   // ping-ponged so the next chunk's history is one device copy; the bucket table of earlier
   // positions; the output buffer
@@ -823,6 +824,7 @@ mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
     if (prm.quality >= 9 && prm.lgwin > lgblock) lgblock = std::min(18, prm.lgwin);
   }
   e->block = 1ull << lgblock;
+  e->chunk = (uint64_t)env_u32("MIB_STREAM_CHUNK", (uint32_t)(e->chunk >> 20), 1, 4096) << 20;   // MiB (tests, experiments)
   e->chunk = std::max<uint64_t>(e->block, e->chunk);
   return e;
 }

@@ -120,7 +120,8 @@ def test_corrupt_index_falls_back_to_serial():
         assert got == want, (got, want)
 
 
-def test_streaming_chunks_carry_chained_indexes():
+def test_streaming_chunks_carry_chained_indexes(monkeypatch):
+    monkeypatch.setenv('MIB_STREAM_CHUNK', '8')   # 8 MiB device chunks: three chained indexes
     data = datagen.enwik_text(20 << 20, 9)
     e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24})
     parts = [e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)]
@@ -137,8 +138,9 @@ def test_streaming_chunks_carry_chained_indexes():
     assert brotli_amd.part_stats() == (p0 + 1, f0)
 
 
-def test_streaming_exact_chunks_then_empty_finish():
+def test_streaming_exact_chunks_then_empty_finish(monkeypatch):
     # the chunks use up the input exactly: finish() only adds the final empty metablock
+    monkeypatch.setenv('MIB_STREAM_CHUNK', '8')
     data = datagen.enwik_text(16 << 20, 11)
     e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'mode': 1})
     parts = [e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)]
