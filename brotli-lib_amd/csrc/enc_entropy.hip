@@ -994,7 +994,8 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
       // type histograms (it == kSplitIters: of the final assignment); one type = all units
       for (int x = t; x < A; x += 256) {
         uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-        for (int i = 0; i < nu; i++) {
+#pragma unroll 8
+        for (int i = 0; i < nu; i++) {   // (unrolled: eight unit rows in flight, not one)
           const uint32_t v = H[(size_t)i * kSubHist + x];
           const int a = asg[i];
           s0 += a == 0 ? v : 0u;
@@ -1044,6 +1045,7 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
         float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
         if (ns[i]) {
           const uint32_t *h = H + (size_t)i * kSubHist;
+#pragma unroll 4
           for (int x = t & 63; x < A; x += 64) {
             const float v = (float)h[x];
             c0 += v * bc[0][x];
