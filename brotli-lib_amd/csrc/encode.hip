@@ -164,7 +164,7 @@ uint32_t zopfli_iterations() {
 // bytes at the start of each segment the first iteration parses when it only feeds the
 // model (MIB_ZOPFLI_SAMPLE; >= 64 KiB parses whole segments)
 uint32_t zopfli_sample() {
-  static uint32_t v = env_u32("MIB_ZOPFLI_SAMPLE", 4096, 1024, kSeg);
+  static uint32_t v = env_u32("MIB_ZOPFLI_SAMPLE", 2048, 1024, kSeg);
   return v;
 }
 bool wants_parts(const StreamDesc &d) {
