@@ -18,13 +18,36 @@ namespace enc {
 // wave of find_matches tiles touches stay within one group's streams (cache locality).
 __global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
                                  uint32_t *vals) {
-  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < total; g += gridDim.x * blockDim.x) {
-    uint32_t j = pos_job[g >> kSegBits];
+  // four consecutive positions per thread (total is a multiple of the 64 KiB segment): one
+  // 16-byte load covers their 6-byte keys, and keys / values are stored as uint4
+  for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) * 4; g < total; g += gridDim.x * blockDim.x * 4) {
+    const uint32_t j = pos_job[g >> kSegBits];
     const Job &jb = jobs[j];
-    uint32_t p = g - jb.pos_base;
-    keys[g] = ((j >> gshift) << (kHashBits + 1)) |
-              ((p + (uint32_t)hb <= jb.n && !jb.uncompressed) ? (hb > 4 ? hashn(jb.data + p, hb) : hash4(jb.data + p)) : kInvalidKey);
-    vals[g] = g;
+    const uint32_t p = g - jb.pos_base, grp = (j >> gshift) << (kHashBits + 1);
+    uint32_t k4[4];
+    if (hb == kHashBytes && !jb.uncompressed && p + 16 <= jb.n) {
+      const uintptr_t a = (uintptr_t)(jb.data + p);
+      const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+      const uint32_t sh = (uint32_t)(a & 3);
+      const uint32_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
+      const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(v1, v0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(v2, v1, sh) << 32);
+      const uint64_t hi = __builtin_amdgcn_alignbyte(v3, v2, sh);   // bytes 8..11
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint64_t x = k ? (lo >> (8 * k)) | (hi << (64 - 8 * k)) : lo;
+        const uint64_t v = (x & 0xFFFFFFFFFFFFull) << (64 - 8 * kHashBytes);
+        k4[k] = grp | (uint32_t)((v * 0x1E35A7BD1E35A7BDull) >> (64 - kHashBits));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t q = p + k;
+        k4[k] = grp | ((q + (uint32_t)hb <= jb.n && !jb.uncompressed) ? (hb > 4 ? hashn(jb.data + q, hb) : hash4(jb.data + q))
+                                                                        : kInvalidKey);
+      }
+    }
+    *reinterpret_cast<uint4 *>(keys + g) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
+    *reinterpret_cast<uint4 *>(vals + g) = make_uint4(g, g + 1, g + 2, g + 3);
   }
 }
 // ---------------------------------------------------------------- 2. matches
@@ -321,7 +344,7 @@ __global__ __launch_bounds__(256) void dict_matches_kernel(const Job *jobs, int 
 
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals) {
-  const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total + 255) / 256);
+  const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total / 4 + 255) / 256);
   static const int hb = getenv("MIB_HASH_BYTES") ? std::min(7, std::max(4, atoi(getenv("MIB_HASH_BYTES")))) : kHashBytes;
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, hb, keys, vals);
 }
