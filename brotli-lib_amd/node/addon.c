@@ -344,6 +344,31 @@ static napi_value start_async(napi_env env, napi_callback_info info, int decode)
   CHECK(env, napi_queue_async_work(env, a->work));
   return promise;
 }
+/* woff2Glyf(ttf) / woff2Hmtx(ttf) -> Buffer: the WOFF2-transformed glyf / hmtx table computed on
+ * the GPU (the FONT-mode input of encode for a WOFF2 writer, reference README.md:63); hmtx
+ * gives null when no transform applies */
+static napi_value js_woff2(napi_env env, napi_callback_info info, int hmtx) {
+  size_t argc = 1;
+  napi_value argv[1];
+  CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
+  const uint8_t *p;
+  size_t n;
+  if (argc < 1 || get_bytes(env, argv[0], &p, &n)) {
+    napi_throw_type_error(env, NULL, "input must be a Uint8Array");
+    return NULL;
+  }
+  mib_buf b = {0, 0};
+  const int rc = hmtx ? mib_woff2_transform_hmtx(p, n, &b) : mib_woff2_transform_glyf(p, n, &b);
+  if (rc) return throw_code(env, rc);
+  if (hmtx && !b.size) {
+    napi_value nul;
+    CHECK(env, napi_get_null(env, &nul));
+    return nul;
+  }
+  return take(env, &b);
+}
+static napi_value js_woff2_glyf(napi_env env, napi_callback_info info) { return js_woff2(env, info, 0); }
+static napi_value js_woff2_hmtx(napi_env env, napi_callback_info info) { return js_woff2(env, info, 1); }
 static napi_value js_encode_batch_async(napi_env env, napi_callback_info info) { return start_async(env, info, 0); }
 static napi_value js_decode_batch_async(napi_env env, napi_callback_info info) { return start_async(env, info, 1); }
 
@@ -358,6 +383,8 @@ static napi_value init(napi_env env, napi_value exports) {
       {"encodeBatch", 0, js_encode_batch, 0, 0, 0, napi_default, 0},
       {"encodeBatchAsync", 0, js_encode_batch_async, 0, 0, 0, napi_default, 0},
       {"decodeBatchAsync", 0, js_decode_batch_async, 0, 0, 0, napi_default, 0},
+      {"woff2Glyf", 0, js_woff2_glyf, 0, 0, 0, napi_default, 0},
+      {"woff2Hmtx", 0, js_woff2_hmtx, 0, 0, 0, napi_default, 0},
   };
   napi_define_properties(env, exports, sizeof(props) / sizeof(props[0]), props);
   return exports;

@@ -45,3 +45,7 @@ export declare function brotliEncodeBatch(inputs: Uint8Array[], options?: Brotli
 export declare function brotliEncodeBatchAsync(inputs: Uint8Array[], options?: BrotliEncodeOptions): Promise<Uint8Array[]>
 /** a stream that fails to decode resolves to its Error in its slot */
 export declare function brotliDecodeBatchAsync(inputs: Uint8Array[]): Promise<(Uint8Array | Error)[]>
+/** WOFF2 'glyf' transform (W3C WOFF2 section 5.1) of a TrueType font, on the GPU: FONT-mode input for brotliEncode */
+export declare function woff2TransformGlyf(ttf: Uint8Array): Uint8Array
+/** WOFF2 'hmtx' transform (section 5.4), or null when the table must stay untransformed */
+export declare function woff2TransformHmtx(ttf: Uint8Array): Uint8Array | null

@@ -86,7 +86,18 @@ function brotliDecodeBatchAsync(inputs) {
   return native.decodeBatchAsync(inputs).then((outs) => outs.map((o) => (o instanceof Error ? o : toU8(o))))
 }
 
+// the FONT-mode caller's step before brotliEncode (reference README.md:63): the WOFF2
+// transformed 'glyf' / 'hmtx' tables of a TrueType font, computed on the GPU
+function woff2TransformGlyf(ttf) {
+  return toU8(native.woff2Glyf(ttf))
+}
+function woff2TransformHmtx(ttf) {
+  const r = native.woff2Hmtx(ttf)
+  return r === null ? null : toU8(r)
+}
+
 module.exports = {
   brotliEncode, BrotliEncoder, brotliDecode, brotliDecodedSize, EncoderMode,
   brotliEncodeBatch, brotliEncodeBatchAsync, brotliDecodeBatchAsync,
+  woff2TransformGlyf, woff2TransformHmtx,
 }

@@ -136,6 +136,21 @@ const outs = lib.brotliEncodeBatch(bufs, { quality: 11 })
 for (let i = 0; i < bufs.length; i++) eq(lib.brotliDecode(outs[i]), bufs[i], 'batch ' + i)
 console.log('batch ok')
 
+// WOFF2 transforms of the reference's TrueType bench font, against the fontTools goldens
+{
+  const path = require('path'), crypto = require('crypto')
+  const gold = path.join(__dirname, '..', 'golden', 'woff2')
+  const ttf = new Uint8Array(fs.readFileSync(path.join(__dirname, '..', 'golden', 'bench', 'enc-ttf.bin')))
+  const sha = (u) => crypto.createHash('sha256').update(Buffer.from(u)).digest('hex')
+  const g = JSON.parse(fs.readFileSync(path.join(gold, 'glyf_golden.json')))
+  const h = JSON.parse(fs.readFileSync(path.join(gold, 'hmtx_golden.json')))
+  const glyf = lib.woff2TransformGlyf(ttf)
+  assert.strictEqual(sha(glyf), g.fonts['enc-ttf'].sha256, 'woff2 glyf')
+  assert.strictEqual(sha(lib.woff2TransformHmtx(ttf)), h.fonts['enc-ttf/asis'].sha256, 'woff2 hmtx')
+  eq(lib.brotliDecode(lib.brotliEncode(glyf, { mode: lib.EncoderMode.FONT })), glyf, 'woff2 glyf FONT round trip')
+  console.log('woff2 ok')
+}
+
 // asynchronous batches (napi_async_work): the JS thread stays free while the GPU works
 ;(async () => {
   let ticks = 0
