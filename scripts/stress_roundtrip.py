@@ -37,4 +37,6 @@ while time.time() - t0 < float(sys.argv[2]) if len(sys.argv) > 2 else 60:
         print('FAIL', kind, len(d), seed, q, lg, mode, flush=True)
         sys.exit(1)
     n_ok += 1
+    if n_ok % 100 == 0:
+        print(n_ok, 'round trips', round(time.time() - t0), 's', flush=True)
 print('ok', n_ok, 'round trips', flush=True)
