@@ -1893,7 +1893,18 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       } else {
         int lastv = 0;
         const int nit = U((cl + 63) >> 6);
-        if (dist >= cl) {
+        if (dist >= cl && nit <= 4) {
+          // up to 256 bytes: every load issued before the first store (one round trip, not nit)
+          const int v0 = lane < cl ? (int)ring[src + lane] : 0;
+          const int v1 = lane + 64 < cl ? (int)ring[src + 64 + lane] : 0;
+          const int v2 = lane + 128 < cl ? (int)ring[src + 128 + lane] : 0;
+          const int v3 = lane + 192 < cl ? (int)ring[src + 192 + lane] : 0;
+          if (lane < cl) ring[pos + lane] = (uint8_t)v0;
+          if (lane + 64 < cl) ring[pos + 64 + lane] = (uint8_t)v1;
+          if (lane + 128 < cl) ring[pos + 128 + lane] = (uint8_t)v2;
+          if (lane + 192 < cl) ring[pos + 192 + lane] = (uint8_t)v3;
+          lastv = lane + 192 < cl ? v3 : lane + 128 < cl ? v2 : lane + 64 < cl ? v1 : v0;
+        } else if (dist >= cl) {
           for (int it = 0; it < nit; it++) {
             const int k = it * 64 + lane;
             if (k < cl) {
