@@ -375,8 +375,10 @@ __device__ __forceinline__ uint32_t header_bits(const Codes &cd, const Cmd &c, c
   if (switch_at(u, 1, q)) bits += switch_bits(cd, 1, u);
   return bits;
 }
-__device__ __forceinline__ int literal_tree(const Mb &mb, const uint8_t *lut, const Unit &u, uint32_t p12) {
-  return mb.lit_cmap[u.type[0] * kLitCtx + (lut[p12 & 0xFF] | lut[256 + (p12 >> 8)])];
+// (lut, cmap: the context-mode table and the metablock's literal context map, LDS copies in
+// the sizes / emit kernels)
+__device__ __forceinline__ int literal_tree(const uint8_t *cmap, const uint8_t *lut, const Unit &u, uint32_t p12) {
+  return cmap[u.type[0] * kLitCtx + (lut[p12 & 0xFF] | lut[256 + (p12 >> 8)])];
 }
 __device__ __forceinline__ uint32_t dist_bits(const Codes &cd, const Mb &mb, const Cmd &c, const Unit &u, uint32_t q) {
   if (!c.copy || c.cmd_prefix < 128) return 0;
@@ -386,14 +388,14 @@ __device__ __forceinline__ uint32_t dist_bits(const Codes &cd, const Mb &mb, con
 }
 // bits of item k of command c (insert at stream position p); su: the segment's units (the
 // command's header and distance go by the unit of p, each literal by its own position's)
-__device__ __forceinline__ uint32_t item_bits(const Codes &cd, const Mb &mb, const uint8_t *lut, const Job &jb,
+__device__ __forceinline__ uint32_t item_bits(const Codes &cd, const Mb &mb, const uint8_t *cmap, const uint8_t *lut, const Job &jb,
                                               const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q,
                                               uint32_t k) {
   if (k == 0) return header_bits(cd, c, su[unit_of(sg, p)], q);
   if (k > c.ins) return dist_bits(cd, mb, c, su[unit_of(sg, p)], q);
   const uint32_t lp = p + k - 1;
   const Unit &ul = su[unit_of(sg, lp)];
-  return (lit_switch_at(ul, lp) ? switch_bits(cd, 0, ul) : 0u) + cd.ld[literal_tree(mb, lut, ul, prev2(jb, lp))][jb.data[lp]];
+  return (lit_switch_at(ul, lp) ? switch_bits(cd, 0, ul) : 0u) + cd.ld[literal_tree(cmap, lut, ul, prev2(jb, lp))][jb.data[lp]];
 }
 
 // Load-balanced expansion of a batch of at most B commands into their items: off[j] is the

@@ -108,7 +108,7 @@ __device__ __forceinline__ void put_switch(W &wr, const Codes &cd, int cat, cons
 
 // item k of command q (see item_bits in enc_common.h: same bits, in stream order)
 template <class W>
-__device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb, const uint8_t *lut, const Job &jb,
+__device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb, const uint8_t *cmap, const uint8_t *lut, const Job &jb,
                                            const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q, uint32_t k) {
   const Unit &u = su[unit_of(sg, p)];
   if (k == 0) {
@@ -125,7 +125,7 @@ __device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb,
     const Unit &ul = su[unit_of(sg, lp)];
     if (lit_switch_at(ul, lp)) put_switch(wr, cd, 0, ul);
     const uint32_t lit = jb.data[lp];
-    const int tree = literal_tree(mb, lut, ul, prev2(jb, lp));
+    const int tree = literal_tree(cmap, lut, ul, prev2(jb, lp));
     wr.put(cd.ld[tree][lit], cd.lc[tree][lit]);
   } else if (c.copy && c.cmd_prefix >= 128) {
     if (switch_at(u, 2, q)) put_switch(wr, cd, 2, u);
@@ -160,7 +160,11 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   const int t = threadIdx.x;
   const Codes &cd = codes[sg.mb];
   const Mb &mb = mbs[sg.mb];
-  const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
+  __shared__ uint8_t sh_lut[512], sh_cmap[kLitSlots];   // per-literal lookups from LDS
+  for (int i = t; i < 512; i += kBlock) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
+  for (int i = t; i < kLitSlots; i += kBlock) sh_cmap[i] = mb.lit_cmap[i];
+  __syncthreads();
+  const uint8_t *lut = sh_lut;
   uint32_t *words = reinterpret_cast<uint32_t *>(out + jb.out_off);
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
           kk[e] = i - map.off[j];
           const Cmd &k = sh_c[j];
           const uint32_t p = sh_p[j];
-          bits[e] = item_bits(cd, mb, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
+          bits[e] = item_bits(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
         }
       }
       uint32_t boff[kEmitItems], total;
@@ -212,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
         const uint32_t p = sh_p[jj];
         OrW<false> wr;
         wr.init(win, rel0 + boff[e]);
-        write_item(wr, cd, mb, lut, jb, k, p, sg, sh_u, base + jj, kk[e]);
+        write_item(wr, cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + jj, kk[e]);
         wr.finish();
       }
       __syncthreads();

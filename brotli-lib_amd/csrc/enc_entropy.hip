@@ -1359,7 +1359,11 @@ __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *seg
   const int t = threadIdx.x;
   const Mb &mb = mbs[sg.mb];
   const Codes &cd = codes[sg.mb];
-  const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
+  __shared__ uint8_t sh_lut[512], sh_cmap[kLitSlots];   // per-literal lookups from LDS
+  for (int i = t; i < 512; i += kBlock) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
+  for (int i = t; i < kLitSlots; i += kBlock) sh_cmap[i] = mb.lit_cmap[i];
+  __syncthreads();
+  const uint8_t *lut = sh_lut;
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
   if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
   unsigned long long bits = 0;
@@ -1379,7 +1383,7 @@ __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *seg
     for (uint32_t i = t; i < nitems; i += kBlock) {
       const uint32_t j = map.find(i, nb);
       const uint32_t p = sh_p[j];
-      bits += item_bits(cd, mb, lut, jb, sh_c[j], p, sg, sh_u, base + j, i - map.off[j]);
+      bits += item_bits(cd, mb, sh_cmap, lut, jb, sh_c[j], p, sg, sh_u, base + j, i - map.off[j]);
     }
     __syncthreads();
   }
