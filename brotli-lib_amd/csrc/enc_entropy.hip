@@ -234,8 +234,9 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
   const Mb &mb = mbs[sg.mb];
-  const uint8_t *lut = kRfcContextLut + (mb.ctx_mode << 9);
   const int t = threadIdx.x;
+  __shared__ uint8_t lut[512];   // the context-mode table, per-literal lookups from LDS
+  for (int i = t; i < 512; i += kBlock) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
   for (int i = t; i < kMaxBT * 704; i += kBlock) sh_c[i] = 0;
