@@ -333,12 +333,13 @@ __device__ __forceinline__ float hist_cost(float bits, int nnz) {
 constexpr int kCluT = 1024;
 __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
   constexpr int kMaxH = kLitCtx;
-  __shared__ uint32_t h[kMaxH][256];
+  // rows padded by one word: lanes reading one symbol of 64 different histograms hit 64 banks
+  __shared__ uint32_t h[kMaxH][257];
   __shared__ float cost[kMaxH];
   __shared__ float save[kMaxH][kMaxH];
   __shared__ int alive[kMaxH], label[kMaxH];
-  __shared__ float red_v[kCluT];
-  __shared__ int red_i[kCluT];
+  __shared__ float red_v[kCluT / 64];
+  __shared__ int red_i[kCluT / 64];
   __shared__ int sh_best, sh_alive;
   const int m = blockIdx.x / (2 * kMaxBT), kind = (blockIdx.x / kMaxBT) & 1, ty = blockIdx.x % kMaxBT;
   Mb &mb = mbs[m];
@@ -402,47 +403,72 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     if (sum > 0.f) ent += sum * __log2f(sum);
     return cost[a] + cost[b] - hist_cost(ent, nnz);
   };
-  for (int p = t; p < nh * nh; p += kCluT) {
-    const int a = p / nh, b = p % nh;
-    save[a][b] = (a < b && alive[a] && alive[b]) ? pair_saving(a, b) : -1e30f;
+  for (int p = t; p < kMaxH * kMaxH; p += kCluT) save[p / kMaxH][p % kMaxH] = -1e30f;
+  __syncthreads();
+  // only the nh (nh - 1) / 2 pairs a < b, folded into nh / 2 rows of nh - 1: row r holds
+  // (r, r+1 .. nh-1) and (nh-1-r, nh-r .. nh-1)
+  for (int p = t; p < (nh / 2) * (nh - 1); p += kCluT) {
+    const int r = p / (nh - 1), c = p % (nh - 1);
+    const int a = c >= r ? r : nh - 1 - r, b = c >= r ? c + 1 : nh - r + c;
+    if (alive[a] && alive[b]) save[a][b] = pair_saving(a, b);
   }
   __syncthreads();
   for (;;) {
     // best pair
     float bv = -1e30f;
     int bi = -1;
-    for (int p = t; p < nh * nh; p += kCluT) {
-      const float v = save[p / nh][p % nh];
+    // the whole (padded) table: flat index a * kMaxH + b orders pairs as a * nh + b does
+    for (int p = t; p < kMaxH * kMaxH; p += kCluT) {
+      const float v = save[p / kMaxH][p % kMaxH];
       if (v > bv) {
         bv = v;
         bi = p;
       }
     }
-    red_v[t] = bv;
-    red_i[t] = bi;
-    __syncthreads();
-    for (int o = kCluT / 2; o; o >>= 1) {
-      if (t < o && (red_v[t + o] > red_v[t] || (red_v[t + o] == red_v[t] && red_i[t + o] >= 0 &&
-                                                 (red_i[t] < 0 || red_i[t + o] < red_i[t])))) {
-        red_v[t] = red_v[t + o];
-        red_i[t] = red_i[t + o];
+    // the largest saving, ties to the lowest pair index: within the wave by shuffles, then
+    // one wave over the 16 wave winners
+    auto better = [](float v, int i, float bv, int bi) {
+      return v > bv || (v == bv && i >= 0 && (bi < 0 || i < bi));
+    };
+    for (int o = 32; o; o >>= 1) {
+      const float v = __shfl_xor(bv, o);
+      const int i = __shfl_xor(bi, o);
+      if (better(v, i, bv, bi)) {
+        bv = v;
+        bi = i;
       }
-      __syncthreads();
     }
-    if (t == 0) sh_best = (red_v[0] > 0.f || (sh_alive > cap && red_v[0] > -1e29f)) ? red_i[0] : -1;
+    if ((t & 63) == 0) {
+      red_v[t >> 6] = bv;
+      red_i[t >> 6] = bi;
+    }
+    __syncthreads();
+    if (t < 64) {
+      bv = t < kCluT / 64 ? red_v[t] : -1e30f;
+      bi = t < kCluT / 64 ? red_i[t] : -1;
+      for (int o = 32; o; o >>= 1) {
+        const float v = __shfl_xor(bv, o);
+        const int i = __shfl_xor(bi, o);
+        if (better(v, i, bv, bi)) {
+          bv = v;
+          bi = i;
+        }
+      }
+      if (t == 0) sh_best = (bv > 0.f || (sh_alive > cap && bv > -1e29f)) ? bi : -1;
+    }
     __syncthreads();
     const int best = sh_best;
     if (best < 0) break;
-    const int a = best / nh, b = best % nh;   // merge b into a
+    const int a = best / kMaxH, b = best % kMaxH;   // merge b into a
     for (int x = t; x < A; x += kCluT) h[a][x] += h[b][x];
     __syncthreads();
     if (t == 0) {
       cost[a] = cost[a] + cost[b] - save[a][b];
       alive[b] = 0;
       sh_alive--;
-      for (int q = 0; q < nh; q++)
-        if (label[q] == b) label[q] = a;
     }
+    for (int q = t; q < nh; q += kCluT)
+      if (label[q] == b) label[q] = a;
     __syncthreads();
     // pairs with b die; pairs with a change: a wave per pair, lanes over the symbols
     for (int q = t; q < nh; q += kCluT) save[min(q, b)][max(q, b)] = -1e30f;
