@@ -328,15 +328,19 @@ __device__ __forceinline__ float hist_cost(float bits, int nnz) {
 // Block per (metablock, literal | distance, block type): the type's context histograms.  A
 // literal block type may keep at most kMaxLitTrees / (literal block types) codes: past that
 // cap the cheapest merge is taken even when it costs bits.
-// 16 waves: the LDS working set (64 histograms) allows one block per CU, and a lone wave per
-// SIMD would leave every LDS round trip of the merge loop exposed
-constexpr int kCluT = 1024;
+// 8 waves, and a working set (64 histograms + the a < b pair savings) small enough for two
+// blocks per CU: one block's barriers and LDS round trips in the merge loop overlap the other's
+constexpr int kCluT = 512;
+constexpr int kCluPairs = kLitCtx * (kLitCtx - 1) / 2;
+// pair (a, b), a < b, in the triangular savings table; lexicographic, as a * 64 + b orders them
+__device__ __forceinline__ int tri(int a, int b) { return a * (2 * kLitCtx - a - 1) / 2 + b - a - 1; }
 __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
   constexpr int kMaxH = kLitCtx;
   // rows padded by one word: lanes reading one symbol of 64 different histograms hit 64 banks
   __shared__ uint32_t h[kMaxH][257];
   __shared__ float cost[kMaxH];
-  __shared__ float save[kMaxH][kMaxH];
+  __shared__ float save[kCluPairs];
+  __shared__ uint16_t pair_of[kCluPairs];   // tri index -> a << 8 | b
   __shared__ int alive[kMaxH], label[kMaxH];
   __shared__ float red_v[kCluT / 64];
   __shared__ int red_i[kCluT / 64];
@@ -403,23 +407,29 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     if (sum > 0.f) ent += sum * __log2f(sum);
     return cost[a] + cost[b] - hist_cost(ent, nnz);
   };
-  for (int p = t; p < kMaxH * kMaxH; p += kCluT) save[p / kMaxH][p % kMaxH] = -1e30f;
+  for (int p = t; p < kMaxH * kMaxH; p += kCluT) {
+    const int a = p / kMaxH, b = p % kMaxH;
+    if (a < b) {
+      save[tri(a, b)] = -1e30f;
+      pair_of[tri(a, b)] = (uint16_t)(a << 8 | b);
+    }
+  }
   __syncthreads();
   // only the nh (nh - 1) / 2 pairs a < b, folded into nh / 2 rows of nh - 1: row r holds
   // (r, r+1 .. nh-1) and (nh-1-r, nh-r .. nh-1)
   for (int p = t; p < (nh / 2) * (nh - 1); p += kCluT) {
     const int r = p / (nh - 1), c = p % (nh - 1);
     const int a = c >= r ? r : nh - 1 - r, b = c >= r ? c + 1 : nh - r + c;
-    if (alive[a] && alive[b]) save[a][b] = pair_saving(a, b);
+    if (alive[a] && alive[b]) save[tri(a, b)] = pair_saving(a, b);
   }
   __syncthreads();
   for (;;) {
     // best pair
     float bv = -1e30f;
     int bi = -1;
-    // the whole (padded) table: flat index a * kMaxH + b orders pairs as a * nh + b does
-    for (int p = t; p < kMaxH * kMaxH; p += kCluT) {
-      const float v = save[p / kMaxH][p % kMaxH];
+    // the whole table: its index orders pairs as a * nh + b does
+    for (int p = t; p < kCluPairs; p += kCluT) {
+      const float v = save[p];
       if (v > bv) {
         bv = v;
         bi = p;
@@ -459,11 +469,11 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     __syncthreads();
     const int best = sh_best;
     if (best < 0) break;
-    const int a = best / kMaxH, b = best % kMaxH;   // merge b into a
+    const int a = pair_of[best] >> 8, b = pair_of[best] & 0xFF;   // merge b into a
     for (int x = t; x < A; x += kCluT) h[a][x] += h[b][x];
     __syncthreads();
     if (t == 0) {
-      cost[a] = cost[a] + cost[b] - save[a][b];
+      cost[a] = cost[a] + cost[b] - save[best];
       alive[b] = 0;
       sh_alive--;
     }
@@ -471,13 +481,14 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
       if (label[q] == b) label[q] = a;
     __syncthreads();
     // pairs with b die; pairs with a change: a wave per pair, lanes over the symbols
-    for (int q = t; q < nh; q += kCluT) save[min(q, b)][max(q, b)] = -1e30f;
+    for (int q = t; q < nh; q += kCluT)
+      if (q != b) save[tri(min(q, b), max(q, b))] = -1e30f;
     __syncthreads();
     for (int q = t >> 6; q < nh; q += kCluT / 64) {
       if (q == a || q == b) continue;
       const int lo = min(q, a), hi = max(q, a);
       if (!alive[q]) {
-        if ((t & 63) == 0) save[lo][hi] = -1e30f;
+        if ((t & 63) == 0) save[tri(lo, hi)] = -1e30f;
         continue;
       }
       float sum = 0.f, ent = 0.f;
@@ -497,7 +508,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
       }
       if ((t & 63) == 0) {
         if (sum > 0.f) ent += sum * __log2f(sum);
-        save[lo][hi] = cost[lo] + cost[hi] - hist_cost(ent, nnz);
+        save[tri(lo, hi)] = cost[lo] + cost[hi] - hist_cost(ent, nnz);
       }
     }
     __syncthreads();
