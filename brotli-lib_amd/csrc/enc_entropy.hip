@@ -328,9 +328,10 @@ __device__ __forceinline__ float hist_cost(float bits, int nnz) {
 // Block per (metablock, literal | distance, block type): the type's context histograms.  A
 // literal block type may keep at most kMaxLitTrees / (literal block types) codes: past that
 // cap the cheapest merge is taken even when it costs bits.
-// 8 waves, and a working set (64 histograms + the a < b pair savings) small enough for two
-// blocks per CU: one block's barriers and LDS round trips in the merge loop overlap the other's
-constexpr int kCluT = 512;
+// 16 waves, and a working set (64 histograms + the a < b pair savings) small enough for two
+// blocks per CU (44 VGPRs: 8 waves per SIMD): one block's barriers and LDS round trips in the
+// merge loop overlap the other's
+constexpr int kCluT = 1024;
 constexpr int kCluPairs = kLitCtx * (kLitCtx - 1) / 2;
 // pair (a, b), a < b, in the triangular savings table; lexicographic, as a * 64 + b orders them
 __device__ __forceinline__ int tri(int a, int b) { return a * (2 * kLitCtx - a - 1) / 2 + b - a - 1; }
