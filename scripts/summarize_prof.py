@@ -55,9 +55,11 @@ def main(tag):
     # bench.py names kernels by its event labels; map the HIP symbol names onto them
     alias = {'decode_streams_kernel': 'decode_streams_kernel', 'find_matches_kernel': 'find_matches',
              'dp_kernel': 'dp_parse', 'emit_kernel': 'emit', 'assemble_kernel': 'assemble'}
-    for src, dst in alias.items():
-        if src in kernels:
-            kernels[dst] = kernels[src]
+    for src, dst in alias.items():   # templated kernels: the first instantiation with the base name
+        hit = [k for k in sorted(kernels) if k == src or k.startswith(src + '<') and 'true' in k]
+        hit = hit or [k for k in sorted(kernels) if k.startswith(src + '<')]
+        if hit:
+            kernels[dst] = kernels[hit[0]]
     with open(os.path.join(ROOT, 'profiles', 'pmc_summary.json'), 'w') as f:
         json.dump({'tag': tag, 'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of '
                    'bench.py --steps 1 --warmup 1 (scripts/gpu_profile.sh)',

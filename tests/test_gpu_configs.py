@@ -88,3 +88,20 @@ def test_context_on_last_device():
     assert status == [0] and sizes == [len(d)]
     assert bytes(out[:len(d)].cpu().numpy().tobytes()) == d
     assert _oracle.decode(comp[:off[1]].cpu().numpy().tobytes()) == d
+
+
+def test_default_context_from_threads():
+    """ctypes drops the GIL: concurrent brotliEncode / brotliDecode on the default context
+    are serialised by the library (runtime.cpp g_default_mu), never interleaved."""
+    from concurrent.futures import ThreadPoolExecutor
+    bufs = [datagen.enwik_text(200000 + 4099 * i, 40 + i) for i in range(8)]
+
+    def trip(d):
+        enc = brotli_amd.brotliEncode(d, {'quality': 11 if len(d) % 2 else 9})
+        return enc, brotli_amd.brotliDecode(enc)
+
+    with ThreadPoolExecutor(8) as ex:
+        res = list(ex.map(trip, bufs * 2))
+    for (enc, dec), d in zip(res, bufs * 2):
+        assert dec == d
+        assert _oracle.decode(enc) == d
