@@ -989,7 +989,11 @@ constexpr int kSplitIters = 4;
 __device__ __forceinline__ float sym_bits(uint32_t c, float log_total) {
   return c ? log_total - __log2f((float)c) : log_total + 2.f;
 }
-__global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h,
+// NT threads per (metablock, category) block: 1024 when the blocks do not fill the chip (one
+// long stream: its few metablocks), else 256; the type histograms sum NT / 256 unit ranges in
+// parallel, every float sum keeps the 256-thread grouping (identical output either way)
+template <int NT>
+__global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h,
                                                     Codes *codes) {
   __shared__ uint32_t th[kMaxBT][704];
   __shared__ float bc[kMaxBT][704];
@@ -997,7 +1001,8 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
   __shared__ uint8_t asg[kMaxUnits], bp[kMaxUnits];
   __shared__ uint32_t ns[kMaxUnits];   // the units' symbol counts (the serial steps read them from LDS)
   __shared__ uint32_t tot[kMaxBT];
-  __shared__ float red[256];
+  constexpr int kSplitT = NT;
+  __shared__ float red[kSplitT];
   __shared__ int sh_ne, sh_keep;
   const int m = blockIdx.x / 3, cat = blockIdx.x % 3;
   Mb &mb = mbs[m];
@@ -1011,7 +1016,7 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
   const int nu = (int)mb.nseg * kSubPerSeg;
   Unit *U = units + u0;
   const uint32_t *H = unit_h + (size_t)u0 * kSubHist + hoff;
-  for (int i = t; i < nu; i += 256) ns[i] = U[i].nsym[cat];
+  for (int i = t; i < nu; i += kSplitT) ns[i] = U[i].nsym[cat];
   __syncthreads();
   // seed: the non-empty units in kMaxBT contiguous runs
   if (t == 0) {
@@ -1030,22 +1035,29 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
   if (ne >= 2 * kMaxBT) {
     float base_cost = 0.f;
     for (int it = 0; it <= kSplitIters; it++) {
-      // type histograms (it == kSplitIters: of the final assignment); one type = all units
-      for (int x = t; x < A; x += 256) {
-        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+      // type histograms (it == kSplitIters: of the final assignment); one type = all units.
+      // NT / 256 unit ranges in parallel (256 symbols each), summed with LDS atomics
+      for (int x = t; x < A; x += kSplitT)
+        for (int q = 0; q < kMaxBT; q++) th[q][x] = 0;
+      __syncthreads();
+      {
+        const int qd = t >> 8, i0 = (nu * qd) / (kSplitT / 256), i1 = (nu * (qd + 1)) / (kSplitT / 256);
+        for (int x = t & 255; x < A; x += 256) {
+          uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
 #pragma unroll 8
-        for (int i = 0; i < nu; i++) {   // (unrolled: eight unit rows in flight, not one)
-          const uint32_t v = H[(size_t)i * kSubHist + x];
-          const int a = asg[i];
-          s0 += a == 0 ? v : 0u;
-          s1 += a == 1 ? v : 0u;
-          s2 += a == 2 ? v : 0u;
-          s3 += a == 3 ? v : 0u;
+          for (int i = i0; i < i1; i++) {   // (unrolled: eight unit rows in flight, not one)
+            const uint32_t v = H[(size_t)i * kSubHist + x];
+            const int a = asg[i];
+            s0 += a == 0 ? v : 0u;
+            s1 += a == 1 ? v : 0u;
+            s2 += a == 2 ? v : 0u;
+            s3 += a == 3 ? v : 0u;
+          }
+          if (s0) atomicAdd(&th[0][x], s0);
+          if (s1) atomicAdd(&th[1][x], s1);
+          if (s2) atomicAdd(&th[2][x], s2);
+          if (s3) atomicAdd(&th[3][x], s3);
         }
-        th[0][x] = s0;
-        th[1][x] = s1;
-        th[2][x] = s2;
-        th[3][x] = s3;
       }
       __syncthreads();
       if (t < kMaxBT) {
@@ -1059,7 +1071,7 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
         const uint32_t all = tot[0] + tot[1] + tot[2] + tot[3];
         const float la = __log2f((float)all);
         int nz = 0;
-        for (int x = t; x < A; x += 256) {
+        for (int x = t; t < 256 && x < A; x += 256) {
           const uint32_t c = th[0][x] + th[1][x] + th[2][x] + th[3][x];
           if (c) {
             part += (float)c * (la - __log2f((float)c));
@@ -1068,19 +1080,19 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
         }
         red[t] = part + 3.5f * (float)nz;
         __syncthreads();
-        for (int o = 128; o; o >>= 1) {
+        for (int o = kSplitT / 2; o; o >>= 1) {
           if (t < o) red[t] += red[t + o];
           __syncthreads();
         }
         base_cost = red[0] + 40.f;
         __syncthreads();
       }
-      for (int x = t; x < A; x += 256)
+      for (int x = t; x < A; x += kSplitT)
         for (int q = 0; q < kMaxBT; q++) bc[q][x] = tot[q] ? sym_bits(th[q][x], __log2f((float)tot[q])) : 1e9f;
       __syncthreads();
       if (it == kSplitIters) break;
       // every unit's bits under every type: a wave per unit, lanes over the symbols
-      for (int i = t >> 6; i < nu; i += 4) {
+      for (int i = t >> 6; i < nu; i += kSplitT / 64) {
         float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
         if (ns[i]) {
           const uint32_t *h = H + (size_t)i * kSubHist;
@@ -1149,18 +1161,18 @@ __global__ __launch_bounds__(256) void split_kernel(const Job *jobs, Mb *mbs, in
       __syncthreads();
     }
     // the split's cost: unit bits under the final histograms, switches, one code header per type
-    float part = 0.f;
-    for (int i = t >> 6; i < nu; i += 4) {
+    float part = 0.f;   // (the first 256 threads, in the same grouping as ever: identical sums)
+    for (int i = t >> 6; t < 256 && i < nu; i += 4) {
       if (!ns[i]) continue;
       const uint32_t *h = H + (size_t)i * kSubHist;
       const int q = asg[i];
       for (int x = t & 63; x < A; x += 64) part += (float)h[x] * bc[q][x];
     }
-    for (int x = t; x < A; x += 256)
+    for (int x = t; t < 256 && x < A; x += 256)
       for (int q = 0; q < kMaxBT; q++) part += th[q][x] ? 3.5f : 0.f;
     red[t] = part;
     __syncthreads();
-    for (int o = 128; o; o >>= 1) {
+    for (int o = kSplitT / 2; o; o >>= 1) {
       if (t < o) red[t] += red[t + o];
       __syncthreads();
     }
@@ -1475,7 +1487,10 @@ void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mb
   hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
 }
 void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes) {
-  hipLaunchKernelGGL(split_kernel, dim3(nmbs * 3), dim3(256), 0, st, jobs, mbs, nmbs, units, unit_h, codes);
+  if (nmbs * 3 <= 256)
+    hipLaunchKernelGGL(split_kernel<1024>, dim3(nmbs * 3), dim3(1024), 0, st, jobs, mbs, nmbs, units, unit_h, codes);
+  else
+    hipLaunchKernelGGL(split_kernel<256>, dim3(nmbs * 3), dim3(256), 0, st, jobs, mbs, nmbs, units, unit_h, codes);
 }
 void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
