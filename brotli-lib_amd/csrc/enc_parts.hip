@@ -113,71 +113,100 @@ void launch_ring_scan(hipStream_t st, Job *jobs, int njobs, Seg *segs, int nsegs
   hipLaunchKernelGGL(ring_scan_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, push);
 }
 
-// Lane per stream: the entries in stream order, then the metadata block (window bits, header,
-// payload) at the front of the stream's output slice.
-__global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, const Unit *units,
-                                  const PushSum *push, uint8_t *out) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// Wave per stream: the entries in stream order, then the metadata block (window bits, header,
+// payload) at the front of the stream's output slice.  The walk is serial in its state (ring,
+// block types, remaining block lengths) but not in its inputs: the lanes stage 64 segments at
+// a time (Seg, pushes, block-split units, the two bytes before the entry) in LDS, so the walk
+// pays one memory round trip per 64 segments instead of several per segment.
+constexpr int kPiChunk = 64;
+__global__ __launch_bounds__(kPiChunk) void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, const Seg *segs,
+                                                              const Unit *units, const PushSum *push, uint8_t *out) {
+  __shared__ Seg s_seg[kPiChunk];
+  __shared__ PushSum s_push[kPiChunk];
+  __shared__ Unit s_unit[kPiChunk * kSubPerSeg];
+  __shared__ uint32_t s_p12[kPiChunk];
+  const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= njobs) return;
   const Job &jb = jobs[j];
   if (!jb.parts || jb.uncompressed) return;
   uint8_t *o = out + jb.out_off;
   const int wb = jb.hdr_lgwin ? window_bits_len((int)jb.hdr_lgwin) : 0;
   const int nb = part_skip_bytes(jb.idx_payload);
-  BitW w{o, 0};
-  if (jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
-  w.put(1, 0);                       // ISLAST
-  w.put(2, 3);                       // MNIBBLES: metadata
-  w.put(1, 0);                       // reserved
-  w.put(2, (uint32_t)nb);            // MSKIPBYTES
-  w.put(8 * nb, jb.idx_payload - 1);   // MSKIPLEN - 1 (then zero bits to the byte boundary)
-  uint8_t *pay = o + ((uint64_t)(wb + 6 + 8 * nb) + 7) / 8;
-  PartHead h;
-  h.magic = kPartMagic;
-  h.version = 1;
-  h.entry_bytes = (uint16_t)sizeof(PartEntry);
   const uint32_t every = 1u << (jb.part_bits - kSegBits);   // segments per part
-  h.nentries = (jb.nseg + every - 1) / every;
-  h.lgwin = jb.lgwin;
-  h.next_byte = jb.final_ ? 0 : jb.out_base + ((jb.total_bits + 7) >> 3);
-  h.total = (uint64_t)jb.abs_base + jb.n;
-  const uint8_t *hb = reinterpret_cast<const uint8_t *>(&h);
-  for (int i = 0; i < (int)sizeof(h); i++) pay[i] = hb[i];
+  uint8_t *pay = o + ((uint64_t)(wb + 6 + 8 * nb) + 7) / 8;
+  if (lane == 0) {
+    BitW w{o, 0};
+    if (jb.hdr_lgwin) put_window_bits(w, (int)jb.hdr_lgwin);
+    w.put(1, 0);                       // ISLAST
+    w.put(2, 3);                       // MNIBBLES: metadata
+    w.put(1, 0);                       // reserved
+    w.put(2, (uint32_t)nb);            // MSKIPBYTES
+    w.put(8 * nb, jb.idx_payload - 1);   // MSKIPLEN - 1 (then zero bits to the byte boundary)
+    PartHead h;
+    h.magic = kPartMagic;
+    h.version = 1;
+    h.entry_bytes = (uint16_t)sizeof(PartEntry);
+    h.nentries = (jb.nseg + every - 1) / every;
+    h.lgwin = jb.lgwin;
+    h.next_byte = jb.final_ ? 0 : jb.out_base + ((jb.total_bits + 7) >> 3);
+    h.total = (uint64_t)jb.abs_base + jb.n;
+    const uint8_t *hb = reinterpret_cast<const uint8_t *>(&h);
+    for (int i = 0; i < (int)sizeof(h); i++) pay[i] = hb[i];
+  }
   uint8_t *ent = pay + sizeof(PartHead);
   uint32_t ring[4];
   for (int q = 0; q < 4; q++) ring[q] = (uint32_t)jb.dc_in[q];
   const uint64_t bit0 = 8 * jb.out_base;
+  const uint32_t seg_end = jb.seg_base + jb.nseg;
+  uint32_t c0 = ~0u;   // first segment staged in LDS
   for (uint32_t m = 0; m < jb.nmb; m++) {
     const Mb &mb = mbs[jb.mb_base + m];
     uint32_t type[3] = {0, 0, 0}, prev[3] = {1, 1, 1}, blen[3];
     for (int c = 0; c < 3; c++) blen[c] = mb.nbt[c] > 1 ? mb.first_count[c] : (1u << 28);
     for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
-      const Seg &sg = segs[s];
-      PartEntry e;
-      const bool at_mb = s == mb.first_seg;
-      const bool has_cmd = sg.ncmd + (sg.extra_ins ? 1 : 0) > 0;
-      const uint32_t p = at_mb ? mb.start : sg.start - sg.carry_in;
-      e.flags = at_mb ? (kPartValid | kPartAtMb) : has_cmd ? kPartValid : 0u;
-      e.bit = bit0 + (at_mb ? mb.bit_off : sg.bit_off);
-      e.pos = (uint64_t)jb.abs_base + p;
-      e.mb_bit = bit0 + mb.bit_off;
-      e.mb_pos = (uint64_t)jb.abs_base + mb.start;
-      for (int q = 0; q < 4; q++) e.ring[q] = ring[q];
-      for (int c = 0; c < 3; c++) {
-        e.blen[c] = at_mb ? 0 : blen[c];
-        e.type[c] = (uint8_t)(at_mb ? 0 : type[c]);
-        e.prev[c] = (uint8_t)(at_mb ? 0 : prev[c]);
+      if (c0 == ~0u || s - c0 >= (uint32_t)kPiChunk) {   // (uniform) stage the next 64 segments
+        c0 = s;
+        __syncthreads();
+        const uint32_t ls = c0 + lane;
+        if (ls < seg_end) {
+          const Seg sg = segs[ls];
+          s_seg[lane] = sg;
+          s_push[lane] = push[ls];
+          const Mb &lm = mbs[sg.mb];
+          const uint32_t p = ls == lm.first_seg ? lm.start : sg.start - sg.carry_in;
+          s_p12[lane] = prev2(jb, p);
+        }
+        for (int i = lane; i < kPiChunk * kSubPerSeg; i += kPiChunk)
+          if (c0 + i / kSubPerSeg < seg_end) s_unit[i] = units[(size_t)c0 * kSubPerSeg + i];
+        __syncthreads();
       }
-      const uint32_t p12 = prev2(jb, p);
-      e.p1 = (uint8_t)(p12 & 0xFF);
-      e.p2 = (uint8_t)(p12 >> 8);
-      if ((s - jb.seg_base) % every == 0) {   // a part starts at this segment
+      const uint32_t k = s - c0;
+      const Seg &sg = s_seg[k];
+      const bool at_mb = s == mb.first_seg;
+      if (lane == 0 && (s - jb.seg_base) % every == 0) {   // a part starts at this segment
+        PartEntry e;
+        const bool has_cmd = sg.ncmd + (sg.extra_ins ? 1 : 0) > 0;
+        const uint32_t p = at_mb ? mb.start : sg.start - sg.carry_in;
+        e.flags = at_mb ? (kPartValid | kPartAtMb) : has_cmd ? kPartValid : 0u;
+        e.bit = bit0 + (at_mb ? mb.bit_off : sg.bit_off);
+        e.pos = (uint64_t)jb.abs_base + p;
+        e.mb_bit = bit0 + mb.bit_off;
+        e.mb_pos = (uint64_t)jb.abs_base + mb.start;
+        for (int q = 0; q < 4; q++) e.ring[q] = ring[q];
+        for (int c = 0; c < 3; c++) {
+          e.blen[c] = at_mb ? 0 : blen[c];
+          e.type[c] = (uint8_t)(at_mb ? 0 : type[c]);
+          e.prev[c] = (uint8_t)(at_mb ? 0 : prev[c]);
+        }
+        const uint32_t p12 = s_p12[k];
+        e.p1 = (uint8_t)(p12 & 0xFF);
+        e.p2 = (uint8_t)(p12 >> 8);
         const uint8_t *eb = reinterpret_cast<const uint8_t *>(&e);
         uint8_t *dst = ent + (size_t)((s - jb.seg_base) / every) * sizeof(PartEntry);
         for (int i = 0; i < (int)sizeof(e); i++) dst[i] = eb[i];
       }
       // the segment's distance pushes and block-split units, in stream order
-      const PushSum &ps = push[s];
+      const PushSum &ps = s_push[k];
       if (ps.n >= 4) {
         for (int q = 0; q < 4; q++) ring[q] = ps.d[q];
       } else if (ps.n) {
@@ -186,7 +215,7 @@ __global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, con
         for (int q = 0; q < 4; q++) ring[q] = r[q];
       }
       for (int u = 0; u < kSubPerSeg; u++) {
-        const Unit &un = units[(size_t)s * kSubPerSeg + u];
+        const Unit &un = s_unit[k * kSubPerSeg + u];
         for (int c = 0; c < 3; c++) {
           if (un.sw_count[c]) {
             prev[c] = type[c];
@@ -203,7 +232,7 @@ __global__ void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, con
 void launch_part_index(hipStream_t st, const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, int nsegs,
                        const Cmd *cmds, const Unit *units, PushSum *push, uint8_t *out) {
   hipLaunchKernelGGL(part_push_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, cmds, push);
-  hipLaunchKernelGGL(part_index_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, units, push, out);
+  hipLaunchKernelGGL(part_index_kernel, dim3(njobs), dim3(kPiChunk), 0, st, jobs, njobs, mbs, segs, units, push, out);
 }
 
 size_t part_push_bytes() { return sizeof(PushSum); }
