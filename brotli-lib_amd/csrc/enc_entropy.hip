@@ -220,15 +220,16 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
 // histograms per block type, distance-code histograms per (block type, distance context),
 // accumulated in LDS (literals one block type at a time) and added to the metablock's with
 // one global atomic per non-zero bin (the histogram pass of storeMetaBlock, metablock.ts:580-640).
-__global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
+template <int NT>
+__global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Unit *units, uint32_t *hl,
                                                        uint32_t *hc, uint32_t *hd) {
-  typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
+  typedef hipcub::BlockScan<uint32_t, NT> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
   __shared__ uint8_t ut[kSubPerSeg][3];
-  __shared__ ItemMap<kBlock> map;
-  __shared__ uint32_t sh_pos[kBlock], sh_ins[kBlock];
+  __shared__ ItemMap<NT> map;
+  __shared__ uint32_t sh_pos[NT], sh_ins[NT];
   uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
@@ -236,16 +237,16 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
   const Mb &mb = mbs[sg.mb];
   const int t = threadIdx.x;
   __shared__ uint8_t lut[512];   // the context-mode table, per-literal lookups from LDS
-  for (int i = t; i < 512; i += kBlock) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
+  for (int i = t; i < 512; i += NT) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
-  for (int i = t; i < kMaxBT * 704; i += kBlock) sh_c[i] = 0;
-  for (int i = t; i < kMaxBT * kDistCtx * 128; i += kBlock) sh_d[i] = 0;
+  for (int i = t; i < kMaxBT * 704; i += NT) sh_c[i] = 0;
+  for (int i = t; i < kMaxBT * kDistCtx * 128; i += NT) sh_d[i] = 0;
   __syncthreads();
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
-  for (uint32_t q = t; q < n; q += kBlock) {
+  for (uint32_t q = t; q < n; q += NT) {
     const Cmd k = c[q];
     const uint32_t u = unit_of(sg, cp[q]);
     atomicAdd(&sh_c[ut[u][1] * 704 + k.cmd_prefix], 1u);
@@ -253,19 +254,19 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
   }
   const uint32_t m = sg.mb;
   __syncthreads();
-  for (int i = t; i < kMaxBT * 704; i += kBlock)
+  for (int i = t; i < kMaxBT * 704; i += NT)
     if (sh_c[i]) atomicAdd(&hc[(size_t)m * kMaxBT * 704 + i], sh_c[i]);
-  for (int i = t; i < kMaxBT * kDistCtx * 128; i += kBlock)
+  for (int i = t; i < kMaxBT * kDistCtx * 128; i += NT)
     if (sh_d[i]) atomicAdd(&hd[(size_t)m * kMaxBT * kDistCtx * 128 + i], sh_d[i]);
   __syncthreads();
   uint32_t present = 0;   // literal block types used by this segment
   for (int u = 0; u < kSubPerSeg; u++) present |= 1u << ut[u][0];
   for (int ty = 0; ty < kMaxBT; ty++) {
     if (!(present >> ty & 1)) continue;
-    for (int i = t; i < kLitCtx * 256; i += kBlock) sh_l[i] = 0;
+    for (int i = t; i < kLitCtx * 256; i += NT) sh_l[i] = 0;
     __syncthreads();
-    for (uint32_t base = 0; base < n; base += kBlock) {   // the literals of this type, spread over the lanes
-      const uint32_t q = base + t, nb = min((uint32_t)kBlock, n - base);
+    for (uint32_t base = 0; base < n; base += NT) {   // the literals of this type, spread over the lanes
+      const uint32_t q = base + t, nb = min((uint32_t)NT, n - base);
       uint32_t cnt = 0;
       if (q < n && c[q].ins) {   // the command's literals that lie in units of this type
         const uint32_t pos = cp[q], ins = c[q].ins;
@@ -284,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
       map.off[t] = off;
       if (t == 0) map.off[nb] = nlits;
       __syncthreads();
-      for (uint32_t i = t; i < nlits; i += kBlock) {
+      for (uint32_t i = t; i < nlits; i += NT) {
         const uint32_t j = map.find(i, nb);
         // the (i - off)-th of command j's literals in type-ty units (an insert spans few units)
         const uint32_t pos = sh_pos[j], ins = sh_ins[j];
@@ -306,7 +307,7 @@ __global__ __launch_bounds__(kBlock) void histo_kernel(const Job *jobs, const Se
       __syncthreads();
     }
     uint32_t *dst = hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256;
-    for (int i = t; i < kLitCtx * 256; i += kBlock)
+    for (int i = t; i < kLitCtx * 256; i += NT)
       if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
     __syncthreads();
   }
@@ -1494,7 +1495,15 @@ void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *unit
 }
 void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
-  hipLaunchKernelGGL(histo_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, units, hl, hc, hd);
+  // 1024 threads: the 64 KiB literal histogram allows two blocks per CU, so wider blocks are
+  // what hides the per-literal gathers (C3 type_histo 9.6 -> 5.3 ms; MIB_HISTO_NT overrides)
+  static const int nt = getenv("MIB_HISTO_NT") ? atoi(getenv("MIB_HISTO_NT")) : 1024;
+  if (nt >= 1024)
+    hipLaunchKernelGGL(histo_kernel<1024>, dim3(nsegs), dim3(1024), 0, st, jobs, segs, mbs, cmds, cmd_pos, units, hl, hc, hd);
+  else if (nt >= 512)
+    hipLaunchKernelGGL(histo_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, units, hl, hc, hd);
+  else
+    hipLaunchKernelGGL(histo_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, units, hl, hc, hd);
 }
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds) {
   hipLaunchKernelGGL(dist_ring_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, cmds);
