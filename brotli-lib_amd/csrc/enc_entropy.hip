@@ -85,22 +85,23 @@ __global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs) {
 // (block scan), and per block-split unit (8 KiB of the segment's commands) its order-0
 // literal, command and distance-code histograms, symbol counts and first commands -- the
 // symbol streams splitBlock works on (block-splitter.ts:394-464).
-__global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const RawCmd *raw,
+template <int NT>
+__global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const RawCmd *raw,
                                                        Cmd *cmds, uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
-  typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
+  typedef hipcub::BlockScan<uint32_t, NT> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t sh_h[kSubPerSeg * kSubHist];
   __shared__ uint32_t sh_n[kSubPerSeg][3], sh_first[kSubPerSeg][3];
   __shared__ uint32_t sh_run;
-  __shared__ ItemMap<kBlock> map;
-  __shared__ uint32_t sh_pos[kBlock];
-  __shared__ uint32_t sh_push[kBlock];   // the batch's pushed distances, by rank
+  __shared__ ItemMap<NT> map;
+  __shared__ uint32_t sh_pos[NT];
+  __shared__ uint32_t sh_push[NT];   // the batch's pushed distances, by rank
   __shared__ uint32_t sh_ring[4];        // the ring before the batch, most recent first
   const Seg sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
-  for (int i = t; i < kSubPerSeg * kSubHist; i += kBlock) sh_h[i] = 0;
+  for (int i = t; i < kSubPerSeg * kSubHist; i += NT) sh_h[i] = 0;
   if (t < kSubPerSeg * 3) {
     sh_n[t / 3][t % 3] = 0;
     sh_first[t / 3][t % 3] = ~0u;
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
   Cmd *out = cmds + sg.cmd_off;
   uint32_t *outp = cmd_pos + sg.cmd_off;
   const uint32_t nraw = sg.ncmd, n = nraw + (sg.extra_ins ? 1 : 0);
-  for (uint32_t base = 0; base < n; base += kBlock) {
+  for (uint32_t base = 0; base < n; base += NT) {
     const uint32_t q = base + t;
     uint32_t ins = 0, len = 0, d = 0, prevd = 0;
     if (q < nraw) {
@@ -187,11 +188,11 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
     sh_pos[t] = pos;
     uint32_t loff, nlits;
     Scan(scan_tmp).ExclusiveSum(q < n ? ins : 0u, loff, nlits);
-    const uint32_t nb = min((uint32_t)kBlock, n - base);
+    const uint32_t nb = min((uint32_t)NT, n - base);
     map.off[t] = loff;
     if (t == 0) map.off[nb] = nlits;
     __syncthreads();
-    for (uint32_t i = t; i < nlits; i += kBlock) {
+    for (uint32_t i = t; i < nlits; i += NT) {
       const uint32_t j = map.find(i, nb);
       const uint32_t lp = sh_pos[j] + i - map.off[j];
       atomicAdd(&sh_h[unit_of(sg, lp) * kSubHist + jb.data[lp]], 1u);
@@ -200,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void codes_kernel(const Job *jobs, const Se
   }
   const uint32_t u0 = blockIdx.x * kSubPerSeg;
   uint32_t *gh = unit_h + (size_t)u0 * kSubHist;
-  for (int i = t; i < kSubPerSeg * kSubHist; i += kBlock) gh[i] = sh_h[i];
+  for (int i = t; i < kSubPerSeg * kSubHist; i += NT) gh[i] = sh_h[i];
   if (t < kSubPerSeg) {
     Unit un;
     for (int c = 0; c < 3; c++) {
@@ -1395,15 +1396,16 @@ __global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hd
 // ---------------------------------------------------------------- sizes: block per segment
 // The segment's bit size: the sum of item_bits over its commands' items (the same
 // load-balanced expansion as emit_kernel, so literal-heavy segments use every lane).
-__global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
+template <int NT>
+__global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
-  typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
-  typedef hipcub::BlockReduce<unsigned long long, kBlock> Reduce;
+  typedef hipcub::BlockScan<uint32_t, NT> Scan;
+  typedef hipcub::BlockReduce<unsigned long long, NT> Reduce;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ typename Reduce::TempStorage red_tmp;
-  __shared__ ItemMap<kBlock> map;
-  __shared__ Cmd sh_c[kBlock];
-  __shared__ uint32_t sh_p[kBlock];
+  __shared__ ItemMap<NT> map;
+  __shared__ Cmd sh_c[NT];
+  __shared__ uint32_t sh_p[NT];
   __shared__ Unit sh_u[kSubPerSeg];
   Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
@@ -1412,15 +1414,15 @@ __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *seg
   const Mb &mb = mbs[sg.mb];
   const Codes &cd = codes[sg.mb];
   __shared__ uint8_t sh_lut[512], sh_cmap[kLitSlots];   // per-literal lookups from LDS
-  for (int i = t; i < 512; i += kBlock) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
-  for (int i = t; i < kLitSlots; i += kBlock) sh_cmap[i] = mb.lit_cmap[i];
+  for (int i = t; i < 512; i += NT) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
+  for (int i = t; i < kLitSlots; i += NT) sh_cmap[i] = mb.lit_cmap[i];
   __syncthreads();
   const uint8_t *lut = sh_lut;
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
   if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
   unsigned long long bits = 0;
-  for (uint32_t base = 0; base < n; base += kBlock) {
-    const uint32_t nb = min((uint32_t)kBlock, n - base);
+  for (uint32_t base = 0; base < n; base += NT) {
+    const uint32_t nb = min((uint32_t)NT, n - base);
     uint32_t cnt = 0;
     if ((uint32_t)t < nb) {
       sh_c[t] = cmds[sg.cmd_off + base + t];
@@ -1432,7 +1434,7 @@ __global__ __launch_bounds__(kBlock) void sizes_kernel(const Job *jobs, Seg *seg
     map.off[t] = off;
     if (t == 0) map.off[nb] = nitems;
     __syncthreads();
-    for (uint32_t i = t; i < nitems; i += kBlock) {
+    for (uint32_t i = t; i < nitems; i += NT) {
       const uint32_t j = map.find(i, nb);
       const uint32_t p = sh_p[j];
       bits += item_bits(cd, mb, sh_cmap, lut, jb, sh_c[j], p, sg, sh_u, base + j, i - map.off[j]);
@@ -1485,7 +1487,12 @@ void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs
 }
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
-  hipLaunchKernelGGL(codes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
+  // 512 threads: the 35 KiB unit histograms allow four blocks (32 waves) per CU (MIB_CODES_NT overrides)
+  static const int nt = getenv("MIB_CODES_NT") ? atoi(getenv("MIB_CODES_NT")) : 512;
+  if (nt >= 512)
+    hipLaunchKernelGGL(codes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
+  else
+    hipLaunchKernelGGL(codes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
 }
 void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes) {
   if (nmbs * 3 <= 256)
@@ -1521,7 +1528,11 @@ void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const ui
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
-  hipLaunchKernelGGL(sizes_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
+  static const int nt = getenv("MIB_SIZES_NT") ? atoi(getenv("MIB_SIZES_NT")) : 512;   // (MIB_SIZES_NT overrides)
+  if (nt >= 512)
+    hipLaunchKernelGGL(sizes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
+  else
+    hipLaunchKernelGGL(sizes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
 }
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
   hipLaunchKernelGGL(offsets_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, out);
