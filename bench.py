@@ -53,9 +53,9 @@ WORKLOADS = {
     'c4': (1024, MIB, 0, 2000, 'enwik'),
     'c3': (1024, 256 * 1024, 2, 1000, 'glyf'),
     'c2': (1, 64 * MIB, 0, 2, 'enwik'),
-    # C5's per-GPU stream, shortened (the single-stream decode is the slow half): BrotliEncoder
-    # .update() in 1 MiB chunks, q9 lgwin 24, then one decode of the whole stream
-    'c5': (1, 64 * MIB, 1, 5000, 'enwik'),
+    # C5's per-GPU stream: 1 GiB through BrotliEncoder.update() in 1 MiB chunks, q9 lgwin 24,
+    # custom dictionary, then one decode of the whole stream
+    'c5': (1, 1024 * MIB, 1, 5000, 'enwik'),
 }
 
 
@@ -183,20 +183,23 @@ def cpu_baseline(sample, gpu_sizes, args, mode, what):
         'node_native_MBps_1thread': round(nn_bytes / 1e6 / (nat['ns'] * 1e-9), 3) if nat else None}
 
 
-def load_traffic(kernel):
-    """HBM bytes per launch of `kernel` from profiles/pmc_summary.json (collect_pmc.py)."""
+def load_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` in `workload` from profiles/pmc_summary.json (the
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes, scripts/collect_pmc.py), or None."""
     p = os.path.join(ROOT, 'profiles', 'pmc_summary.json')
     try:
         with open(p) as f:
             d = json.load(f)
-        return int(d['kernels'][kernel]['hbm_bytes_per_launch'])
+        k = d['workloads'][workload]['kernels'] if 'workloads' in d else d['kernels']
+        return int(k[kernel]['hbm_bytes_per_launch'])
     except Exception:
         return None
 
 
 def run_stream(args, rank, world, local):
-    """C5 leg: host chunks through the streaming encoder (PCIe inside: this is the API the
-    reference exposes), then the HIP decoder on the whole stream; both timed."""
+    """C5 leg: one stream per GPU through the streaming encoder in 1 MiB host chunks with the
+    C5 custom dictionary (PCIe inside: update() takes host bytes, the API the reference
+    exposes), then brotliDecode of the whole stream with the dictionary; both timed."""
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
@@ -204,11 +207,13 @@ def run_stream(args, rank, world, local):
     if world > 1:
         dist.init_process_group('nccl', device_id=dev)
     import brotli_amd
+    from brotli_amd import datagen
     size = args.size if args.size > 0 else WORKLOADS['c5'][1]
     q = 9 if args.quality == 11 else args.quality
     lg = 24 if args.lgwin == 22 else args.lgwin
-    data = bytes(datagen_device(size, 5000 + rank, dev).cpu().numpy().tobytes())
-    opts = {'quality': q, 'lgwin': lg, 'mode': 1}
+    data = datagen.c5_stream(size, 5000 + rank, dev)
+    cdict = datagen.c5_dictionary()
+    opts = {'quality': q, 'lgwin': lg, 'mode': 1, 'customDictionary': cdict}
     step = MIB
 
     def enc():
@@ -218,18 +223,22 @@ def run_stream(args, rank, world, local):
         return b''.join(parts)
     for _ in range(max(1, args.warmup)):
         stream = enc()
-    if brotli_amd.brotliDecode(stream) != data:
+    if brotli_amd.brotliDecode(stream, {'customDictionary': cdict}) != data:
         raise SystemExit('c5 round trip FAILED')
     if world > 1:
         dist.barrier()
+    brotli_amd.default_profiling(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         stream = enc()
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        out = brotli_amd.brotliDecode(stream)
+        out = brotli_amd.brotliDecode(stream, {'customDictionary': cdict})
     t2 = time.perf_counter()
+    times = brotli_amd.default_kernel_times()
+    brotli_amd.default_profiling(False)
     assert out == data
+    del out
     te, td = (t1 - t0) / args.steps, (t2 - t1) / args.steps
     dt = te + td
     if world > 1:
@@ -238,16 +247,45 @@ def run_stream(args, rank, world, local):
         dt, te, td = (float(x) for x in t.tolist())
     if rank == 0:
         mb = world * size / 1e6
+        dom_name, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0])
+        # the dominant kernel: decode launches cover the whole stream, encoder launches one
+        # device chunk each (update() hands the device whole chunks of the stream)
+        launches_per_step = max(1, dom_n // args.steps)
+        launch_bytes = (size + len(stream)) // launches_per_step
+        avg_ms = dom_ms / max(1, dom_n)
+        achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            # the oracle (reference decoder restated) decodes the same stream with the same
+            # dictionary on one host thread (it is one bit-serial stream); the oracle restates
+            # the reference's q10/q11 encoder, not its q9 hash-chain path, so decode only
+            sys.path.insert(0, os.path.join(ROOT, 'tests'))
+            import _oracle
+            c0 = time.perf_counter()
+            got = _oracle.decode(stream, dictionary=cdict)
+            ct = time.perf_counter() - c0
+            ok = got == data
+            del got
+            cpu = {'value': round(size / 1e6 / ct, 3), 'unit': 'MB/s', 'cores': 1, 'kind': 'port',
+                   'sample': 'decode only: the whole %d B C5 stream, oracle decoder with the dictionary, one host '
+                             'thread, %.1f s, %s' % (size, ct, 'bit-exact' if ok else 'MISMATCH')}
         print(json.dumps({
             'metric': 'encode+decode MB/s at q11 lgwin=22', 'value': round(mb / dt, 3), 'unit': 'MB/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt * 1e3, 3),
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
             'config': {'workload': 'C5 per GPU: one %d B enwik-style stream, BrotliEncoder.update() in 1 MiB host '
-                                   'chunks, q%d lgwin%d TEXT, then brotliDecode of the stream (host buffers: PCIe '
-                                   'included)' % (size, q, lg), 'name': 'c5', 'bytes_per_stream': size,
-                       'quality': q, 'lgwin': lg, 'parallelism': 'replicas%d' % world},
+                                   'chunks, q%d lgwin%d TEXT, %d B custom dictionary, then brotliDecode of the stream '
+                                   'with it (host buffers: PCIe included)' % (size, q, lg, len(cdict)),
+                       'name': 'c5', 'bytes_per_stream': size, 'quality': q, 'lgwin': lg,
+                       'custom_dictionary_bytes': len(cdict), 'parallelism': 'replicas%d' % world},
             'encode_MBps': round(mb / te, 3), 'decode_MBps': round(mb / td, 3),
-            'compressed_ratio': round(len(stream) / size, 5), 'roofline': None, 'cpu_baseline': None}), flush=True)
+            'compressed_ratio': round(len(stream) / size, 5),
+            'kernel_ms_per_step': {n: round(v[0] / args.steps, 3) for n, v in sorted(times.items())},
+            'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 3), 'peak': PEAK_HBM_GBS,
+                         'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 6),
+                         'traffic': load_traffic(dom_name, 'c5'),
+                         'algorithmic_bytes_per_launch': launch_bytes, 'avg_launch_ms': round(avg_ms, 3)},
+            'cpu_baseline': cpu}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -480,7 +518,7 @@ def main():
             'kernel_ms_per_step': {n: round(v[0] / args.steps, 3) for n, v in sorted(times.items())},
             'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 3), 'peak': PEAK_HBM_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 6),
-                         'traffic': load_traffic(dom_name) if wl == 'c4' else None,
+                         'traffic': load_traffic(dom_name, wl),
                          'algorithmic_bytes_per_launch': launch_bytes, 'avg_launch_ms': round(avg_ms, 3)},
             'cpu_baseline': cpu,
         }

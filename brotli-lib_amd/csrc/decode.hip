@@ -119,6 +119,7 @@ struct Dec {
   // part mode: [part_start, part_end) of the output, progress publishing, the stream's
   // progress words (part_end = INT_MAX: whole-stream mode)
   int part, part_start, part_end, pub_next, pidx, cover_lo;
+  int pctx;              // part mode: the two output bytes before part_start (p1 | p2 << 8, from the entry)
   uint64_t *prog;
   const int64_t *ppos;   // the stream's part start positions (+ its total at [nparts])
   Lds *l;
@@ -252,6 +253,14 @@ __device__ int jump_to_byte_boundary(DecS &s) {
 constexpr int kPartFail = -120;   // internal: the part cannot vouch for its bytes (stream falls back)
 
 __device__ __forceinline__ int64_t abs_bit(const DecS &s) { return (s.win_base + 2 * (int64_t)s.ho) * 8 - 32 + s.bo; }
+
+// The output byte at position p >= pos - 2 (a literal context byte).  A part never reads the
+// bytes before its start from the output: the previous part may still be writing them; they
+// come from its entry (0 before the stream start, as in the reference's zeroed ring).
+__device__ __forceinline__ int ctx_byte(const DecS &s, int p, int rmask) {
+  if (s.part && p < s.part_start) return p < 0 ? 0 : (s.pctx >> (8 * (s.part_start - 1 - p))) & 0xFF;
+  return s.ring[p & rmask];
+}
 
 // position the bit reader at absolute bit `bit` with a fresh 4 KiB window from there
 __device__ int part_seek(DecS &s, int64_t bit) {
@@ -1091,8 +1100,8 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
         // back from the ring would wait for every outstanding ring store (vmcnt is in order).
         // (part mode: absolute positions -- before the stream start the context bytes are 0;
         // the ring's last bytes would lie past the output buffer)
-        int c1 = (s.part && s.pos < 1) ? 0 : __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 1) & rmask]);
-        int c2b = (s.part && s.pos < 2) ? 0 : __builtin_amdgcn_readfirstlane(s.ring[(s.pos - 2) & rmask]);
+        int c1 = __builtin_amdgcn_readfirstlane(ctx_byte(s, s.pos - 1, rmask));
+        int c2b = __builtin_amdgcn_readfirstlane(ctx_byte(s, s.pos - 2, rmask));
         int dr0, dr1, dr2, dr3, dridx;   // the distance ring (rings[0..3], dist_rb_idx)
         uint32_t acc;
         int bo, ho, pos, j, mbl, insert_len, copy_len, dist_code, distance, cmd_blen, lit_blen, dist_blen, max_dist;
@@ -1564,8 +1573,9 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
               }
               if (j < copy_len) cut = 1;
               if (cut) break;
-              c1 = __builtin_amdgcn_readfirstlane(ring[(pos - 1) & rmask]);
-              c2b = __builtin_amdgcn_readfirstlane(ring[(pos - 2) & rmask]);
+              wave_sync();
+              c1 = __builtin_amdgcn_readfirstlane(ctx_byte(s, pos - 1, rmask));
+              c2b = __builtin_amdgcn_readfirstlane(ctx_byte(s, pos - 2, rmask));
             }
             phase = ST_MAIN_LOOP;
             PMARK(3);
@@ -1643,8 +1653,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   uint32_t pf = win16[ho + 2];
   int cmd_blen = U(s.cmd_blen), lit_blen = U(s.lit_blen), dist_blen = U(s.dist_blen), max_dist = U(s.max_dist);
   int dr0 = U(s.rings[0]), dr1 = U(s.rings[1]), dr2 = U(s.rings[2]), dr3 = U(s.rings[3]), dridx = U(s.dist_rb_idx);
-  int c1 = (kPart && pos < 1) ? 0 : U((int)s.ring[(pos - 1) & rmask]);
-  int c2b = (kPart && pos < 2) ? 0 : U((int)s.ring[(pos - 2) & rmask]);
+  int c1 = U(ctx_byte(s, pos - 1, rmask));
+  int c2b = U(ctx_byte(s, pos - 2, rmask));
   const int cmd_root = U((int)t16[s.cmd_base + s.cmd_tree_idx]);
   const int lit_root = kTrivial ? U((int)t16[s.lit_tree_idx]) : 0;
   // lut1 of the literal context mode, packed: lane l holds entries l, l + 64, l + 128, l + 192
@@ -2177,6 +2187,7 @@ __device__ void dec_init(DecS &s, const DecJob &job, uint8_t *ring, int32_t *tab
   s.pub_next = 0x7FFFFFFF;
   s.pidx = 0;
   s.cover_lo = 0;
+  s.pctx = 0;
   s.prog = nullptr;
   s.ppos = nullptr;
 }
@@ -2286,10 +2297,9 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
   s.rings[0] = (int)e.ring[3]; s.rings[1] = (int)e.ring[2]; s.rings[2] = (int)e.ring[1]; s.rings[3] = (int)e.ring[0];
   s.dist_rb_idx = 3;
   s.max_dist = s.pos < s.max_back ? s.pos : s.max_back;
-  // the literal context: the two bytes before the part (the previous part writes the same)
-  if (lane == 0 && s.pos >= 1) s.ring[s.pos - 1] = e.p1;
-  if (lane == 1 && s.pos >= 2) s.ring[s.pos - 2] = e.p2;
-  wave_sync();
+  // the literal context: the two bytes before the part, from the entry (ctx_byte); the
+  // previous part's output is never written here, and it checks those bytes itself
+  s.pctx = (int)e.p1 | ((int)e.p2 << 8);
   r = decompress(s, dist_extra, dist_offset, ctxmap_table);
   if (last) return (r == 1 && s.pos == (int)job.total) ? 0 : kPartFail;
   if (r != 3) return kPartFail;
@@ -2316,8 +2326,10 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
          s.rings[7] == n.type[1] && s.rings[6] == n.prev[1] && s.cmd_blen == (int)n.blen[1] &&
          s.rings[9] == n.type[2] && s.rings[8] == n.prev[2] && s.dist_blen == (int)n.blen[2];
   }
-  if (ok && s.pos >= 2) {
-    ok = s.ring[s.pos - 1] == n.p1 && s.ring[s.pos - 2] == n.p2;
+  if (ok) {   // the bytes this part wrote (or, for a part under 2 bytes, its own entry's)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int rmask = s.ring_size - 1;
+    ok = ctx_byte(s, s.pos - 1, rmask) == n.p1 && ctx_byte(s, s.pos - 2, rmask) == n.p2;
   }
   return ok ? 0 : kPartFail;
 }

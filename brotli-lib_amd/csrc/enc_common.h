@@ -81,7 +81,20 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint64_t out_off;         // byte offset of its scratch output slice
   uint64_t out_cap;
   uint64_t total_bits;      // written by offsets / stored
+  const uint8_t *cdict;     // custom dictionary (device), or null (see kCDictMark)
+  uint32_t cdict_len;
+  uint32_t cdict_tail4;     // its last four bytes (little endian)
 };
+
+// Custom-dictionary copies (mib_enc_opts.dict; the reference decoder's compound dictionary,
+// engine.ts:142-159,903-1011).  A copy of length L at stream position p with distance
+// d = min(p, max backward distance) + L is read by the decoder from dictionary offset
+// dict_len - L: the dictionary's last L bytes (the reference decoder rejects any other
+// compound copy, engine.ts:992, so these are the only ones ever emitted).  A match record
+// names one by the distance kCDictMark (no window distance is that large) and its exact
+// length; the parse turns it into d.  Downstream it is an ordinary copy: it pushes on the
+// distance ring and may be repeated by a short code, as in the decoder.
+constexpr uint32_t kCDictMark = 0xFFFFFFu;
 
 // Static-dictionary references (RFC 7932 section 8, identity transform):
 // a copy whose distance exceeds the decoder's maximum backward distance names the word of
@@ -420,6 +433,7 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
                       uint32_t *vals);
 void launch_dict_matches(hipStream_t st, const Job *jobs, int njobs, uint32_t span, const uint32_t *dict_tab,
                          const uint8_t *dict_data, uint32_t *matches);
+void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *matches);
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                          const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
@@ -429,7 +443,7 @@ size_t cost_model_hist_bytes(int njobs);
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,
                        uint32_t *hist, CostModel *model);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
-               const uint32_t *matches, uint64_t *choice);
+               const uint32_t *matches, uint64_t *choice, bool cdict);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,

@@ -342,6 +342,43 @@ __global__ __launch_bounds__(256) void dict_matches_kernel(const Job *jobs, int 
   }
 }
 
+// ---------------------------------------------------------------- custom-dictionary copies
+// (kCDictMark, enc_common.h.)  Thread per stream position q: where the four bytes ending at q
+// equal the dictionary's last four, the common suffix of the input up to q and of the
+// dictionary is measured backwards (within q's parse segment, at most kLongCopy bytes); the
+// copy of that length starting at p = q - L + 1 is offered at p if the window found nothing
+// there.  Several q may offer one p: the longest wins (a compare-and-swap maximum, so the
+// result does not depend on thread order).
+__global__ __launch_bounds__(256) void cdict_matches_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total,
+                                                            uint32_t *matches) {
+  for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < total; g += gridDim.x * 256) {
+    const Job &jb = jobs[pos_job[g >> kSegBits]];
+    if (!jb.cdict) continue;
+    const uint32_t q = g - jb.pos_base;
+    if (q < 3 || q >= jb.n) continue;
+    const uint8_t *d = jb.data;
+    if (load_u32(d + q - 3) != jb.cdict_tail4) continue;
+    const uint32_t seg0 = (q >> kSegBits) << kSegBits;
+    const uint32_t cap = min(min((uint32_t)kLongCopy, jb.cdict_len), q - seg0 + 1);
+    const uint8_t *t = jb.cdict + jb.cdict_len;   // one past the dictionary's last byte
+    uint32_t L = 4;
+    while (L < cap && d[q - L] == t[-1 - (int)L]) L++;
+    if (L > cap) continue;   // (a dictionary or segment of fewer than four bytes)
+    uint32_t *rec = matches + (uint64_t)(g - L + 1) * kMatchRec;
+    const uint32_t mine = pack_match(kCDictMark, L);
+    uint32_t old = rec[0];
+    while ((old == 0u || match_dist(old) == kCDictMark) && old < mine) {
+      const uint32_t prev = atomicCAS(rec, old, mine);
+      if (prev == old) break;
+      old = prev;
+    }
+  }
+}
+void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *matches) {
+  const unsigned grid = (unsigned)std::min<uint64_t>(16384, (total + 255) / 256);
+  hipLaunchKernelGGL(cdict_matches_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, matches);
+}
+
 void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
                       uint32_t *vals) {
   const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total / 4 + 255) / 256);

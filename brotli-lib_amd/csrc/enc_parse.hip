@@ -120,8 +120,9 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
 }
 
 // KM: the second iteration (prices from the stream's CostModel; a separate build, so
-// profiles tell the two passes apart)
-template <int KS, bool KM>
+// profiles tell the two passes apart).  KD: some stream has a custom dictionary (records with
+// kCDictMark; a separate build, so the common case pays nothing for it)
+template <int KS, bool KM, bool KD>
 __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
@@ -247,7 +248,11 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         uint32_t extra;
         uint32_t md = match_dist(cur.m[q]), d = md;
         uint32_t ln = min(match_length(cur.m[q]), b - p);
-        if (words && is_dict(md)) {   // a dictionary word (the only entry): its distance at p, its exact length
+        if (KD && md == kCDictMark) {   // a custom-dictionary copy (the only entry): its exact length
+          word = ln == match_length(cur.m[q]) ? 1u : 0u;   // cut by the segment end: unusable
+          ln = word ? ln : 0u;
+          d = min(abs0 + p, maxback) + ln;
+        } else if (words && is_dict(md)) {   // a dictionary word (the only entry): its distance at p, its exact length
           d = min(abs0 + p, maxback) + 1 + (md & 0x7FF);
           md = d | kDictFlag;
           word = ln == match_length(cur.m[q]) ? 1u : 0u;   // cut by the segment end: unusable
@@ -394,6 +399,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
         nd = match_dist(x);
+        if (KD && nd == kCDictMark) nd = min(abs0 + i, maxback) + l;   // (d of the copy at i: see kCDictMark)
         const float alt = __builtin_fmaf((float)(x >> 24), 0.25f, pn);   // (exact: code / 4 needs no rounding)
         // a match at the path's last distance is priced with short code 0
         const uint32_t use_last = 0u - (uint32_t)(nd == ld);   // a select, not a branch
@@ -639,20 +645,26 @@ static int dp_workgroups(int nsegs) {
   const int spw = kDpWaves * dp_ks(nsegs);
   return (nsegs + spw - 1) / spw;
 }
-void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
-               const uint32_t *matches, uint64_t *choice) {
+template <bool KD>
+static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
+                        const CostModel *model, const uint32_t *matches, uint64_t *choice) {
   const dim3 g(dp_workgroups(nsegs)), b(64 * kDpWaves);
   if (dp_ks(nsegs) == 1) {
     if (model)
-      hipLaunchKernelGGL((dp_kernel<1, true>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
     else
-      hipLaunchKernelGGL((dp_kernel<1, false>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<1, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
   } else {
     if (model)
-      hipLaunchKernelGGL((dp_kernel<2, true>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<2, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
     else
-      hipLaunchKernelGGL((dp_kernel<2, false>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<2, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
   }
+}
+void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
+               const uint32_t *matches, uint64_t *choice, bool cdict) {
+  if (cdict) launch_dp_t<true>(st, jobs, segs, nsegs, lit_h, model, matches, choice);
+  else launch_dp_t<false>(st, jobs, segs, nsegs, lit_h, model, matches, choice);
 }
 size_t cost_model_hist_bytes(int njobs) { return (size_t)njobs * kHistLen * 4; }
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,

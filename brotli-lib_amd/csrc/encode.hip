@@ -129,6 +129,8 @@ struct StreamDesc {
   uint32_t *hist_tab;    // streaming: the encoder's bucket table (null: none)
   uint64_t out_base;     // streaming: stream bytes emitted before this chunk
   bool streaming;        // a BrotliEncoder chunk (part index whenever it has segments to split)
+  const uint8_t *cdict;  // custom dictionary (device), or null
+  uint32_t cdict_len, cdict_tail4;
 };
 
 // Streams that get a part index (parts.h): one-shot streams of at least kPartMinStream bytes
@@ -268,7 +270,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   std::vector<Mb> mbs;
   std::vector<uint32_t> seg_job;   // per 64 KiB of global positions: its stream
   uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0;
-  bool any_hist = false, any_parts = false, any_dict = false;
+  bool any_hist = false, any_parts = false, any_dict = false, any_cdict = false;
   for (size_t j = 0; j < k; j++) {
     Job &jb = jobs[j];
     memset(&jb, 0, sizeof(jb));
@@ -289,6 +291,15 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     if (jb.hist_tab) any_hist = true;
     jb.out_base = sd[j].out_base;
     jb.parts = (!jb.uncompressed && wants_parts(sd[j])) ? 1 : 0;
+    // custom dictionary: its tail copies (kCDictMark records; beside the static words: a word
+    // record is kDictFlag | index, and a tail copy's real distance stays below 2^23 wherever
+    // words are used)
+    if (!jb.uncompressed && sd[j].cdict) {
+      jb.cdict = sd[j].cdict;
+      jb.cdict_len = sd[j].cdict_len;
+      jb.cdict_tail4 = sd[j].cdict_tail4;
+      any_cdict = true;
+    }
     jb.dict = (!jb.uncompressed && !sd[j].streaming && !sd[j].hist_tab && prm.quality >= 10 && prm.lgwin <= 22 &&
                dict_enabled()) ? 1 : 0;
     jb.dict_span = dict_span();
@@ -441,6 +452,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     if (any_dict && !dd) return MIB_E_OUT_OF_MEMORY;
     launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, any_hist, any_parts, matches);
     if (dd) launch_dict_matches(st, d_jobs, (int)k, dict_span(), dd->tab, dd->data, matches);
+    if (any_cdict) launch_cdict_matches(st, d_jobs, d_seg_job, total, matches);
     if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
     tm.stop();
     tm.start("lit_histo");
@@ -448,7 +460,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.stop();
     tm.start(two_pass ? "dp_sample" : "dp_parse");
     Seg *s1 = sampled ? d_sample : d_segs;
-    launch_dp(st, d_jobs, s1, nsegs, lit_h, nullptr, matches, choice);
+    launch_dp(st, d_jobs, s1, nsegs, lit_h, nullptr, matches, choice, any_cdict);
     tm.stop();
     tm.start("backtrack");
     launch_backtrack(st, d_jobs, s1, nsegs, choice, raw);
@@ -458,7 +470,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
       launch_cost_model(st, d_jobs, (int)k, s1, nsegs, raw, model_h, model);
       tm.stop();
       tm.start("dp_parse");
-      launch_dp(st, d_jobs, d_segs, nsegs, lit_h, model, matches, choice);
+      launch_dp(st, d_jobs, d_segs, nsegs, lit_h, model, matches, choice, any_cdict);
       tm.stop();
       tm.start("backtrack");
       launch_backtrack(st, d_jobs, d_segs, nsegs, choice, raw);
@@ -580,6 +592,9 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
   d.hist_tab = nullptr;
   d.out_base = 0;
   d.streaming = !one_shot;
+  d.cdict = nullptr;
+  d.cdict_len = 0;
+  d.cdict_tail4 = 0;
   if (!one_shot) {
     d.hdr_lgwin = (uint32_t)prm.lgwin;
   } else if (n == 0) {
@@ -596,6 +611,32 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
     d.hdr_lgwin = (uint32_t)prm.lgwin;
   }
 }
+
+// A custom dictionary (mib_enc_opts.dict) on the device.  Fewer than four bytes cannot hold
+// a copy the encoder would emit (kCDictMark): no upload, no dictionary copies.
+struct DevDict {
+  uint8_t *d = nullptr;
+  uint32_t n = 0, tail4 = 0;
+  int upload(const uint8_t *h, uint64_t len, hipStream_t st) {
+    if (!h || len < 4) return 0;
+    if (len >= (1ull << 31)) return MIB_E_INVALID_ARG;
+    if (hipMalloc(&d, len + 64) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+    CK(hipMemcpyAsync(d, h, len, hipMemcpyHostToDevice, st));
+    n = (uint32_t)len;
+    tail4 = (uint32_t)h[len - 4] | ((uint32_t)h[len - 3] << 8) | ((uint32_t)h[len - 2] << 16) | ((uint32_t)h[len - 1] << 24);
+    return 0;
+  }
+  void attach(StreamDesc &sd) const {
+    sd.cdict = d;
+    sd.cdict_len = n;
+    sd.cdict_tail4 = tail4;
+  }
+  void release() {
+    if (d) hipFree(d);
+    d = nullptr;
+    n = 0;
+  }
+};
 
 uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096 + 16 + sizeof(PartHead) + ((n + kSeg - 1) / kSeg) * sizeof(PartEntry); }
 
@@ -622,6 +663,8 @@ struct mib_encoder {
   uint64_t abs = 0;               // stream bytes encoded so far
   uint64_t obytes = 0;            // compressed bytes returned so far (part index offsets)
   uint32_t *tab = nullptr;
+  std::vector<uint8_t> dict;      // customDictionary (the encoder's own copy) and its device copy
+  DevDict ddict;
 };
 extern "C" {
 
@@ -639,12 +682,22 @@ int mib_ctx_encode(mib_ctx *c, const mib_enc_opts *o, const uint8_t *d_in, const
   hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)mib_ctx_stream_of(c);
   mib_ctx_clear_times(c);
   Params prm = make_params(o);
+  DevDict dd;
+  int rc = o ? dd.upload(o->dict, o->dict_len, st) : 0;
+  if (rc) return rc;
   std::vector<StreamDesc> sd(k);
   for (size_t i = 0; i < k; i++) {
-    if (in_offsets[i + 1] < in_offsets[i] || in_offsets[i + 1] - in_offsets[i] >= (1ull << 31)) return MIB_E_INVALID_ARG;
+    if (in_offsets[i + 1] < in_offsets[i] || in_offsets[i + 1] - in_offsets[i] >= (1ull << 31)) {
+      dd.release();
+      return MIB_E_INVALID_ARG;
+    }
     fill_desc(sd[i], d_in + in_offsets[i], in_offsets[i + 1] - in_offsets[i], prm, true);
+    dd.attach(sd[i]);
   }
-  return encode_streams(c, o, sd.data(), k, d_out, out_cap, out_offsets, nullptr, st);
+  rc = encode_streams(c, o, sd.data(), k, d_out, out_cap, out_offsets, nullptr, st);
+  hipStreamSynchronize(st);
+  dd.release();
+  return rc;
 }
 
 // host buffers -> device -> encode -> host
@@ -675,10 +728,20 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
   hipMemsetAsync(d_in, 0, ioff[k] + 64, st);
   for (size_t i = 0; i < k; i++)
     if (in[i].size) hipMemcpyAsync(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice, st);
+  DevDict dd;
+  int rc = o ? dd.upload(o->dict, o->dict_len, st) : 0;
+  if (rc) {
+    hipFree(d_out);
+    hipFree(d_in);
+    return rc;
+  }
   std::vector<StreamDesc> sd(k);
-  for (size_t i = 0; i < k; i++) fill_desc(sd[i], d_in + ioff[i], in[i].size, prm, true);
+  for (size_t i = 0; i < k; i++) {
+    fill_desc(sd[i], d_in + ioff[i], in[i].size, prm, true);
+    dd.attach(sd[i]);
+  }
   std::vector<uint64_t> ooff(k + 1, 0);
-  int rc = encode_streams(c, o, sd.data(), k, d_out, cap, ooff.data(), nullptr, st);
+  rc = encode_streams(c, o, sd.data(), k, d_out, cap, ooff.data(), nullptr, st);
   if (rc == 0) {
     std::vector<uint8_t> host(ooff[k]);
     if (ooff[k] && hipMemcpy(host.data(), d_out, ooff[k], hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
@@ -690,6 +753,8 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
       if (status) status[i] = 0;
     }
   }
+  hipStreamSynchronize(st);
+  dd.release();
   hipFree(d_out);
   hipFree(d_in);
   return rc;
@@ -734,6 +799,10 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
       if (hipMalloc(&e->tab, sizeof(uint32_t) * kHistWays << kHashBits) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
       CK(hipMemsetAsync(e->tab, 0xFF, sizeof(uint32_t) * kHistWays << kHashBits, st));
     }
+    if (!e->ddict.d && e->dict.size() >= 4) {
+      const int r = e->ddict.upload(e->dict.data(), e->dict.size(), st);
+      if (r) return r;
+    }
     e->device = dev;
     cap += out_bound(ns[i]);
   }
@@ -754,6 +823,7 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
     sd[i].abs_base = (uint32_t)e->abs;
     sd[i].hist_tab = e->tab;
     sd[i].out_base = e->obytes;
+    e->ddict.attach(sd[i]);
   }
   std::vector<uint64_t> ooff(k + 1, 0);
   std::vector<int32_t> dcs(4 * std::max<size_t>(k, 1));
@@ -812,9 +882,13 @@ int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_bu
 // distance ring, the literal context and the 2^lgwin window of history carry over (the
 // reference's ring, encode.ts:312-374, without Bug D's overwrite).
 mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
+  if (o && o->dict && o->dict_len >= (1ull << 31)) return nullptr;
   mib_encoder *e = new mib_encoder();
   if (o) e->opts = *o;
   else mib_enc_opts_default(&e->opts);
+  if (o && o->dict && o->dict_len) e->dict.assign(o->dict, o->dict + o->dict_len);
+  e->opts.dict = nullptr;   // (the caller's buffer is not kept)
+  e->opts.dict_len = 0;
   Params prm = make_params(&e->opts);
   int lgblock;
   if (prm.quality == 0 || prm.quality == 1) lgblock = prm.lgwin;
@@ -917,6 +991,7 @@ void mib_encoder_free(mib_encoder *e) {
     for (int b = 0; b < 2; b++)
       if (e->buf[b]) hipFree(e->buf[b]);
     if (e->tab) hipFree(e->tab);
+    e->ddict.release();
   }
   delete e;
 }

@@ -142,8 +142,9 @@ struct HdrBits {
 
 // The index block at byte `at` (with the stream's window bits first when at == 0).
 // fetch(offset, length, dst) copies stream bytes; false past the end.
+// *end: the byte after the block's payload (where the decoder reads the next header).
 template <class Fetch>
-bool read_part_index(Fetch &fetch, uint64_t at, PartPlan &plan, uint64_t *next) {
+bool read_part_index(Fetch &fetch, uint64_t at, PartPlan &plan, uint64_t *next, uint64_t *end) {
   HdrBits<Fetch> r{fetch, at * 8};
   if (at == 0) {   // decodeWindowBits (engine.ts:91-124)
     int lg;
@@ -176,15 +177,20 @@ bool read_part_index(Fetch &fetch, uint64_t at, PartPlan &plan, uint64_t *next) 
     if (x.flags & mib::kPartValid) plan.ent.push_back(x);
   plan.total = (int64_t)h.total;
   *next = h.next_byte;
+  *end = pay + len;
   return true;
 }
 
 // The whole chain of a stream of n bytes; false if it has none or it does not hold together.
+// Every part proves it ended exactly at the next entry's state, so the chain of parts is the
+// serial decode once its FIRST entry is: that entry must be the metablock header the
+// reference decoder reads right after skipping the first index block (its payload is opaque
+// to every decoder, so an entry pointing into it -- or anywhere else -- is not trusted).
 template <class Fetch>
 bool plan_parts(Fetch &fetch, uint64_t n, PartPlan &plan) {
-  uint64_t at = 0, next = 0;
+  uint64_t at = 0, next = 0, end = 0, first_end = 0;
   for (int guard = 0; guard < (1 << 16); guard++) {
-    if (!read_part_index(fetch, at, plan, &next)) {
+    if (!read_part_index(fetch, at, plan, &next, &end)) {
       if (at == 0) return false;
       // BrotliEncoder.finish() with nothing pending adds only the final empty metablock
       // (ISLAST, ISLASTEMPTY: one byte 0x03): the chain is complete
@@ -192,6 +198,7 @@ bool plan_parts(Fetch &fetch, uint64_t n, PartPlan &plan) {
       if (n - at == 1 && fetch(at, 1, &b) && b == 0x03) next = 0;
       break;
     }
+    if (at == 0) first_end = end;
     if (next == 0) break;
     if (next <= at || next >= n) return false;
     at = next;
@@ -199,6 +206,7 @@ bool plan_parts(Fetch &fetch, uint64_t n, PartPlan &plan) {
   if (next != 0) return false;   // the stream's total is only known from the final chunk's head
   if (plan.ent.size() < 2 || plan.total <= 0 || plan.total >= (1ll << 30)) return false;
   if (plan.ent[0].pos != 0 || !(plan.ent[0].flags & mib::kPartAtMb)) return false;
+  if (plan.ent[0].bit != 8 * first_end || plan.ent[0].mb_bit != plan.ent[0].bit || plan.ent[0].mb_pos != 0) return false;
   for (size_t i = 0; i < plan.ent.size(); i++) {
     const mib::PartEntry &x = plan.ent[i];
     if (x.bit >= 8 * n || x.mb_bit > x.bit || x.mb_pos > x.pos || x.pos >= (uint64_t)plan.total) return false;
@@ -237,7 +245,7 @@ struct DeviceFetch {   // stream bytes on the device (small reads: index heads a
   uint64_t n;
   hipStream_t st;
   uint64_t cache_off = ~0ull;
-  uint8_t cache[64];
+  uint8_t cache[64] = {};
   bool operator()(uint64_t off, uint64_t len, uint8_t *dst) {
     if (off > n || len > n - off) return false;
     if (len == 1) {   // header bits: one cached 64-byte line at a time
@@ -340,6 +348,8 @@ void mib_enc_opts_default(mib_enc_opts *o) {
   o->lgwin = 22;
   o->mode = MIB_MODE_GENERIC;
   o->size_hint = 0;
+  o->dict = nullptr;
+  o->dict_len = 0;
 }
 
 int mib_init(int device) {
@@ -507,6 +517,8 @@ struct PartStream {
   uint64_t in_len;
   uint8_t *out;
   const PartPlan *plan;
+  const uint8_t *dict;   // customDictionary (device), or null
+  uint64_t dict_len;
 };
 static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vector<int> &ok, hipStream_t stream) {
   size_t nj = 0, ne = 0;
@@ -548,6 +560,8 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
       j.out = p.out;
       j.out_cap = (uint64_t)p.plan->total;
       j.out_size = p.plan->total;
+      j.dict = p.dict;
+      j.dict_len = p.dict_len;
       j.max_ring_log = p.plan->lgwin;
       j.part_entry = d_ent + e0 + i;
       j.next_entry = i + 1 < np ? d_ent + e0 + i + 1 : nullptr;
@@ -645,7 +659,7 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
       part = plan_parts(f, jobs[i].in_len, plans[i]) && (uint64_t)plans[i].total + 64 <= jobs[i].out_cap;
     }
     if (part) {
-      ps.push_back(PartStream{jobs[i].in, jobs[i].in_len, jobs[i].out, &plans[i]});
+      ps.push_back(PartStream{jobs[i].in, jobs[i].in_len, jobs[i].out, &plans[i], nullptr, 0});
       ps_idx.push_back(i);
     } else {
       serial.push_back(jobs[i]);
@@ -711,29 +725,24 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     }
     if (dict_n) hipMemcpy(d_dict, dict, dict_n, hipMemcpyHostToDevice);
   }
-  if (!dict && exact_out < 0) {   // a stream with a part index: part-parallel, checked
+  if (exact_out < 0) {   // a stream with a part index: part-parallel, checked
     PartPlan plan;
     HostFetch f{in, n};
-    if (plan_parts(f, n, plan)) {
+    // (the index is untrusted: a total beyond maxOutputSize, or one the device cannot hold,
+    // just leaves the stream to the serial decoder, which finds out what it really is)
+    if (plan_parts(f, n, plan) && (max_out < 0 || plan.total <= max_out) &&
+        hipMalloc(&d_out, (uint64_t)plan.total + 4096) == hipSuccess) {
       std::vector<PartStream> ps(1);
       std::vector<int> ok;
-      if (hipMalloc(&d_out, (uint64_t)plan.total + 4096) != hipSuccess) {
-        hipFree(d_in);
-        return MIB_E_OUT_OF_MEMORY;
-      }
-      ps[0] = PartStream{d_in, n, d_out, &plan};
+      ps[0] = PartStream{d_in, n, d_out, &plan, d_dict, dict ? dict_n : 0};
       rc = decode_parts(c, ps, ok, c->stream);
       if (rc == 0 && ok[0]) {
         const uint64_t len = (uint64_t)plan.total;
-        if (max_out >= 0 && (int64_t)len > max_out) {   // decode.ts:57-62
-          out->size = len;
-          rc = MIB_E_OUTPUT_LIMIT;
-        } else {
-          out->data = (uint8_t *)malloc(len);
-          out->size = len;
-          if (hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
-        }
+        out->data = (uint8_t *)malloc(len);
+        out->size = len;
+        if (hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
         hipFree(d_out);
+        if (d_dict) hipFree(d_dict);
         hipFree(d_in);
         return rc;
       }

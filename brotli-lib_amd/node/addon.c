@@ -83,10 +83,10 @@ static int64_t get_i64(napi_env env, napi_value v, int64_t dflt) {
   return r;
 }
 
-/* encode(bytes, quality, lgwin, mode) -> Buffer */
+/* encode(bytes, quality, lgwin, mode, dictionary|null) -> Buffer */
 static napi_value js_encode(napi_env env, napi_callback_info info) {
-  size_t argc = 4;
-  napi_value argv[4];
+  size_t argc = 5;
+  napi_value argv[5];
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   const uint8_t *p;
   size_t n;
@@ -99,6 +99,9 @@ static napi_value js_encode(napi_env env, napi_callback_info info) {
   o.quality = get_int(env, argc > 1 ? argv[1] : NULL, o.quality);
   o.lgwin = get_int(env, argc > 2 ? argv[2] : NULL, o.lgwin);
   o.mode = get_int(env, argc > 3 ? argv[3] : NULL, o.mode);
+  size_t dn = 0;
+  if (argc > 4 && get_bytes(env, argv[4], &o.dict, &dn) == 0) o.dict_len = dn;
+  else o.dict = NULL;
   mib_buf b = {0, 0};
   int rc = mib_encode(p, n, &o, &b);
   if (rc) return throw_code(env, rc);
@@ -156,16 +159,20 @@ static void encoder_finalize(napi_env env, void *data, void *hint) {
   mib_encoder_free((mib_encoder *)data);
 }
 
-/* encoderNew(quality, lgwin, mode) -> external handle */
+/* encoderNew(quality, lgwin, mode, dictionary|null) -> external handle (the encoder copies
+ * the dictionary) */
 static napi_value js_encoder_new(napi_env env, napi_callback_info info) {
-  size_t argc = 3;
-  napi_value argv[3], out;
+  size_t argc = 4;
+  napi_value argv[4], out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   mib_enc_opts o;
   mib_enc_opts_default(&o);
   o.quality = get_int(env, argc > 0 ? argv[0] : NULL, o.quality);
   o.lgwin = get_int(env, argc > 1 ? argv[1] : NULL, o.lgwin);
   o.mode = get_int(env, argc > 2 ? argv[2] : NULL, o.mode);
+  size_t dn = 0;
+  if (argc > 3 && get_bytes(env, argv[3], &o.dict, &dn) == 0) o.dict_len = dn;
+  else o.dict = NULL;
   mib_encoder *e = mib_encoder_new(&o);
   if (!e) return throw_code(env, MIB_E_OUT_OF_MEMORY);
   CHECK(env, napi_create_external(env, e, encoder_finalize, NULL, &out));
@@ -251,19 +258,25 @@ static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
 }
 
 /* ---- asynchronous batches: the GPU work runs on a libuv worker thread (napi_async_work),
-   the JS thread gets a Promise; the input arrays are held by references until it settles */
+   the JS thread gets a Promise.  The inputs are COPIED into memory the addon owns before the
+   work is queued: JS may transfer or detach an ArrayBuffer while the Promise is pending, and
+   the worker must never read a buffer the JS heap has let go of. */
 typedef struct {
   napi_async_work work;
   napi_deferred deferred;
-  napi_ref *refs;   /* the inputs, alive until complete() */
   uint32_t k;
   int decode;       /* 0: encode batch, 1: decode batch */
   mib_enc_opts o;
+  uint8_t *blob;    /* the inputs, back to back (owned) */
   mib_span *in;
   mib_buf *res;
   int *st;
   int rc;
 } AsyncBatch;
+
+static void async_free(AsyncBatch *a) {
+  free(a->blob), free(a->in), free(a->res), free(a->st), free(a);
+}
 
 static void async_execute(napi_env env, void *data) {
   AsyncBatch *a = (AsyncBatch *)data;
@@ -297,9 +310,8 @@ static void async_complete(napi_env env, napi_status status, void *data) {
     napi_reject_deferred(env, a->deferred, err);
     for (uint32_t i = 0; i < a->k; i++) mib_buf_free(&a->res[i]);
   }
-  for (uint32_t i = 0; i < a->k; i++) napi_delete_reference(env, a->refs[i]);
   napi_delete_async_work(env, a->work);
-  free(a->refs), free(a->in), free(a->res), free(a->st), free(a);
+  async_free(a);
 }
 
 /* encodeBatchAsync(inputs, quality, lgwin, mode) / decodeBatchAsync(inputs) -> Promise */
@@ -326,17 +338,38 @@ static napi_value start_async(napi_env env, napi_callback_info info, int decode)
   a->in = (mib_span *)calloc(k ? k : 1, sizeof(mib_span));
   a->res = (mib_buf *)calloc(k ? k : 1, sizeof(mib_buf));
   a->st = (int *)calloc(k ? k : 1, sizeof(int));
-  a->refs = (napi_ref *)calloc(k ? k : 1, sizeof(napi_ref));
-  for (uint32_t i = 0; i < k; i++) {
-    napi_value e;
-    napi_get_element(env, argv[0], i, &e);
-    if (get_bytes(env, e, &a->in[i].data, &a->in[i].size)) {
-      for (uint32_t q = 0; q < i; q++) napi_delete_reference(env, a->refs[q]);
-      free(a->refs), free(a->in), free(a->res), free(a->st), free(a);
-      napi_throw_type_error(env, NULL, "every input must be a Uint8Array");
-      return NULL;
+  if (!a->in || !a->res || !a->st) {
+    async_free(a);
+    return throw_code(env, MIB_E_OUT_OF_MEMORY);
+  }
+  size_t total = 0;
+  for (int pass = 0; pass < 2; pass++) {   /* sizes, then the copies */
+    size_t at = 0;
+    for (uint32_t i = 0; i < k; i++) {
+      napi_value e;
+      const uint8_t *p;
+      size_t n;
+      napi_get_element(env, argv[0], i, &e);
+      if (get_bytes(env, e, &p, &n)) {
+        async_free(a);
+        napi_throw_type_error(env, NULL, "every input must be a Uint8Array");
+        return NULL;
+      }
+      if (pass) {
+        if (n) memcpy(a->blob + at, p, n);
+        a->in[i].data = a->blob + at;
+        a->in[i].size = n;
+      }
+      at += n;
     }
-    napi_create_reference(env, e, 1, &a->refs[i]);
+    if (!pass) {
+      total = at;
+      a->blob = (uint8_t *)malloc(total ? total : 1);
+      if (!a->blob) {
+        async_free(a);
+        return throw_code(env, MIB_E_OUT_OF_MEMORY);
+      }
+    }
   }
   CHECK(env, napi_create_promise(env, &a->deferred, &promise));
   napi_create_string_utf8(env, decode ? "brotli_amd.decodeBatch" : "brotli_amd.encodeBatch", NAPI_AUTO_LENGTH, &name);

@@ -17,6 +17,9 @@ export interface BrotliEncodeOptions {
   mode?: EncoderMode
   /** accepted, no effect (as in the reference) */
   sizeHint?: number
+  /** extension: the encoder side of BrotliDecodeOptions.customDictionary; the stream decodes
+   *  with (and only with) the same dictionary */
+  customDictionary?: Uint8Array | Int8Array
 }
 
 export declare function brotliEncode(input: Uint8Array, options?: BrotliEncodeOptions): Uint8Array

@@ -25,19 +25,26 @@ function clampOptions(options) {
   return [quality | 0, lgwin | 0, mode | 0]
 }
 
+// customDictionary (extension, the encoder side of brotliDecode's option): Uint8Array / Int8Array
+function dictOf(options) {
+  const d = options && options.customDictionary
+  if (!d) return null
+  return d instanceof Uint8Array ? d : new Uint8Array(d.buffer, d.byteOffset, d.byteLength)
+}
+
 function toU8(b) {
   return new Uint8Array(b.buffer, b.byteOffset, b.byteLength)
 }
 
 function brotliEncode(input, options) {
   const [q, lg, m] = clampOptions(options)
-  return toU8(native.encode(input, q, lg, m))
+  return toU8(native.encode(input, q, lg, m, dictOf(options)))
 }
 
 class BrotliEncoder {
   constructor(options) {
     const [q, lg, m] = clampOptions(options)
-    this._h = native.encoderNew(q, lg, m)
+    this._h = native.encoderNew(q, lg, m, dictOf(options))
   }
   update(input) {
     return toU8(native.encoderUpdate(this._h, input))

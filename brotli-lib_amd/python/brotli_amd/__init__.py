@@ -41,7 +41,7 @@ class BrotliError(Exception):
 
 class _Opts(ctypes.Structure):
     _fields_ = [('quality', ctypes.c_int), ('lgwin', ctypes.c_int), ('mode', ctypes.c_int),
-                ('size_hint', ctypes.c_uint64)]
+                ('size_hint', ctypes.c_uint64), ('dict', ctypes.c_char_p), ('dict_len', ctypes.c_uint64)]
 
 
 class _Buf(ctypes.Structure):
@@ -107,6 +107,8 @@ def _L():
         lib.mib_woff2_transform_glyf.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
         lib.mib_woff2_transform_hmtx.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(_Buf)]
         lib.mib_part_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        lib.mib_default_ctx.restype = ctypes.c_void_p
+        lib.mib_ctx_clear_times.argtypes = [ctypes.c_void_p]
         _lib = lib
     return _lib
 
@@ -123,9 +125,12 @@ def _take(buf):
 
 
 def _opts(options):
-    """option clamping of encode.ts:54-71 / BrotliEncoder constructor :293-310"""
+    """option clamping of encode.ts:54-71 / BrotliEncoder constructor :293-310; plus the
+    extension `customDictionary` (the encoder side of brotliDecode's option of that name:
+    the stream then decodes with, and only with, the same dictionary).  The dictionary's
+    bytes object is kept on the returned structure for the duration of the call."""
     options = options or {}
-    o = _Opts(11, 22, EncoderMode.GENERIC, 0)
+    o = _Opts(11, 22, EncoderMode.GENERIC, 0, None, 0)
     if options.get('quality') is not None:
         o.quality = max(0, min(11, int(options['quality'])))
     if options.get('lgwin') is not None:
@@ -134,6 +139,10 @@ def _opts(options):
         o.mode = int(options['mode'])
     if options.get('sizeHint') is not None:
         o.size_hint = int(options['sizeHint'])
+    if options.get('customDictionary') is not None:
+        d = _bytes(options['customDictionary'])
+        o._keep = d
+        o.dict, o.dict_len = d, len(d)
     return o
 
 
@@ -286,6 +295,24 @@ def part_stats(ctx=None):
     a, b = ctypes.c_uint64(), ctypes.c_uint64()
     _L().mib_part_stats(ctx._c if ctx is not None else None, ctypes.byref(a), ctypes.byref(b))
     return a.value, b.value
+
+
+def default_profiling(on=True):
+    """Per-kernel timing (HIP events) of the host-buffer calls (brotliEncode, brotliDecode,
+    BrotliEncoder, the batches): on / off, and the accumulated times cleared."""
+    c = _L().mib_default_ctx()
+    if not c:
+        raise BrotliError('brotli_amd: no usable device')
+    _L().mib_ctx_set_profiling(c, 1 if on else 0)
+    _L().mib_ctx_clear_times(c)
+
+
+def default_kernel_times():
+    """{kernel: (ms, launches)} accumulated by the host-buffer calls since default_profiling()"""
+    c = _L().mib_default_ctx()
+    arr = (_KTime * 64)()
+    n = _L().mib_ctx_kernel_times(c, arr, 64)
+    return {arr[i].name.decode(): (arr[i].ms, arr[i].launches) for i in range(min(n, 64))}
 
 
 class DeviceContext:

@@ -135,6 +135,24 @@ def enwik_text(length, seed=1):
     return b''.join(out)[:length]
 
 
+# the last bytes of every page header of enwik_device's text (below)
+C5_TAIL = b'</timestamp></revision>\n    <text xml:space="preserve">'
+
+
+def c5_dictionary(n=65536, seed=4999):
+    """C5's custom dictionary (BASELINE.json config 5): n bytes of enwik-style text ending
+    with the page-header tail the streamed text repeats."""
+    return enwik_text(n - len(C5_TAIL), seed) + C5_TAIL
+
+
+def c5_stream(size, seed, device):
+    """C5's per-GPU input: ``size`` bytes of enwik_device text that opens with the last 120
+    bytes of c5_dictionary() (host bytes)."""
+    d = c5_dictionary()
+    data = bytes(enwik_device(size, seed, device).cpu().numpy().tobytes())
+    return d[-120:] + data[120:]
+
+
 def enwik_batch(count, length, seed0):
     """``count`` independent buffers (seeds seed0 .. seed0+count-1)."""
     return [enwik_text(length, seed0 + i) for i in range(count)]

@@ -47,6 +47,15 @@ typedef struct {
   int lgwin;          /* 10..24, default 22 */
   int mode;           /* MIB_MODE_* */
   uint64_t size_hint; /* accepted, no effect (as in the reference) */
+  /* customDictionary (extension: the reference's BrotliEncodeOptions, encode.ts:22-27, has
+   * none; this is the encoder side of brotliDecode's customDictionary, decode.ts:13-35).
+   * Copies into it are addressed the way the reference decoder resolves a compound
+   * dictionary (engine.ts:142-159,903-1011): distance > max distance.  That decoder only
+   * accepts a copy that ends exactly at the dictionary's last byte, so the encoder only
+   * emits such copies; the stream then decodes with the same dictionary, and only with it.
+   * Host memory, borrowed for the call (BrotliEncoder keeps its own copy). NULL: none. */
+  const uint8_t *dict;
+  uint64_t dict_len;
 } mib_enc_opts;
 
 typedef struct { uint8_t *data; size_t size; } mib_buf;          /* library-allocated result */
@@ -111,6 +120,11 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
 typedef struct { char name[32]; double ms; uint32_t launches; } mib_kernel_time;
 int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max);
 void mib_ctx_set_profiling(mib_ctx *c, int on);
+/* The context behind the host-buffer entry points (mib_encode, mib_decode, the batches,
+ * BrotliEncoder), created on first use (NULL without a device): for profiling them.  Its
+ * kernel times accumulate over those calls until mib_ctx_clear_times. */
+mib_ctx *mib_default_ctx(void);
+void mib_ctx_clear_times(mib_ctx *c);
 /* WOFF2 'glyf' transform (the FONT-mode caller, reference README.md:63;
  * W3C WOFF2 section 5.1): the glyf + loca tables of the TrueType font `ttf` become the
  * transformed glyf table (header, the seven streams, the overlap-simple bitmap), byte for

@@ -24,6 +24,7 @@ int oracle_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_
 int oracle_decode_probe(const uint8_t *in, size_t n, const uint64_t *pos, size_t npos, void *states);
 /* static-dictionary word references decoded so far by this process (test instrumentation) */
 uint64_t oracle_word_refs(void);
+uint64_t oracle_compound_refs(void);
 
 /* encode.ts:50 brotliEncode (bugs A,B fixed = the survey's "ref-fixed"; C,E fixed too).
  * quality 0..11, lgwin 10..24, mode 0 GENERIC / 1 TEXT / 2 FONT. */

@@ -84,6 +84,12 @@ def word_refs():
     return lib().oracle_word_refs()
 
 
+def compound_refs():
+    """compound-dictionary (customDictionary) copies the oracle decoder has met in this process"""
+    lib().oracle_compound_refs.restype = ctypes.c_uint64
+    return lib().oracle_compound_refs()
+
+
 def probe(data, positions):
     """decoder states (parts.h PartEntry layout) at the given ascending output positions:
     the command starting there, or the metablock header starting there (flags bit 2)."""

@@ -25,6 +25,22 @@ class _Bits:
         return v
 
 
+def index_block(stream, at=0):
+    """(payload byte offset, payload length) of the metadata block at byte `at` (window bits
+    first when at == 0), or None when there is none"""
+    r = _Bits(stream, 8 * at)
+    if at == 0 and r.get(1):
+        if r.get(3) == 0:
+            r.get(3)
+    if r.get(1) != 0 or r.get(2) != 3 or r.get(1) != 0:
+        return None
+    nb = r.get(2)
+    if nb == 0:
+        return None
+    length = r.get(8 * nb) + 1
+    return (r.bit + 7) >> 3, length
+
+
 def read_index(stream, at=0):
     """(head, entries) of the index block at byte `at` (window bits first when at == 0), or None"""
     r = _Bits(stream, 8 * at)

@@ -7,6 +7,8 @@ C2: one 64 MiB (67,108,864 B) enwik-style buffer, q11 GENERIC lgwin 22, encoded 
 C3: 1024 x 262,144 B WOFF2-transformed-glyf-like buffers (seeds 1000+i), q11 FONT, through
     encode_batch and the device-resident context; every stream decoded by the HIP decoder,
     a sample by the oracle.
+C4: the per-GPU shard, 1024 x 1 MiB enwik-style buffers, q11: every stream HIP-decoded, 16 by
+    the oracle.  (C5 at full size: tests/test_gpu_custom_dict.py.)
 Plus: a context on the last visible device round-trips (per-device decoder tables).
 """
 from concurrent.futures import ProcessPoolExecutor
@@ -29,7 +31,9 @@ def test_c2_single_64mib_stream_q11():
     got = _oracle.decode(enc)
     assert isinstance(got, bytes) and got == d, 'oracle decode of the GPU stream'
     assert brotli_amd.brotliDecode(enc) == d, 'HIP decode of the GPU stream'
-    assert brotli_amd.brotliDecodedSize(enc) == -1 or brotli_amd.brotliDecodedSize(enc) == len(d)
+    # 64 MiB is four 16 MiB metablocks (encode.ts:206), so the reference's header peek
+    # (engine.ts:2155-2192: the first metablock must be the last) has no size for it either
+    assert brotli_amd.brotliDecodedSize(enc) == -1 == _oracle.peek_size(enc)
     # the reference's own encoder (oracle, ref-fixed) on a prefix: decoded on the GPU
     ref = _oracle.encode(d[:300000], 11, 22)
     assert brotli_amd.brotliDecode(ref) == d[:300000]
@@ -50,6 +54,33 @@ def test_c3_glyf_batch_font_mode():
     ours = sum(len(outs[i]) for i in range(0, 8))
     print('C3 ratio %.4f; first 8: GPU %d vs ref-fixed %d bytes (%.4f)' % (ratio, ours, ref, ours / ref))
     assert ours < 1.05 * ref
+
+
+def test_c4_per_gpu_shard_1024x1mib_q11():
+    """C4's per-GPU shard at full size, exactly as bench.py runs it on rank 0: 1024 x 1 MiB
+    enwik-style buffers (enwik_device, seed 2000) encoded q11 lgwin 22 through the
+    device-resident context; the HIP decoder returns every buffer bit-exactly, and the oracle
+    (the reference decoder restated) decodes 16 of the GPU streams to the same bytes."""
+    torch = pytest.importorskip('torch')
+    k, n = 1024, MIB
+    dev = torch.device('cuda', 0)
+    data = datagen.enwik_device(k * n, 2000, dev)
+    cap = k * n + k * n // 8 + 4096 * k
+    comp = torch.empty(cap, dtype=torch.uint8, device=dev)
+    ctx = brotli_amd.DeviceContext(0)
+    off = ctx.encode(data.data_ptr(), [i * n for i in range(k + 1)], comp.data_ptr(), cap, {'quality': 11, 'lgwin': 22})
+    slot = n + 4096
+    out = torch.empty(k * slot, dtype=torch.uint8, device=dev)
+    sizes, status = ctx.decode(comp.data_ptr(), off, out.data_ptr(), [i * slot for i in range(k + 1)])
+    assert status == [0] * k and sizes == [n] * k
+    assert torch.equal(out.view(k, slot)[:, :n], data.view(k, n))
+    raw = comp[:off[-1]].cpu().numpy().tobytes()
+    host = data.cpu().numpy().tobytes()
+    for i in range(0, k, 64):
+        assert _oracle.decode(raw[off[i]:off[i + 1]]) == host[i * n:(i + 1) * n], i
+    ratio = off[-1] / (k * n)
+    print('C4 shard ratio %.5f' % ratio)
+    assert ratio < 0.40
 
 
 def test_c3_device_context_matches_batch():

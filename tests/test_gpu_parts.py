@@ -120,6 +120,55 @@ def test_corrupt_index_falls_back_to_serial():
         assert got == want, (got, want)
 
 
+class _W:   # LSB-first bit writer
+    def __init__(self):
+        self.v, self.n = 0, 0
+
+    def put(self, nbits, val):
+        self.v |= (val & ((1 << nbits) - 1)) << self.n
+        self.n += nbits
+
+    def bytes(self):
+        return self.v.to_bytes((self.n + 7) // 8, 'little')
+
+
+def test_index_pointing_into_its_own_payload_is_not_followed():
+    """An index whose first entry is not the metablock right after the index block is not
+    trusted (runtime.cpp plan_parts).  Here the metadata payload hides a second, complete
+    metablock sequence (stream B) and the entries point into it; every part of B would check
+    out against entries describing B.  The reference decoder skips the payload and decodes
+    what follows it (stream A): so must the GPU."""
+    a, enc_a = _enwik_stream(3 << 20, 2)
+    b, enc_b = _enwik_stream(3 << 20, 3)
+    pay_a, len_a = _parts.index_block(enc_a)
+    pay_b, len_b = _parts.index_block(enc_b)
+    head_b = enc_b[pay_b:pay_b + 32]
+    _, ents_b = _parts.read_index(enc_b)
+    mb_a, mb_b = enc_a[pay_a + len_a:], enc_b[pay_b + len_b:]
+    payload_len = len_b + len(mb_b)
+    w = _W()
+    w.put(4, ((22 - 17) << 1) | 1)   # window bits, lgwin 22
+    w.put(1, 0)                      # ISLAST 0
+    w.put(2, 3)                      # MNIBBLES: metadata
+    w.put(1, 0)                      # reserved
+    w.put(2, 3)                      # MSKIPBYTES
+    w.put(24, payload_len - 1)
+    hdr = w.bytes()
+    pay_f = len(hdr)
+    forged_ents = ents_b.copy()
+    shift = 8 * (pay_f - pay_b)
+    forged_ents['bit'] += shift
+    forged_ents['mb_bit'] += shift
+    index_b = head_b + forged_ents.tobytes() + enc_b[pay_b + 32 + ents_b.nbytes:pay_b + len_b]
+    assert len(index_b) == len_b
+    forged = hdr + index_b + mb_b + mb_a
+    assert _oracle.decode(forged) == a   # the reference decoder: A
+    p0, f0 = brotli_amd.part_stats()
+    assert brotli_amd.brotliDecode(forged) == a
+    p1, f1 = brotli_amd.part_stats()
+    assert p1 == p0, 'the forged index was followed'
+
+
 def test_streaming_chunks_carry_chained_indexes(monkeypatch):
     monkeypatch.setenv('MIB_STREAM_CHUNK', '8')   # 8 MiB device chunks: three chained indexes
     data = datagen.enwik_text(20 << 20, 9)
