@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
   const uint8_t *data = nullptr;
   int ndirect = 0, npostfix = 0;
-  uint32_t parts = 0, abs0 = 0, pbits = 16, plag = 0, maxback = 0;
+  uint32_t parts = 0, abs0 = 0, pbits = 16, plag = 0, maxback = 0, cdl = 0;
   bool words = false;
   if (sgi < nsegs) {
     const Seg &sg = segs[sgi];
@@ -171,6 +171,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     plag = jb.part_lag;
     maxback = (1u << jb.lgwin) - 16;
     words = jb.dict != 0;
+    cdl = jb.cdict ? jb.cdict_len : 0u;
   }
   if (__ballot(a < b) == 0) return;
   // prices: iteration 0 from zopfli-cost-model.ts's initial model, iteration 1 from the
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
           ln = word ? ln : 0u;
           d = min(abs0 + p, maxback) + ln;
         } else if (words && is_dict(md)) {   // a dictionary word (the only entry): its distance at p, its exact length
-          d = min(abs0 + p, maxback) + 1 + (md & 0x7FF);
+          d = min(abs0 + p, maxback) + 1 + cdl + (md & 0x7FF);   // (a custom dictionary comes first, engine.ts:907)
           md = d | kDictFlag;
           word = ln == match_length(cur.m[q]) ? 1u : 0u;   // cut by the segment end: unusable
           ln = word ? ln : 0u;

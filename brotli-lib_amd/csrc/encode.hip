@@ -291,16 +291,16 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     if (jb.hist_tab) any_hist = true;
     jb.out_base = sd[j].out_base;
     jb.parts = (!jb.uncompressed && wants_parts(sd[j])) ? 1 : 0;
-    // custom dictionary: its tail copies (kCDictMark records; beside the static words: a word
-    // record is kDictFlag | index, and a tail copy's real distance stays below 2^23 wherever
-    // words are used)
+    // custom dictionary: its tail copies (kCDictMark records) beside the static words, whose
+    // distances it shifts by its length (the decoder addresses it first, engine.ts:907-913);
+    // a word's flagged distance must stay below 2^23, so words need a dictionary < 4 MiB
     if (!jb.uncompressed && sd[j].cdict) {
       jb.cdict = sd[j].cdict;
       jb.cdict_len = sd[j].cdict_len;
       jb.cdict_tail4 = sd[j].cdict_tail4;
       any_cdict = true;
     }
-    jb.dict = (!jb.uncompressed && !sd[j].streaming && !sd[j].hist_tab && prm.quality >= 10 && prm.lgwin <= 22 &&
+    jb.dict = (!jb.uncompressed && jb.cdict_len < (1u << 22) && !sd[j].streaming && !sd[j].hist_tab && prm.quality >= 10 && prm.lgwin <= 22 &&
                dict_enabled()) ? 1 : 0;
     jb.dict_span = dict_span();
     if (jb.dict) any_dict = true;
