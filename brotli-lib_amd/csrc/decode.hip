@@ -2241,7 +2241,7 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
   const PartEntry e = *(const PartEntry *)job.part_entry;
   const bool last = job.next_entry == nullptr;
   const int lane = LANE;
-  if (job.total <= 0 || job.total >= (1ll << 30) || e.pos > (uint64_t)job.total) return kPartFail;
+  if (job.total <= 0 || job.total > (1ll << 30) || e.pos > (uint64_t)job.total) return kPartFail;
   s.part = 1;
   s.pidx = job.pidx;
   s.prog = job.prog;
@@ -2256,9 +2256,10 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
     g_lds.part_seen[lane] = 0;
     s.cover_lo = job.pidx >= 64 ? (int)job.ppos[job.pidx - 64] : 0;
   }
-  // the output is the ring: no wrap, no flush
+  // the output is the ring: no wrap, no flush (positions stay below total <= 2^30 <= the
+  // ring size, so every `& rmask` is the identity and every fence is the end)
   int rs = 1 << job.max_ring_log;
-  while (rs < job.total + 64) rs <<= 1;
+  while (rs < job.total + 64 && rs < (1 << 30)) rs <<= 1;
   s.max_ring = 1 << job.max_ring_log;
   s.max_back = s.max_ring - 16;
   s.ring = job.out;

@@ -204,7 +204,7 @@ bool plan_parts(Fetch &fetch, uint64_t n, PartPlan &plan) {
     at = next;
   }
   if (next != 0) return false;   // the stream's total is only known from the final chunk's head
-  if (plan.ent.size() < 2 || plan.total <= 0 || plan.total >= (1ll << 30)) return false;
+  if (plan.ent.size() < 2 || plan.total <= 0 || plan.total > (1ll << 30)) return false;
   if (plan.ent[0].pos != 0 || !(plan.ent[0].flags & mib::kPartAtMb)) return false;
   if (plan.ent[0].bit != 8 * first_end || plan.ent[0].mb_bit != plan.ent[0].bit || plan.ent[0].mb_pos != 0) return false;
   for (size_t i = 0; i < plan.ent.size(); i++) {
