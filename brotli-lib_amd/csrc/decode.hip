@@ -1756,7 +1756,10 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     fill();
     copy_len = copy_off + rmany(cbits >> 8);
     // literals and copy must stay inside this block type, the window and the ring
-    if (insert_len > lit_blen || (int64_t)pos + insert_len + copy_len >= lim ||
+    // (32-bit: pos < 2^30 and each length < 2^24 + 2^15, so the sum cannot overflow; a 64-bit
+    // compare is a VALU op on VGPRs here, and the compiler drained vmcnt before it -- every
+    // command then waited for the previous command's copy load and stores)
+    if (insert_len > lit_blen || pos + insert_len + copy_len >= lim ||
         ho + ((insert_len * 15) >> 4) > 2030 - 12) {
       // hand the command over undecoded
       buf = buf0;
@@ -1895,20 +1898,25 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     finish_copy();
     {
       const int cl = copy_len, dist = distance;
+      // Every copy load below is unconditional (lanes past the copy read an in-range byte):
+      // a load under an exec-masked branch can stay outstanding on the path that skips the
+      // branch, and the compiler then drains vmcnt at an unrelated later reuse of its
+      // register -- it did so inside the literal loop, once per literal.
       if (cl <= 64) {   // one lane per byte: issue the load, complete later
         const int q = dist >= cl ? lane : lane % dist;
-        pend_v = lane < cl ? (int)ring[src + q] : 0;
+        pend_v = (int)ring[src + (lane < cl ? q : 0)];
         pend_dst = pos;
         pend_cl = cl;
       } else {
         int lastv = 0;
         const int nit = U((cl + 63) >> 6);
+        const int last = cl - 1;
         if (dist >= cl && nit <= 4) {
           // up to 256 bytes: every load issued before the first store (one round trip, not nit)
-          const int v0 = lane < cl ? (int)ring[src + lane] : 0;
-          const int v1 = lane + 64 < cl ? (int)ring[src + 64 + lane] : 0;
-          const int v2 = lane + 128 < cl ? (int)ring[src + 128 + lane] : 0;
-          const int v3 = lane + 192 < cl ? (int)ring[src + 192 + lane] : 0;
+          const int v0 = ring[src + min(lane, last)];
+          const int v1 = ring[src + min(lane + 64, last)];
+          const int v2 = ring[src + min(lane + 128, last)];
+          const int v3 = ring[src + min(lane + 192, last)];
           if (lane < cl) ring[pos + lane] = (uint8_t)v0;
           if (lane + 64 < cl) ring[pos + 64 + lane] = (uint8_t)v1;
           if (lane + 128 < cl) ring[pos + 128 + lane] = (uint8_t)v2;
@@ -1917,9 +1925,10 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
         } else if (dist >= cl) {
           for (int it = 0; it < nit; it++) {
             const int k = it * 64 + lane;
+            const int v = ring[src + min(k, last)];
             if (k < cl) {
-              lastv = ring[src + k];
-              ring[pos + k] = (uint8_t)lastv;
+              lastv = v;
+              ring[pos + k] = (uint8_t)v;
             }
           }
         } else {
@@ -1927,9 +1936,10 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
           const int qstep = 64 % dist;
           for (int it = 0; it < nit; it++) {
             const int k = it * 64 + lane;
+            const int v = ring[src + q];   // (q < dist: inside the source)
             if (k < cl) {
-              lastv = ring[src + q];
-              ring[pos + k] = (uint8_t)lastv;
+              lastv = v;
+              ring[pos + k] = (uint8_t)v;
             }
             q += qstep;
             if (q >= dist) q -= dist;
