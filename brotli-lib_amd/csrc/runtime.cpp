@@ -18,9 +18,9 @@
 #include "parts.h"
 
 extern "C" hipError_t mib_decode_parts_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
-                                              unsigned *d_ticket, int grid, hipStream_t stream);
+                                              unsigned *d_ticket, int grid, int per_cu, hipStream_t stream);
 extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
-                                        uint64_t ring_bytes, int grid, hipStream_t stream);
+                                        uint64_t ring_bytes, int grid, int per_cu, hipStream_t stream);
 extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut);
 extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t *d_offsets, int k, uint8_t *d_heads,
                                             hipStream_t stream);
@@ -40,6 +40,7 @@ std::mutex g_mu;
 int g_device = 0;                 // device of the default context (mib_init)
 constexpr int kMaxDevices = 64;
 bool g_dev_ready[kMaxDevices];    // per device: checked to be gfx950, command table uploaded
+int g_dev_cus[kMaxDevices];       // per device: compute units
 
 void build_cmd_lut(int16_t *lut) {   // engine.ts:65-90
   static const int ins_bits[24] = {0, 0, 0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 7, 8, 9, 10, 12, 14, 24};
@@ -82,6 +83,7 @@ int ensure_device(int device) {
     fprintf(stderr, "brotli_amd: device %d is %s, this build targets gfx950\n", device, prop.gcnArchName);
     return MIB_E_NO_DEVICE;
   }
+  g_dev_cus[device] = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   int16_t lut[704 * 4];
   build_cmd_lut(lut);
   HIP_OK(mib_decode_init_tables(lut));
@@ -262,6 +264,14 @@ struct DeviceFetch {   // stream bytes on the device (small reads: index heads a
     return hipMemcpyAsync(dst, d + off, len, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess;
   }
 };
+
+// Waves a decode launch puts on each CU (1..4): a call with few streams gives each stream
+// a whole CU's LDS (decode.hip decode_lds_plan)
+int waves_per_cu(int device, size_t waves) {
+  const size_t cus = (device >= 0 && device < kMaxDevices && g_dev_cus[device] > 0) ? (size_t)g_dev_cus[device] : 256;
+  const size_t w = (waves + cus - 1) / cus;
+  return (int)std::max<size_t>(1, std::min<size_t>(4, w));
+}
 
 }  // namespace
 
@@ -495,7 +505,8 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
     hipEventCreate(&e1);
     hipEventRecord(e0, stream);
   }
-  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, stream));
+  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, waves_per_cu(c->device, (size_t)grid),
+                           stream));
   if (c->profiling) hipEventRecord(e1, stream);
   HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * k, hipMemcpyDeviceToHost, stream));
   HIP_OK(hipStreamSynchronize(stream));
@@ -594,7 +605,8 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
     hipEventCreate(&e1);
     hipEventRecord(e0, stream);
   }
-  HIP_OK(mib_decode_parts_launch(c->d_jobs, (int)nj, c->d_scratch, per_block, d_ticket, grid, stream));
+  HIP_OK(mib_decode_parts_launch(c->d_jobs, (int)nj, c->d_scratch, per_block, d_ticket, grid,
+                                 waves_per_cu(c->device, (size_t)grid), stream));
   if (c->profiling) hipEventRecord(e1, stream);
   HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * nj, hipMemcpyDeviceToHost, stream));
   HIP_OK(hipStreamSynchronize(stream));
