@@ -13,6 +13,8 @@ resident in HBM when the timed region starts):
                 (64 MiB by default: --size for more).
   ref           decode of the reference's own bench streams (noto-tc etc.), one stream per
                 call: the single-stream latency case of the reference's README.
+  latency       one brotliEncode + one brotliDecode per call of the reference's encode bench
+                inputs (13 B .. 45 KB) and C1 through the host API, next to README.md:88-94.
 A step encodes the batch (mib_ctx_encode: packed compressed streams in HBM), gathers the
 compressed shards to rank 0 over RCCL (N > 1, c3/c4; the only collective)
 and decodes them back (mib_ctx_decode) into HBM.  The round trip is checked bit-exact on
@@ -64,7 +66,7 @@ def parse():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--workload', default='c4', choices=sorted(WORKLOADS) + ['ref'])
+    ap.add_argument('--workload', default='c4', choices=sorted(WORKLOADS) + ['ref', 'latency'])
     ap.add_argument('--streams', type=int, default=-1, help='buffers per GPU (-1: the workload\'s)')
     ap.add_argument('--size', type=int, default=-1, help='bytes per buffer (-1: the workload\'s)')
     ap.add_argument('--quality', type=int, default=11)
@@ -290,6 +292,75 @@ def run_stream(args, rank, world, local):
         dist.destroy_process_group()
 
 
+# The reference's encode bench inputs (bench/encode.bench.ts:5-16) and its published q11 encode
+# times (README.md:88-94, "unstated, M2 Max implied"), plus C1's 45,000 B enwik-style slice.
+LATENCY_INPUTS = [
+    ('short 13 B', lambda: b'Hello, World!', 0.001),
+    ('medium 4.5 KB', lambda: b'The quick brown fox jumps over the lazy dog. ' * 100, 0.27),
+    ('long 45 KB', lambda: b'The quick brown fox jumps over the lazy dog. ' * 1000, 3.0),
+    ('html 8 KB', lambda: b'<!DOCTYPE html><html><head><title>Test</title></head><body>' + b'<p>Content</p>' * 500
+     + b'</body></html>', None),
+    ('C1 enwik 45,000 B', None, None),
+]
+
+
+def run_latency(args):
+    """latency leg: ONE brotliEncode (q11) and ONE brotliDecode per call through the drop-in
+    host API (host buffers in and out: PCIe, launch and synchronisation included), median of
+    `steps` x 20 calls per input, next to the reference's published single-call encode times;
+    the oracle (the reference's q11 encoder restated) times the same calls on one host core."""
+    import statistics
+    import brotli_amd
+    from brotli_amd import datagen
+    sys.path.insert(0, os.path.join(ROOT, 'tests'))
+    rows = []
+    reps = max(1, args.steps) * 20
+    for name, make, ref_ms in LATENCY_INPUTS:
+        data = make() if make else datagen.enwik_text(45000, 1)
+        for _ in range(max(1, args.warmup) * 3):
+            enc = brotli_amd.brotliEncode(data, {'quality': 11})
+            assert brotli_amd.brotliDecode(enc) == data
+        te, td = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            enc = brotli_amd.brotliEncode(data, {'quality': 11})
+            t1 = time.perf_counter()
+            out = brotli_amd.brotliDecode(enc)
+            t2 = time.perf_counter()
+            te.append(t1 - t0)
+            td.append(t2 - t1)
+        assert out == data
+        row = {'input': name, 'bytes': len(data), 'compressed': len(enc),
+               'encode_ms_median': round(statistics.median(te) * 1e3, 4),
+               'decode_ms_median': round(statistics.median(td) * 1e3, 4),
+               'ref_encode_ms_published': ref_ms}
+        if not args.no_cpu_baseline:
+            import _oracle
+            t0 = time.perf_counter()
+            n = 0
+            while n < 5 or time.perf_counter() - t0 < 0.5:
+                e = _oracle.encode(data, 11, 22)
+                n += 1
+            row['oracle_encode_ms'] = round((time.perf_counter() - t0) / n * 1e3, 4)
+            row['oracle_compressed'] = len(e)
+        rows.append(row)
+    tot_b = sum(r['bytes'] for r in rows)
+    tot_s = sum((r['encode_ms_median'] + r['decode_ms_median']) * 1e-3 for r in rows)
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = {'value': round(tot_b / 1e6 / sum(r['oracle_encode_ms'] * 1e-3 for r in rows), 4), 'unit': 'MB/s',
+               'cores': 1, 'kind': 'port',
+               'sample': 'the same inputs, one oracle q11 encode per call on one host thread (encode only)'}
+    print(json.dumps({
+        'metric': 'single-call brotliEncode + brotliDecode latency (host API)', 'value': round(tot_b / 1e6 / tot_s, 4),
+        'unit': 'MB/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(tot_s * 1e3, 4),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u8', 'data': 'reference bench inputs',
+        'config': {'workload': 'one call per input: the reference encode bench inputs (bench/encode.bench.ts) and C1 '
+                               '(45,000 B enwik-style), q11 lgwin 22, host buffers', 'name': 'latency',
+                   'parallelism': 'replicas1'},
+        'inputs': rows, 'roofline': None, 'cpu_baseline': cpu}), flush=True)
+
+
 # The reference's own bench streams (tests/golden/bench, bench/fixtures of the reference) and
 # its decode times: README.md:79-82 (Apple M2 Max, Node 22) and SURVEY.md §6 (the survey
 # host: Xeon, Node 12, 1 thread).
@@ -381,6 +452,8 @@ def main():
     wl = args.workload
     if wl == 'ref':
         return run_ref(args)
+    if wl == 'latency':
+        return run_latency(args)
     if wl == 'c5':
         return run_stream(args, int(os.environ.get('RANK', '0')), int(os.environ.get('WORLD_SIZE', '1')),
                           int(os.environ.get('LOCAL_RANK', '0')))

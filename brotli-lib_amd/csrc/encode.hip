@@ -38,6 +38,7 @@
 extern "C" void mib_ctx_add_time(mib_ctx *c, const char *name, double ms);
 extern "C" int mib_ctx_profiling(mib_ctx *c);
 extern "C" void **mib_ctx_enc_ws(mib_ctx *c);
+extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need);
 
 // ====================================================================== host orchestration
 using namespace mib;
@@ -719,22 +720,15 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
     ioff[i + 1] = ioff[i] + ((in[i].size + 255) & ~(uint64_t)255);
     cap += out_bound(in[i].size);
   }
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  if (hipMalloc(&d_in, ioff[k] + 64) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
-  if (hipMalloc(&d_out, cap + 64) != hipSuccess) {
-    hipFree(d_in);
-    return MIB_E_OUT_OF_MEMORY;
-  }
+  // (the default context's staging buffers, kept across calls)
+  uint8_t *d_in = mib_ctx_stage(c, 0, ioff[k] + 64), *d_out = mib_ctx_stage(c, 1, cap + 64);
+  if (!d_in || !d_out) return MIB_E_OUT_OF_MEMORY;
   hipMemsetAsync(d_in, 0, ioff[k] + 64, st);
   for (size_t i = 0; i < k; i++)
     if (in[i].size) hipMemcpyAsync(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice, st);
   DevDict dd;
   int rc = o ? dd.upload(o->dict, o->dict_len, st) : 0;
-  if (rc) {
-    hipFree(d_out);
-    hipFree(d_in);
-    return rc;
-  }
+  if (rc) return rc;
   std::vector<StreamDesc> sd(k);
   for (size_t i = 0; i < k; i++) {
     fill_desc(sd[i], d_in + ioff[i], in[i].size, prm, true);
@@ -755,8 +749,6 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
   }
   hipStreamSynchronize(st);
   dd.release();
-  hipFree(d_out);
-  hipFree(d_in);
   return rc;
 }
 
@@ -806,8 +798,8 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
     e->device = dev;
     cap += out_bound(ns[i]);
   }
-  uint8_t *d_out = nullptr;
-  if (hipMalloc(&d_out, cap + 64) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  uint8_t *d_out = mib_ctx_stage(c, 3, cap + 64);
+  if (!d_out) return MIB_E_OUT_OF_MEMORY;
   std::vector<StreamDesc> sd(k);
   for (size_t i = 0; i < k; i++) {
     mib_encoder *e = es[i];
@@ -851,7 +843,6 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
     }
     CK(hipStreamSynchronize(st));
   }
-  hipFree(d_out);
   return rc;
 }
 

@@ -290,6 +290,10 @@ struct mib_ctx {
   uint64_t parts_bytes = 0;
   // encode workspace (encode.hip)
   void *enc_ws = nullptr;
+  // staging buffers of the host-memory entry points (input, output, dictionary, encoder
+  // output), kept across calls so a small call does not pay hipMalloc / hipFree
+  uint8_t *stage[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t stage_cap[4] = {0, 0, 0, 0};
   // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
   uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
@@ -314,6 +318,12 @@ struct mib_ctx {
 extern "C" void mib_ctx_add_time(mib_ctx *c, const char *name, double ms) { c->add_time(name, ms); }
 extern "C" int mib_ctx_profiling(mib_ctx *c) { return c->profiling ? 1 : 0; }
 extern "C" void **mib_ctx_enc_ws(mib_ctx *c) { return &c->enc_ws; }
+int grow(void **p, uint64_t *cap, uint64_t need);
+// a staging buffer of at least `need` bytes (its content is not kept when it grows)
+extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need) {
+  if (slot < 0 || slot > 3) return nullptr;
+  return grow((void **)&c->stage[slot], &c->stage_cap[slot], need) == 0 ? c->stage[slot] : nullptr;
+}
 extern "C" void mib_encode_ws_free(void *ws);
 
 namespace {
@@ -338,6 +348,7 @@ mib_ctx *default_ctx() {
   return g_default_ctx;
 }
 
+}  // namespace
 int grow(void **p, uint64_t *cap, uint64_t need) {
   if (*cap >= need) return 0;
   if (*p) hipFree(*p);
@@ -348,7 +359,7 @@ int grow(void **p, uint64_t *cap, uint64_t need) {
   *cap = n;
   return 0;
 }
-
+namespace {
 }  // namespace
 
 extern "C" {
@@ -448,6 +459,8 @@ void mib_ctx_free(mib_ctx *c) {
   if (c->d_jobs) hipFree(c->d_jobs);
   if (c->d_aux) hipFree(c->d_aux);
   if (c->d_parts) hipFree(c->d_parts);
+  for (int i = 0; i < 4; i++)
+    if (c->stage[i]) hipFree(c->stage[i]);
   if (c->enc_ws) mib_encode_ws_free(c->enc_ws);
   if (c->stream) hipStreamDestroy(c->stream);
   delete c;
@@ -728,13 +741,10 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
   uint64_t cap = known ? (uint64_t)out_size : std::max<uint64_t>(1 << 20, 4 * (uint64_t)n + 4096);
   uint8_t *d_in = nullptr, *d_out = nullptr, *d_dict = nullptr;
   int rc = 0;
-  if (hipMalloc(&d_in, n + 16) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  if (!(d_in = mib_ctx_stage(c, 0, n + 16))) return MIB_E_OUT_OF_MEMORY;
   if (n) hipMemcpy(d_in, in, n, hipMemcpyHostToDevice);
   if (dict) {
-    if (hipMalloc(&d_dict, dict_n + 16) != hipSuccess) {
-      hipFree(d_in);
-      return MIB_E_OUT_OF_MEMORY;
-    }
+    if (!(d_dict = mib_ctx_stage(c, 2, dict_n + 16))) return MIB_E_OUT_OF_MEMORY;
     if (dict_n) hipMemcpy(d_dict, dict, dict_n, hipMemcpyHostToDevice);
   }
   if (exact_out < 0) {   // a stream with a part index: part-parallel, checked
@@ -743,7 +753,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     // (the index is untrusted: a total beyond maxOutputSize, or one the device cannot hold,
     // just leaves the stream to the serial decoder, which finds out what it really is)
     if (plan_parts(f, n, plan) && (max_out < 0 || plan.total <= max_out) &&
-        hipMalloc(&d_out, (uint64_t)plan.total + 4096) == hipSuccess) {
+        (d_out = mib_ctx_stage(c, 1, (uint64_t)plan.total + 4096)) != nullptr) {
       std::vector<PartStream> ps(1);
       std::vector<int> ok;
       ps[0] = PartStream{d_in, n, d_out, &plan, d_dict, dict ? dict_n : 0};
@@ -753,13 +763,8 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
         out->data = (uint8_t *)malloc(len);
         out->size = len;
         if (hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
-        hipFree(d_out);
-        if (d_dict) hipFree(d_dict);
-        hipFree(d_in);
         return rc;
       }
-      hipFree(d_out);
-      d_out = nullptr;
       rc = 0;
     }
   }
@@ -769,7 +774,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     uint64_t alloc = 1;
     while (alloc < cap) alloc <<= 1;
     alloc += 4096;
-    if (hipMalloc(&d_out, alloc) != hipSuccess) {
+    if (!(d_out = mib_ctx_stage(c, 1, alloc))) {
       rc = MIB_E_OUT_OF_MEMORY;
       break;
     }
@@ -788,8 +793,6 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     if (rc) break;
     rc = jobs[0].status;
     if (rc == MIB_E_NEED_SPACE && !known && cap < ((uint64_t)1 << 31)) {   // JS caps a Uint8Array near 2^31
-      hipFree(d_out);
-      d_out = nullptr;
       cap *= 4;
       continue;
     }
@@ -806,9 +809,6 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     }
     break;
   }
-  if (d_out) hipFree(d_out);
-  if (d_dict) hipFree(d_dict);
-  hipFree(d_in);
   return rc;
 }
 
@@ -824,17 +824,12 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
     uint64_t cap = est > 0 ? (uint64_t)est : std::max<uint64_t>(1 << 16, 8 * (uint64_t)in[i].size);
     ooff[i + 1] = ooff[i] + ((cap + 64 + 255) & ~(uint64_t)255);
   }
-  uint8_t *d_in = nullptr, *d_out = nullptr;
-  if (hipMalloc(&d_in, ioff[k] + 16) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+  uint8_t *d_in = mib_ctx_stage(c, 0, ioff[k] + 16), *d_out = mib_ctx_stage(c, 1, ooff[k] + 64);
+  if (!d_in || !d_out) return MIB_E_OUT_OF_MEMORY;
   for (size_t i = 0; i < k; i++)
     if (in[i].size) hipMemcpy(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice);
-  std::vector<int64_t> sizes(k);
   int rc = 0;
   for (size_t i = 0; i < k; i++) out[i].data = nullptr, out[i].size = 0;
-  if (hipMalloc(&d_out, ooff[k] + 64) != hipSuccess) {
-    hipFree(d_in);
-    return MIB_E_OUT_OF_MEMORY;
-  }
   // exact input lengths, padded slots
   std::vector<mib::DecJob> jobs(k);
   for (size_t i = 0; i < k; i++) {
@@ -857,16 +852,13 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
         out[i].data = (uint8_t *)malloc(len ? len : 1);
         out[i].size = len;
         if (len) hipMemcpy(out[i].data, d_out + ooff[i], len, hipMemcpyDeviceToHost);
-      } else if (jobs[i].status == MIB_E_NEED_SPACE) {
-        // retry this one alone with the growing single-stream path
-        mib_buf b;
-        status[i] = mib_decode(in[i].data, in[i].size, nullptr, 0, -1, -1, &b);
-        out[i] = b;
       }
     }
+    // then (the staging buffers are reused) the streams that outgrew their slots, alone
+    // through the growing single-stream path
+    for (size_t i = 0; i < k; i++)
+      if (jobs[i].status == MIB_E_NEED_SPACE) status[i] = mib_decode(in[i].data, in[i].size, nullptr, 0, -1, -1, &out[i]);
   }
-  hipFree(d_out);
-  hipFree(d_in);
   return rc;
 }
 

@@ -211,10 +211,11 @@ static napi_value js_encoder_finish(napi_env env, napi_callback_info info) {
   return take(env, &b);
 }
 
-/* encodeBatch([bytes...], quality, lgwin, mode) -> [Buffer...]: one GPU launch sequence */
+/* encodeBatch([bytes...], quality, lgwin, mode, gpus) -> [Buffer...]: one GPU launch sequence
+ * (gpus >= 0: sharded over that many GPUs, 0 = all; -1 / absent: the default device) */
 static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
-  size_t argc = 4;
-  napi_value argv[4], out;
+  size_t argc = 5;
+  napi_value argv[5], out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   uint32_t k = 0;
   bool is_arr = false;
@@ -240,7 +241,8 @@ static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
       return NULL;
     }
   }
-  int rc = mib_encode_batch(in, k, &o, res, st);
+  const int gpus = argc > 4 ? get_int(env, argv[4], -1) : -1;
+  int rc = gpus >= 0 ? mib_encode_batch_n(in, k, &o, gpus, res, st) : mib_encode_batch(in, k, &o, res, st);
   free(in);
   if (rc) {
     free(res), free(st);
@@ -266,6 +268,7 @@ typedef struct {
   napi_deferred deferred;
   uint32_t k;
   int decode;       /* 0: encode batch, 1: decode batch */
+  int gpus;         /* >= 0: sharded over that many GPUs (0 = all), else the default device */
   mib_enc_opts o;
   uint8_t *blob;    /* the inputs, back to back (owned) */
   mib_span *in;
@@ -280,7 +283,11 @@ static void async_free(AsyncBatch *a) {
 
 static void async_execute(napi_env env, void *data) {
   AsyncBatch *a = (AsyncBatch *)data;
-  a->rc = a->decode ? mib_decode_batch(a->in, a->k, a->res, a->st) : mib_encode_batch(a->in, a->k, &a->o, a->res, a->st);
+  if (a->gpus >= 0)
+    a->rc = a->decode ? mib_decode_batch_n(a->in, a->k, a->gpus, a->res, a->st)
+                      : mib_encode_batch_n(a->in, a->k, &a->o, a->gpus, a->res, a->st);
+  else
+    a->rc = a->decode ? mib_decode_batch(a->in, a->k, a->res, a->st) : mib_encode_batch(a->in, a->k, &a->o, a->res, a->st);
 }
 
 static void async_complete(napi_env env, napi_status status, void *data) {
@@ -314,10 +321,10 @@ static void async_complete(napi_env env, napi_status status, void *data) {
   async_free(a);
 }
 
-/* encodeBatchAsync(inputs, quality, lgwin, mode) / decodeBatchAsync(inputs) -> Promise */
+/* encodeBatchAsync(inputs, quality, lgwin, mode, gpus) / decodeBatchAsync(inputs, gpus) -> Promise */
 static napi_value start_async(napi_env env, napi_callback_info info, int decode) {
-  size_t argc = 4;
-  napi_value argv[4], promise, name;
+  size_t argc = 5;
+  napi_value argv[5], promise, name;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   bool is_arr = false;
   uint32_t k = 0;
@@ -329,6 +336,7 @@ static napi_value start_async(napi_env env, napi_callback_info info, int decode)
   AsyncBatch *a = (AsyncBatch *)calloc(1, sizeof(AsyncBatch));
   a->k = k;
   a->decode = decode;
+  a->gpus = decode ? (argc > 1 ? get_int(env, argv[1], -1) : -1) : (argc > 4 ? get_int(env, argv[4], -1) : -1);
   mib_enc_opts_default(&a->o);
   if (!decode) {
     a->o.quality = get_int(env, argc > 1 ? argv[1] : NULL, a->o.quality);

@@ -43,11 +43,15 @@ export declare function brotliDecode(buffer: Uint8Array, options?: BrotliDecodeO
 /** decoded size from the first metablock header, -1 when unknown */
 export declare function brotliDecodedSize(buffer: Uint8Array): number
 
-/** independent buffers in one GPU launch sequence */
-export declare function brotliEncodeBatch(inputs: Uint8Array[], options?: BrotliEncodeOptions): Uint8Array[]
-export declare function brotliEncodeBatchAsync(inputs: Uint8Array[], options?: BrotliEncodeOptions): Promise<Uint8Array[]>
+export interface BatchOptions {
+  /** shard the batch over this many GPUs (0: every visible one); absent: one GPU */
+  gpus?: number
+}
+/** independent buffers in one GPU launch sequence (or one per GPU, options.gpus) */
+export declare function brotliEncodeBatch(inputs: Uint8Array[], options?: BrotliEncodeOptions & BatchOptions): Uint8Array[]
+export declare function brotliEncodeBatchAsync(inputs: Uint8Array[], options?: BrotliEncodeOptions & BatchOptions): Promise<Uint8Array[]>
 /** a stream that fails to decode resolves to its Error in its slot */
-export declare function brotliDecodeBatchAsync(inputs: Uint8Array[]): Promise<(Uint8Array | Error)[]>
+export declare function brotliDecodeBatchAsync(inputs: Uint8Array[], options?: BatchOptions): Promise<(Uint8Array | Error)[]>
 /** WOFF2 'glyf' transform (W3C WOFF2 section 5.1) of a TrueType font, on the GPU: FONT-mode input for brotliEncode */
 export declare function woff2TransformGlyf(ttf: Uint8Array): Uint8Array
 /** WOFF2 'hmtx' transform (section 5.4), or null when the table must stay untransformed */

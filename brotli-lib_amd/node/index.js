@@ -77,20 +77,26 @@ function brotliDecode(buffer, options) {
   }
 }
 
+// options.gpus: shard the batch over that many GPUs (0: every visible one); absent: one GPU
+function gpusOf(options) {
+  const g = options && options.gpus
+  return g === undefined || g === null ? -1 : Math.max(0, g | 0)
+}
+
 // batch entry point of this engine: independent buffers in one GPU launch sequence
 function brotliEncodeBatch(inputs, options) {
   const [q, lg, m] = clampOptions(options)
-  return native.encodeBatch(inputs, q, lg, m).map(toU8)
+  return native.encodeBatch(inputs, q, lg, m, gpusOf(options)).map(toU8)
 }
 
 // the same, off the JS thread: the GPU work runs on a worker (napi_async_work), a Promise
 // resolves to the outputs (decode: a stream that fails gives its Error in its slot)
 function brotliEncodeBatchAsync(inputs, options) {
   const [q, lg, m] = clampOptions(options)
-  return native.encodeBatchAsync(inputs, q, lg, m).then((outs) => outs.map(toU8))
+  return native.encodeBatchAsync(inputs, q, lg, m, gpusOf(options)).then((outs) => outs.map(toU8))
 }
-function brotliDecodeBatchAsync(inputs) {
-  return native.decodeBatchAsync(inputs).then((outs) => outs.map((o) => (o instanceof Error ? o : toU8(o))))
+function brotliDecodeBatchAsync(inputs, options) {
+  return native.decodeBatchAsync(inputs, gpusOf(options)).then((outs) => outs.map((o) => (o instanceof Error ? o : toU8(o))))
 }
 
 // the FONT-mode caller's step before brotliEncode (reference README.md:63): the WOFF2

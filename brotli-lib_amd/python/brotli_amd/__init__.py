@@ -93,6 +93,10 @@ def _L():
                                          ctypes.POINTER(_Buf), ctypes.POINTER(ctypes.c_int)]
         lib.mib_decode_batch.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.POINTER(_Buf),
                                          ctypes.POINTER(ctypes.c_int)]
+        lib.mib_encode_batch_n.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.POINTER(_Opts), ctypes.c_int,
+                                           ctypes.POINTER(_Buf), ctypes.POINTER(ctypes.c_int)]
+        lib.mib_decode_batch_n.argtypes = [ctypes.POINTER(_Span), ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(_Buf),
+                                           ctypes.POINTER(ctypes.c_int)]
         lib.mib_ctx_new.argtypes = [ctypes.c_int]
         lib.mib_ctx_new.restype = ctypes.c_void_p
         lib.mib_ctx_free.argtypes = [ctypes.c_void_p]
@@ -234,14 +238,18 @@ def brotliDecode(buffer, options=None):
     return _take(buf)
 
 
-def encode_batch(buffers, options=None):
-    """Encode independent buffers in one GPU launch sequence; returns list of bytes."""
+def encode_batch(buffers, options=None, gpus=None):
+    """Encode independent buffers in one GPU launch sequence; returns list of bytes.  gpus:
+    shard the batch over that many GPUs (0: every visible one; mib_encode_batch_n)."""
     k = len(buffers)
     keep = [_bytes(b) for b in buffers]
     spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
     outs = (_Buf * k)()
     st = (ctypes.c_int * k)()
-    rc = _L().mib_encode_batch(spans, k, ctypes.byref(_opts(options)), outs, st)
+    if gpus is None:
+        rc = _L().mib_encode_batch(spans, k, ctypes.byref(_opts(options)), outs, st)
+    else:
+        rc = _L().mib_encode_batch_n(spans, k, ctypes.byref(_opts(options)), int(gpus), outs, st)
     if rc:
         raise _err(rc)
     res = []
@@ -252,14 +260,18 @@ def encode_batch(buffers, options=None):
     return res
 
 
-def decode_batch(buffers):
-    """Decode independent streams on the GPU; returns a list of bytes or BrotliError."""
+def decode_batch(buffers, gpus=None):
+    """Decode independent streams on the GPU; returns a list of bytes or BrotliError.  gpus:
+    shard the batch over that many GPUs (0: every visible one; mib_decode_batch_n)."""
     k = len(buffers)
     keep = [_bytes(b) for b in buffers]
     spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
     outs = (_Buf * k)()
     st = (ctypes.c_int * k)()
-    rc = _L().mib_decode_batch(spans, k, outs, st)
+    if gpus is None:
+        rc = _L().mib_decode_batch(spans, k, outs, st)
+    else:
+        rc = _L().mib_decode_batch_n(spans, k, int(gpus), outs, st)
     if rc:
         raise _err(rc)
     return [(_take(outs[i]) if st[i] == 0 else _err(st[i])) for i in range(k)]

@@ -99,6 +99,13 @@ int mib_encoder_update_batch(mib_encoder *const *e, const mib_span *in, size_t k
 /* Batches of independent buffers in host memory; one result (and status) per buffer. */
 int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_buf *out, int *status);
 int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status);
+/* The same batches sharded over GPUs (SURVEY.md §8(b),(e)): n_gpus shards (<= 0: one per
+ * visible device), size-balanced, one host thread and context per shard, shard s on device
+ * s % device count; results in input order.  Safe from several threads (calls serialise). */
+int mib_encode_batch_n(const mib_span *in, size_t k, const mib_enc_opts *o, int n_gpus, mib_buf *out, int *status);
+int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, int *status);
+/* Visible HIP devices (0 without a GPU). */
+int mib_device_count(void);
 
 void mib_buf_free(mib_buf *b);
 

@@ -134,7 +134,22 @@ const bufs = []
 for (let i = 0; i < 32; i++) bufs.push(new Uint8Array(text.subarray(i * 1000, i * 1000 + 5000 + i)))
 const outs = lib.brotliEncodeBatch(bufs, { quality: 11 })
 for (let i = 0; i < bufs.length; i++) eq(lib.brotliDecode(outs[i]), bufs[i], 'batch ' + i)
+// sharded over GPUs (options.gpus; two shards on a one-GPU host share its device): same streams
+const souts = lib.brotliEncodeBatch(bufs, { quality: 11, gpus: 2 })
+for (let i = 0; i < bufs.length; i++) eq(souts[i], outs[i], 'sharded batch ' + i)
 console.log('batch ok')
+
+// customDictionary on the encoder (the decoder side's option): tail copies, same dictionary back
+{
+  const dict = new Uint8Array(text.subarray(0, 3000))
+  const input = new Uint8Array(Buffer.concat([Buffer.from(dict.subarray(2900)), Buffer.from(text.subarray(50000, 60000))]))
+  const e = lib.brotliEncode(input, { customDictionary: dict })
+  eq(lib.brotliDecode(e, { customDictionary: dict }), input, 'encoder customDictionary')
+  const se = new lib.BrotliEncoder({ quality: 9, customDictionary: new Int8Array(dict.buffer, dict.byteOffset, dict.length) })
+  const st = Buffer.concat([Buffer.from(se.update(input)), Buffer.from(se.finish())])
+  eq(lib.brotliDecode(new Uint8Array(st), { customDictionary: dict }), input, 'BrotliEncoder customDictionary')
+  console.log('encoder dictionary ok')
+}
 
 // WOFF2 transforms of the reference's TrueType bench font, against the fontTools goldens
 {
@@ -158,7 +173,7 @@ console.log('batch ok')
   const aouts = await lib.brotliEncodeBatchAsync(bufs, { quality: 11 })
   for (let i = 0; i < bufs.length; i++) eq(aouts[i], outs[i], 'async batch ' + i)
   const bad = new Uint8Array([0x1b, 0x3f, 0xff, 0xff])
-  const decs = await lib.brotliDecodeBatchAsync([...aouts, bad])
+  const decs = await lib.brotliDecodeBatchAsync([...aouts, bad], { gpus: 2 })
   clearInterval(timer)
   for (let i = 0; i < bufs.length; i++) eq(decs[i], bufs[i], 'async decode ' + i)
   assert.ok(decs[bufs.length] instanceof Error, 'a bad stream gives its Error')
