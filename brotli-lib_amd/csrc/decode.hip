@@ -2402,13 +2402,15 @@ struct LdsPlan {
 };
 LdsPlan decode_lds_plan(int per_cu) {
   per_cu = per_cu < 1 ? 1 : per_cu > 4 ? 4 : per_cu;
-  const size_t stat = sizeof(mib::Lds) + sizeof(mib::Dec) + 256;   // (+ alignment slack)
+  // (the kernels' static LDS is 14,008 bytes; 2 KiB of margin for the allocation granule and
+  // the dynamic area's alignment: four waves per CU must fit, or the launch runs three)
+  const size_t stat = sizeof(mib::Lds) + sizeof(mib::Dec) + 2048;
   size_t budget = (size_t)mib::kLdsPerCu / per_cu - stat;
   LdsPlan p;
   p.bt_lds = per_cu == 1;
   if (p.bt_lds) budget -= (mib::kBlockTreesCap + 1) * 4;
-  p.cap = (int)(budget / 2) & ~63;
-  if (p.cap < mib::kLdsTab) p.cap = mib::kLdsTab;
+  p.cap = (int)(budget / 2) & ~255;
+  if (per_cu >= 4 || p.cap < mib::kLdsTab) p.cap = mib::kLdsTab;   // four per CU: the measured layout
   p.dyn = (size_t)p.cap * 2 + (p.bt_lds ? (mib::kBlockTreesCap + 1) * 4 : 0);
   return p;
 }
