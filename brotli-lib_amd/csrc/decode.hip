@@ -142,7 +142,11 @@ constexpr uint64_t kPartFailed = ~0ull;   // a part's progress word when it fail
 // One stream per workgroup (one wave): the LDS working set lives at file scope, so the hot
 // loop addresses it with constant offsets instead of pointer registers.
 __shared__ Lds g_lds;
+#ifdef MIB_STATIC_LTAB   // experiment: the fixed table area of round 2 (no launch-sized LDS)
+__shared__ uint16_t g_ltab[kLdsTab];
+#else
 extern __shared__ uint16_t g_ltab[];   // tab_cap entries (+ the block-type trees when they fit)
+#endif
 __shared__ Dec g_dec;   // the decoder state: LDS, so that it is wave-uniform and never waits on HBM stores
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
@@ -2411,7 +2415,14 @@ LdsPlan decode_lds_plan(int per_cu) {
   if (p.bt_lds) budget -= (mib::kBlockTreesCap + 1) * 4;
   p.cap = (int)(budget / 2) & ~255;
   if (per_cu >= 4 || p.cap < mib::kLdsTab) p.cap = mib::kLdsTab;   // four per CU: the measured layout
+#ifdef MIB_STATIC_LTAB
+  p.cap = mib::kLdsTab;
+  p.bt_lds = 0;
+#endif
   p.dyn = (size_t)p.cap * 2 + (p.bt_lds ? (mib::kBlockTreesCap + 1) * 4 : 0);
+#ifdef MIB_STATIC_LTAB
+  p.dyn = 0;
+#endif
   return p;
 }
 template <class K>
