@@ -6,7 +6,8 @@ resident in HBM when the timed region starts):
   c4 (default)  C4 per-GPU shard: 1024 independent 1 MiB enwik-style text buffers per GPU,
                 q11, lgwin 22, GENERIC -- the configuration the metric's 1/2/4/8-GPU
                 numbers are quoted on.
-  c3            C3: 1024 x 256 KiB WOFF2-transformed-glyf-like buffers per GPU, q11, FONT.
+  c3            C3: 1024 x 256 KiB WOFF2-transformed glyf tables per GPU (glyph sets drawn from
+                the reference's Inter bench font, jittered per seed), q11, FONT.
   c2            C2: one 64 MiB enwik-style buffer, q11 GENERIC (one stream: replicas at N > 1).
   c5            C5's shape per GPU: one stream streamed through BrotliEncoder.update() in 1 MiB
                 chunks (history window carried on the device), q9 lgwin 24 TEXT, then decoded
@@ -103,10 +104,9 @@ def make_inputs(wl, k, size, rank, dev):
     if gen == 'enwik':
         # one device-generated text, cut into k buffers (seed per rank)
         return datagen.enwik_device(k * size, seed0 + rank * 7919, dev)
-    from concurrent.futures import ProcessPoolExecutor
-    seeds = [seed0 + rank * k + i for i in range(k)]
-    with ProcessPoolExecutor(max(1, min(16, cpu_share()))) as ex:
-        bufs = list(ex.map(datagen.glyf_stream, [size] * k, seeds, chunksize=16))
+    # C3: WOFF2-transformed glyf tables of glyph sets drawn from the reference's Inter bench
+    # font, jittered per seed (the GPU's own glyf transform, §8 f4)
+    bufs = datagen.glyf_font_batch(k, size, seed0 + rank * k, workers=max(1, min(16, cpu_share())))
     host = np.frombuffer(b''.join(bufs), dtype=np.uint8)
     return torch.from_numpy(host.copy()).to(dev)
 
@@ -547,7 +547,7 @@ def main():
             s_out = torch.empty(s_cap, dtype=torch.uint8, device=dev)
             s_off = ctx.encode(s_in.data_ptr(), [i * piece for i in range(nsamp + 1)], s_out.data_ptr(), s_cap, opts)
             samp_gpu = [s_off[i + 1] - s_off[i] for i in range(nsamp)]
-        what = {'enwik': 'enwik-style text', 'glyf': 'WOFF2-glyf-like streams'}[gen]
+        what = {'enwik': 'enwik-style text', 'glyf': 'WOFF2-transformed glyf tables'}[gen]
         cpu, ratios = cpu_baseline(sample, samp_gpu, args, mode, what)
 
     if rank == 0:
@@ -563,7 +563,7 @@ def main():
         avg_ms = dom_ms / max(1, dom_n)
         achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
         desc = {'c4': 'C4 per-GPU shard: %d x %d B enwik-style text, q%d lgwin%d GENERIC',
-                'c3': 'C3: %d x %d B WOFF2-glyf-like streams, q%d lgwin%d FONT',
+                'c3': 'C3: %d x %d B WOFF2-transformed glyf tables (glyph sets from the reference\'s Inter font, jittered per seed), q%d lgwin%d FONT',
                 'c2': 'C2: %d x %d B enwik-style text (one stream), q%d lgwin%d GENERIC'}[wl] % (
                     k, size, args.quality, args.lgwin)
         res = {

@@ -296,3 +296,205 @@ def enwik_device(total, seed, device):
         out[have:have + take] = flat_t[idx[:take]]
         have += take
     return out
+
+
+# ---------------------------------------------------------------------------- C3 from a real font
+# C3's buffers are WOFF2-transformed glyf tables whose parameters come from the
+# reference's Inter bench font (bench/fixtures/enc-ttf.bin, kept in tests/golden/bench), perturbed
+# per seed.  glyf_font(seed) builds a TrueType glyph set from the font's glyphs -- drawn at random
+# with replacement, each simple glyph's points jittered by a few font units -- and
+# glyf_font_stream() runs the WOFF2 glyf transform on it (the GPU's, woff2_transform_glyf: the
+# FONT-mode producer of §8 f4) and cuts the transformed table to the buffer size.
+_FONT = None
+_BENCH = os.path.join(os.path.dirname(os.path.dirname(_DATA)), 'tests', 'golden', 'bench')
+
+
+def _sfnt_tables(font):
+    import struct
+    n = struct.unpack('>H', font[4:6])[0]
+    out = {}
+    for i in range(n):
+        tag, _, off, ln = struct.unpack('>4sIII', font[12 + 16 * i:28 + 16 * i])
+        out[tag.decode('latin-1')] = font[off:off + ln]
+    return out
+
+
+def _font_glyphs():
+    """the bench font's glyphs: ('s', contour ends, instructions, on-curve flags, xs, ys) per
+    simple glyph, ('c', raw bytes) per composite one, None for an empty one"""
+    global _FONT
+    if _FONT is not None:
+        return _FONT
+    import struct
+    with open(os.path.join(_BENCH, 'enc-ttf.bin'), 'rb') as f:
+        font = f.read()
+    t = _sfnt_tables(font)
+    long_loca = struct.unpack('>h', t['head'][50:52])[0] == 1
+    ng = struct.unpack('>H', t['maxp'][4:6])[0]
+    loca = (struct.unpack('>%dI' % (ng + 1), t['loca'][:4 * (ng + 1)]) if long_loca else
+            tuple(2 * v for v in struct.unpack('>%dH' % (ng + 1), t['loca'][:2 * (ng + 1)])))
+    glyf = t['glyf']
+    gl = []
+    for g in range(ng):
+        b = glyf[loca[g]:loca[g + 1]]
+        if not b:
+            gl.append(None)
+            continue
+        nc = struct.unpack('>h', b[:2])[0]
+        if nc < 0:
+            gl.append(('c', bytes(b)))
+            continue
+        raw = bytes(b)
+        ends = struct.unpack('>%dH' % nc, b[10:10 + 2 * nc])
+        p = 10 + 2 * nc
+        il = struct.unpack('>H', b[p:p + 2])[0]
+        instr = bytes(b[p + 2:p + 2 + il])
+        p += 2 + il
+        npts = ends[-1] + 1 if nc else 0
+        flags = []
+        while len(flags) < npts:
+            f = b[p]
+            p += 1
+            flags.append(f)
+            if f & 8:
+                flags += [f] * b[p]
+                p += 1
+        coords = []
+        for short, same in ((2, 16), (4, 32)):
+            v, vals = 0, []
+            for f in flags:
+                if f & short:
+                    d = b[p]
+                    p += 1
+                    v += d if f & same else -d
+                elif not f & same:
+                    v += struct.unpack('>h', b[p:p + 2])[0]
+                    p += 2
+                vals.append(v)
+            coords.append(vals)
+        gl.append(('s', ends, instr, [f & 1 for f in flags], coords[0], coords[1], raw))
+    _FONT = gl
+    return gl
+
+
+def _encode_simple(ends, instr, on, xs, ys):
+    """a TrueType simple glyph (flags with repeats, short / same coordinates, bbox recomputed)"""
+    import struct
+    flags, xb, yb = [], bytearray(), bytearray()
+    px = py = 0
+    for o, x, y in zip(on, xs, ys):
+        f = o
+        for d, short, same, buf in ((x - px, 2, 16, xb), (y - py, 4, 32, yb)):
+            if d == 0:
+                f |= same
+            elif -256 < d < 256:
+                f |= short | (same if d > 0 else 0)
+                buf.append(abs(d))
+            else:
+                buf += struct.pack('>h', d)
+        flags.append(f)
+        px, py = x, y
+    fb = bytearray()
+    i = 0
+    while i < len(flags):
+        r = 1
+        while i + r < len(flags) and flags[i + r] == flags[i] and r < 256:
+            r += 1
+        if r > 1:
+            fb += bytes([flags[i] | 8, r - 1])
+        else:
+            fb.append(flags[i])
+        i += r
+    hdr = struct.pack('>hhhhh', len(ends), min(xs), min(ys), max(xs), max(ys))
+    return hdr + struct.pack('>%dH' % len(ends), *ends) + struct.pack('>H', len(instr)) + instr + bytes(fb) + bytes(xb) + bytes(yb)
+
+
+def _remap_composite(b, ng, rng):
+    """a composite glyph whose components point at glyphs of the new set"""
+    import struct
+    b = bytearray(b)
+    p = 10
+    while True:
+        fl = struct.unpack('>H', b[p:p + 2])[0]
+        b[p + 2:p + 4] = struct.pack('>H', int(rng.integers(0, ng)))
+        p += 4 + (4 if fl & 1 else 2)
+        p += 2 if fl & 8 else 4 if fl & 0x40 else 8 if fl & 0x80 else 0
+        if not fl & 0x20:
+            return bytes(b)
+
+
+def glyf_font(seed, nglyphs=3000, jitter=0.35):
+    """a TrueType font (head, maxp, loca, glyf) of `nglyphs` glyphs drawn from the bench font
+    with replacement; a `jitter` share of the simple glyphs get 30 % of their points moved by
+    up to 3 font units (seed-determined), the others are the font's own bytes"""
+    import struct
+    src = _font_glyphs()
+    rng = np.random.default_rng(0x6F00000 + seed)
+    out = []
+    for g in rng.integers(0, len(src), size=nglyphs):
+        s = src[int(g)]
+        if s is None:
+            out.append(b'')
+        elif s[0] == 'c':
+            out.append(_remap_composite(s[1], nglyphs, rng))
+        elif rng.random() >= jitter:
+            out.append(s[6])
+        else:
+            _, ends, instr, on, xs, ys, _ = s
+            n = len(xs)
+            j = rng.random(n) < 0.3
+            dx = np.where(j, rng.integers(-3, 4, size=n), 0)
+            dy = np.where(j, rng.integers(-3, 4, size=n), 0)
+            out.append(_encode_simple(ends, instr, on, [int(v) for v in np.asarray(xs) + dx], [int(v) for v in np.asarray(ys) + dy]))
+    out = [g + b'\0' * (-len(g) & 3) for g in out]   # 4-byte aligned glyphs
+    loca = [0]
+    for g in out:
+        loca.append(loca[-1] + len(g))
+    tabs = _sfnt_tables(open(os.path.join(_BENCH, 'enc-ttf.bin'), 'rb').read())
+    head = bytearray(tabs['head'])
+    head[50:52] = struct.pack('>h', 1)   # long loca
+    maxp = bytearray(tabs['maxp'])
+    maxp[4:6] = struct.pack('>H', nglyphs)
+    tables = {'glyf': b''.join(out), 'head': bytes(head), 'loca': struct.pack('>%dI' % len(loca), *loca), 'maxp': bytes(maxp)}
+    tags = sorted(tables)
+    off = 12 + 16 * len(tags)
+    dirs, body = b'', b''
+    for t in tags:
+        data = tables[t]
+        dirs += struct.pack('>4sIII', t.encode(), 0, off + len(body), len(data))
+        body += data + b'\0' * (-len(data) & 3)
+    return struct.pack('>IHHHH', 0x00010000, len(tags), 64, 2, 0) + dirs + body
+
+
+def glyf_font_stream(length, seed, transform=None):
+    """C3's buffer: the WOFF2-transformed glyf table of glyf_font(seed), cut to `length` bytes
+    (transform: the glyf transform to use; default the GPU's)"""
+    if transform is None:
+        from brotli_amd import woff2_transform_glyf as transform
+    n = 5600
+    while True:
+        t = transform(glyf_font(seed, n))
+        if len(t) >= length:
+            return t[:length]
+        n = int(n * (length / max(1, len(t))) * 1.1) + 64
+
+
+def _font_job(a):
+    seed, n = a
+    return glyf_font(seed, n)
+
+
+def glyf_font_batch(count, length, seed0, workers=8, transform=None):
+    """C3's batch: glyf_font_stream(length, seed0 + i) for i < count; the fonts are built on
+    `workers` processes, the transforms run here (on the GPU by default)"""
+    from concurrent.futures import ProcessPoolExecutor
+    if transform is None:
+        from brotli_amd import woff2_transform_glyf as transform
+    seeds = [seed0 + i for i in range(count)]
+    with ProcessPoolExecutor(max(1, workers)) as ex:
+        fonts = list(ex.map(_font_job, [(s, 5600) for s in seeds], chunksize=8))
+    out = []
+    for s, f in zip(seeds, fonts):
+        t = transform(f)
+        out.append(t[:length] if len(t) >= length else glyf_font_stream(length, s, transform))
+    return out

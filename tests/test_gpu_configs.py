@@ -4,15 +4,14 @@ C2: one 64 MiB (67,108,864 B) enwik-style buffer, q11 GENERIC lgwin 22, encoded 
     and decoded by the HIP decoder AND by the oracle (the reference decoder restated), both
     bit-exact at the full size; plus the reference-encoded (oracle) stream of a golden-sized
     prefix decoded on the GPU.
-C3: 1024 x 262,144 B WOFF2-transformed-glyf-like buffers (seeds 1000+i), q11 FONT, through
+C3: 1024 x 262,144 B WOFF2-transformed glyf tables (glyph sets from the reference's Inter
+    font, jittered per seed 1000+i; datagen.glyf_font_batch), q11 FONT, through
     encode_batch and the device-resident context; every stream decoded by the HIP decoder,
     a sample by the oracle.
 C4: the per-GPU shard, 1024 x 1 MiB enwik-style buffers, q11: every stream HIP-decoded, 16 by
     the oracle.  (C5 at full size: tests/test_gpu_custom_dict.py.)
 Plus: a context on the last visible device round-trips (per-device decoder tables).
 """
-from concurrent.futures import ProcessPoolExecutor
-
 import pytest
 
 import _oracle
@@ -41,8 +40,7 @@ def test_c2_single_64mib_stream_q11():
 
 def test_c3_glyf_batch_font_mode():
     k, n = 1024, 262144
-    with ProcessPoolExecutor(8) as ex:
-        bufs = list(ex.map(datagen.glyf_stream, [n] * k, [1000 + i for i in range(k)], chunksize=32))
+    bufs = datagen.glyf_font_batch(k, n, 1000, workers=8)
     outs = brotli_amd.encode_batch(bufs, {'quality': 11, 'mode': brotli_amd.EncoderMode.FONT})
     dec = brotli_amd.decode_batch(outs)
     bad = [i for i in range(k) if dec[i] != bufs[i]]
@@ -86,7 +84,7 @@ def test_c4_per_gpu_shard_1024x1mib_q11():
 def test_c3_device_context_matches_batch():
     torch = pytest.importorskip('torch')
     k, n = 64, 262144
-    bufs = [datagen.glyf_stream(n, 1000 + i) for i in range(k)]
+    bufs = datagen.glyf_font_batch(k, n, 1000, workers=8)
     opts = {'quality': 11, 'mode': 2}
     host = brotli_amd.encode_batch(bufs, opts)
     dev = torch.device('cuda', 0)
