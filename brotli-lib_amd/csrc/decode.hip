@@ -52,14 +52,17 @@ enum : int {
 
 constexpr int kBlockTreesCap = 3091;   // engine.ts:163 Int32Array(3091)
 
-// LDS working set of one stream (one wave): the static part below (~14 KiB) plus a
-// launch-sized table area (dynamic LDS, g_ltab): 40 KiB in all when a batch puts 4 streams on
-// a CU; a call with few streams gives each its CU's whole LDS (decode_lds_plan), so a
-// foreign stream's large prefix-code set (native brotli's q11 fonts: 142 literal codes in a
-// metablock) and its block-type trees stay in LDS too.  A metablock's tables are built in HBM
-// scratch (packed, exact sizes) and, when they fit, copied into the table area as 16-bit
-// entries (nbits << 12 | symbol-or-subtable-offset), tree roots resolved to absolute indices.
-constexpr int kLdsTab = 12224;   // the smallest table area a launch gets (4 streams per CU)
+// LDS working set of one stream (one wave): the state below (~14 KiB) plus a table area
+// declared by the kernel itself: 12,224 entries in the batch build (40 KiB per stream, four
+// streams per CU), 68,096 in the one-per-CU build a call with few streams gets, which also
+// keeps the block-type trees in LDS -- so a foreign stream's large prefix-code set (native
+// brotli's q11 fonts: 142 literal codes in a metablock) stays in LDS.  (The table area is
+// static in both builds: a dynamically sized one made the batch decode 14 % slower, 179 vs
+// 157 ms on C4.)  A metablock's tables are built in HBM scratch (packed, exact sizes) and,
+// when they fit, copied into the table area as 16-bit entries (nbits << 12 |
+// symbol-or-subtable-offset), tree roots resolved to absolute indices.
+constexpr int kLdsTab = 12224;   // the batch build's table area (4 streams per CU)
+constexpr int kLdsTabBig = 68096;   // the one-stream-per-CU build's
 
 typedef __attribute__((address_space(1))) uint8_t GU8;          // HBM
 typedef const __attribute__((address_space(1))) int32_t GI32;
@@ -96,9 +99,9 @@ struct Dec {
   int rings[10], dist_rb_idx;
   int32_t *lit_group, *cmd_group, *dist_group;   // HBM scratch, packed
   int32_t *tab_hbm;
-  uint16_t *tab_lds;       // the 16-bit copy of the tables
+  uint16_t *tab_lds;       // the 16-bit copy of the tables: the kernel's table area
   int tab16, cmd_base, dist_base;   // tables in LDS; where the command / distance groups start there
-  int tab_cap;             // entries of the launch's LDS table area
+  int tab_cap;             // entries of the kernel's LDS table area
   int32_t *bt;             // block-type and block-count trees (HBM scratch, cold)
   uint8_t *ring_scratch;   // the block's HBM ring
   int direct;              // ring == out: a single-metablock stream decodes in place
@@ -136,17 +139,13 @@ struct Dec {
 typedef __attribute__((address_space(3))) Dec DecS;
 #define LANE ((int)threadIdx.x)
 static_assert(sizeof(Lds) + sizeof(Dec) + 2 * kLdsTab <= 163840 / 4, "four streams per CU");
-constexpr int kLdsPerCu = 163840;
+static_assert(sizeof(Lds) + sizeof(Dec) + 2 * kLdsTabBig + 4 * (kBlockTreesCap + 1) <= 163840 - 1024, "one stream per CU");
 constexpr uint64_t kPartFailed = ~0ull;   // a part's progress word when it failed
 
 // One stream per workgroup (one wave): the LDS working set lives at file scope, so the hot
 // loop addresses it with constant offsets instead of pointer registers.
 __shared__ Lds g_lds;
-#ifdef MIB_STATIC_LTAB   // experiment: the fixed table area of round 2 (no launch-sized LDS)
-__shared__ uint16_t g_ltab[kLdsTab];
-#else
-extern __shared__ uint16_t g_ltab[];   // tab_cap entries (+ the block-type trees when they fit)
-#endif
+
 __shared__ Dec g_dec;   // the decoder state: LDS, so that it is wave-uniform and never waits on HBM stores
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
@@ -1094,7 +1093,7 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
         LI32 *ctb = (LI32 *)g_lds.ctx_tree_base;
         const int ring_cap = s.ring_cap, npostfix = s.npostfix, ndirect = s.ndirect, max_back = s.max_back;
         constexpr bool tab_lds = kTabLds;   // prefix-code tables in LDS (16-bit) or HBM
-        LU16 *t16 = (LU16 *)g_ltab;
+        LU16 *t16 = (LU16 *)s.tab_lds;
         LU16 *croot = (LU16 *)g_lds.ctx_root;
         const int cmd_base = __builtin_amdgcn_readfirstlane(s.cmd_base), dist_base = __builtin_amdgcn_readfirstlane(s.dist_base);
         GI32 *cmd_h = (GI32 *)s.cmd_group, *dist_h = (GI32 *)s.dist_group, *lit_h = (GI32 *)s.lit_group;
@@ -1635,7 +1634,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   DecS &s = *(DecS *)&g_dec;
   GU8 *ring = (GU8 *)s.ring;
   LU16 *win16 = (LU16 *)g_lds.win;
-  LU16 *t16 = (LU16 *)g_ltab;
+  LU16 *t16 = (LU16 *)s.tab_lds;
   typedef const __attribute__((address_space(3))) uint64_t LU64;
   LU64 *croot64 = (LU64 *)g_lds.ctx_root;
   LU8 *lut1 = (LU8 *)g_lds.ctx_lut + 256;
@@ -2133,7 +2132,7 @@ __device__ __forceinline__ int decompress(DecS &s, int8_t *dist_extra, int32_t *
 
 // A fresh decoder state for one job (initState, engine.ts:160-178), in LDS.
 __device__ void dec_init(DecS &s, const DecJob &job, uint8_t *ring, int32_t *tables, uint8_t *ctx, int32_t *block_trees,
-                         int tab_cap) {
+                         uint16_t *tab, int tab_cap) {
   const int lane = LANE;
     s.l = &g_lds;
   s.in = job.in;
@@ -2164,7 +2163,7 @@ __device__ void dec_init(DecS &s, const DecJob &job, uint8_t *ring, int32_t *tab
   s.dist_rb_idx = 3;
   s.ring_scratch = ring;
   s.direct = 0;
-  s.tab_lds = g_ltab;
+  s.tab_lds = tab;
   s.tab_cap = tab_cap;
   s.tab16 = s.cmd_base = s.dist_base = 0;
   s.bt = block_trees;
@@ -2215,9 +2214,13 @@ __device__ void dec_init(DecS &s, const DecJob &job, uint8_t *ring, int32_t *tab
 
 // Persistent grid: block b decodes jobs b, b + grid, ...  Scratch per block:
 //   [ring: ring_bytes][tables: kDecodeTableInts int32][ctx maps: kDecodeCtxBytes][dist luts]
+// BIG: the one-stream-per-CU build (kLdsTabBig table entries, block-type trees in LDS)
+template <bool BIG>
 __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int njobs, uint8_t *scratch,
-                                                            uint64_t per_block, uint64_t ring_bytes, int tab_cap,
-                                                            int bt_lds) {
+                                                            uint64_t per_block, uint64_t ring_bytes) {
+  constexpr int tab_cap = BIG ? kLdsTabBig : kLdsTab;
+  __shared__ uint16_t tab[tab_cap];
+  __shared__ int32_t bt_lds[BIG ? kBlockTreesCap + 1 : 1];
   uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
   uint8_t *ring = base;
   int32_t *tables = reinterpret_cast<int32_t *>(base + ring_bytes);
@@ -2226,12 +2229,12 @@ __global__ __launch_bounds__(64) void decode_streams_kernel(DecJob *jobs, int nj
   int32_t *dist_offset = reinterpret_cast<int32_t *>(dist_extra + 1152);
   int32_t *ctxmap_table = dist_offset + 1152;
   // the block-type trees: after the table area when the launch gave room for them
-  int32_t *block_trees = bt_lds ? reinterpret_cast<int32_t *>(g_ltab + tab_cap) : ctxmap_table + 1100;
+  int32_t *block_trees = BIG ? bt_lds : ctxmap_table + 1100;
   const int lane = threadIdx.x;
   for (int jb = blockIdx.x; jb < njobs; jb += gridDim.x) {
     DecJob job = jobs[jb];
     DecS &s = *(DecS *)&g_dec;
-    dec_init(s, job, ring, tables, ctx, block_trees, tab_cap);
+    dec_init(s, job, ring, tables, ctx, block_trees, tab, tab_cap);
     int rc = prepare(s);
     if (rc >= 0) {
       s.running = ST_INITED;
@@ -2360,15 +2363,19 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
 
 // Parts are taken in order from a ticket counter, so every part a wave may wait on has
 // already been taken by a running wave: a part only waits on earlier parts of its stream.
+template <bool BIG>
 __global__ __launch_bounds__(64) void decode_parts_kernel(DecJob *jobs, int njobs, uint8_t *scratch, uint64_t per_block,
-                                                          unsigned *ticket, int tab_cap, int bt_lds) {
+                                                          unsigned *ticket) {
+  constexpr int tab_cap = BIG ? kLdsTabBig : kLdsTab;
+  __shared__ uint16_t tab[tab_cap];
+  __shared__ int32_t bt_lds[BIG ? kBlockTreesCap + 1 : 1];
   uint8_t *base = scratch + (uint64_t)blockIdx.x * per_block;
   int32_t *tables = reinterpret_cast<int32_t *>(base);
   uint8_t *ctx = reinterpret_cast<uint8_t *>(tables + kDecodeTableInts);
   int8_t *dist_extra = reinterpret_cast<int8_t *>(ctx + kDecodeCtxBytes);
   int32_t *dist_offset = reinterpret_cast<int32_t *>(dist_extra + 1152);
   int32_t *ctxmap_table = dist_offset + 1152;
-  int32_t *block_trees = bt_lds ? reinterpret_cast<int32_t *>(g_ltab + tab_cap) : ctxmap_table + 1100;
+  int32_t *block_trees = BIG ? bt_lds : ctxmap_table + 1100;
   const int lane = threadIdx.x;
   for (;;) {
     int jb = 0;
@@ -2377,7 +2384,7 @@ __global__ __launch_bounds__(64) void decode_parts_kernel(DecJob *jobs, int njob
     if (jb >= njobs) break;
     const DecJob job = jobs[jb];
     DecS &s = *(DecS *)&g_dec;
-    dec_init(s, job, job.out, tables, ctx, block_trees, tab_cap);
+    dec_init(s, job, job.out, tables, ctx, block_trees, tab, tab_cap);
     int rc = part_run(s, job, dist_extra, dist_offset, ctxmap_table);
     if (rc == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2396,60 +2403,27 @@ __global__ __launch_bounds__(64) void decode_parts_kernel(DecJob *jobs, int njob
 
 }  // namespace mib
 
-// The LDS plan of a decode launch with `per_cu` streams (waves) per CU: the table area
-// (entries) and whether the block-type trees move into LDS after it.  One stream per CU gets
-// the CU's whole LDS: ~66K table entries and the trees.
-namespace {
-struct LdsPlan {
-  int cap, bt_lds;
-  size_t dyn;
-};
-LdsPlan decode_lds_plan(int per_cu) {
-  per_cu = per_cu < 1 ? 1 : per_cu > 4 ? 4 : per_cu;
-  // (the kernels' static LDS is 14,008 bytes; 2 KiB of margin for the allocation granule and
-  // the dynamic area's alignment: four waves per CU must fit, or the launch runs three)
-  const size_t stat = sizeof(mib::Lds) + sizeof(mib::Dec) + 2048;
-  size_t budget = (size_t)mib::kLdsPerCu / per_cu - stat;
-  LdsPlan p;
-  p.bt_lds = per_cu == 1;
-  if (p.bt_lds) budget -= (mib::kBlockTreesCap + 1) * 4;
-  p.cap = (int)(budget / 2) & ~255;
-  if (per_cu >= 4 || p.cap < mib::kLdsTab) p.cap = mib::kLdsTab;   // four per CU: the measured layout
-#ifdef MIB_STATIC_LTAB
-  p.cap = mib::kLdsTab;
-  p.bt_lds = 0;
-#endif
-  p.dyn = (size_t)p.cap * 2 + (p.bt_lds ? (mib::kBlockTreesCap + 1) * 4 : 0);
-#ifdef MIB_STATIC_LTAB
-  p.dyn = 0;
-#endif
-  return p;
-}
-template <class K>
-hipError_t allow_dyn_lds(K kernel) {   // dynamic LDS above the default limit needs an opt-in (once)
-  static hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            (int)decode_lds_plan(1).dyn);
-  return e;
-}
-}  // namespace
-
+// A launch with at most one stream (or part) per CU runs the build that gives each its CU's
+// whole LDS; a larger one the four-per-CU build.
 extern "C" hipError_t mib_decode_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
                                         uint64_t ring_bytes, int grid, int per_cu, hipStream_t stream) {
-  const LdsPlan p = decode_lds_plan(per_cu);
-  hipError_t e = allow_dyn_lds(mib::decode_streams_kernel);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mib::decode_streams_kernel, dim3(grid), dim3(64), p.dyn, stream, d_jobs, njobs, d_scratch, per_block,
-                     ring_bytes, p.cap, p.bt_lds);
+  if (per_cu <= 1)
+    hipLaunchKernelGGL(mib::decode_streams_kernel<true>, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block,
+                       ring_bytes);
+  else
+    hipLaunchKernelGGL(mib::decode_streams_kernel<false>, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block,
+                       ring_bytes);
   return hipGetLastError();
 }
 
 extern "C" hipError_t mib_decode_parts_launch(mib::DecJob *d_jobs, int njobs, uint8_t *d_scratch, uint64_t per_block,
                                               unsigned *d_ticket, int grid, int per_cu, hipStream_t stream) {
-  const LdsPlan p = decode_lds_plan(per_cu);
-  hipError_t e = allow_dyn_lds(mib::decode_parts_kernel);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(mib::decode_parts_kernel, dim3(grid), dim3(64), p.dyn, stream, d_jobs, njobs, d_scratch, per_block, d_ticket,
-                     p.cap, p.bt_lds);
+  if (per_cu <= 1)
+    hipLaunchKernelGGL(mib::decode_parts_kernel<true>, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block,
+                       d_ticket);
+  else
+    hipLaunchKernelGGL(mib::decode_parts_kernel<false>, dim3(grid), dim3(64), 0, stream, d_jobs, njobs, d_scratch, per_block,
+                       d_ticket);
   return hipGetLastError();
 }
 
