@@ -283,12 +283,12 @@ __device__ __forceinline__ uint32_t part_cap(uint32_t A, uint32_t d, uint32_t bi
 __device__ __forceinline__ uint32_t load_u32(const uint8_t *p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
-__device__ __forceinline__ uint32_t hash4(const uint8_t *p) { return (load_u32(p) * 0x1E35A7BDu) >> 15; }
-// Bucket key over the first n bytes at p (n = kHashBytes; MIB_HASH_BYTES overrides, 4..7).
-// The candidate walk is depth-limited (64 at q11), so a longer key makes every candidate a
-// match of >= n bytes and lets the walk reach farther back: C4 0.3770 -> 0.3706 and
-// find_matches 75 -> 59 ms for 6 bytes (4: the reference's hashBytes4, match.ts:162-172;
-// 7: 0.3749); matches of 4-5 bytes are given up (fonts: +0.04 %).
+// Bucket key over the first n bytes at p (n = kHashBytes, 4 in FONT mode: encode.hip
+// hash_bytes; MIB_HASH_BYTES overrides, 4..6).  The candidate walk is depth-limited (64 at
+// q11), so a longer key makes every candidate a match of >= n bytes and lets the walk reach
+// farther back: C4 0.3770 -> 0.3706 and find_matches 75 -> 59 ms for 6 bytes (4: the
+// reference's hashBytes4, match.ts:162-172); matches of 4-5 bytes are given up, which costs
+// glyph data 1.8 %.
 __device__ __forceinline__ uint32_t hashn(const uint8_t *p, int n) {
   uint64_t v = load_u32(p);
   for (int i = 4; i < n; i++) v |= (uint64_t)p[i] << (8 * i);
@@ -429,8 +429,6 @@ struct ItemMap {
 };
 
 // ---------------------------------------------------------------- kernel launchers (host)
-void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
-                      uint32_t *vals);
 void launch_dict_matches(hipStream_t st, const Job *jobs, int njobs, uint32_t span, const uint32_t *dict_tab,
                          const uint8_t *dict_data, uint32_t *matches);
 void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *matches);
@@ -446,6 +444,9 @@ void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, cons
                const uint32_t *matches, uint64_t *choice, bool cdict);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
+void launch_rep(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const CostModel *model, RawCmd *raw, uint32_t *cnts);
+void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
+                      uint32_t *vals);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h);
 void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes);

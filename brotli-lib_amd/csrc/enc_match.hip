@@ -19,13 +19,13 @@ namespace enc {
 __global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
                                  uint32_t *vals) {
   // four consecutive positions per thread (total is a multiple of the 64 KiB segment): one
-  // 16-byte load covers their 6-byte keys, and keys / values are stored as uint4
+  // 16-byte load covers their (<= 6)-byte keys, and keys / values are stored as uint4
   for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) * 4; g < total; g += gridDim.x * blockDim.x * 4) {
     const uint32_t j = pos_job[g >> kSegBits];
     const Job &jb = jobs[j];
     const uint32_t p = g - jb.pos_base, grp = (j >> gshift) << (kHashBits + 1);
     uint32_t k4[4];
-    if (hb == kHashBytes && !jb.uncompressed && p + 16 <= jb.n) {
+    if (!jb.uncompressed && p + 16 <= jb.n) {
       const uintptr_t a = (uintptr_t)(jb.data + p);
       const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
       const uint32_t sh = (uint32_t)(a & 3);
@@ -35,15 +35,14 @@ __global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint3
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint64_t x = k ? (lo >> (8 * k)) | (hi << (64 - 8 * k)) : lo;
-        const uint64_t v = (x & 0xFFFFFFFFFFFFull) << (64 - 8 * kHashBytes);
+        const uint64_t v = (x & ((1ull << (8 * hb)) - 1)) << (64 - 8 * hb);   // (= hashn)
         k4[k] = grp | (uint32_t)((v * 0x1E35A7BD1E35A7BDull) >> (64 - kHashBits));
       }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; k++) {
         const uint32_t q = p + k;
-        k4[k] = grp | ((q + (uint32_t)hb <= jb.n && !jb.uncompressed) ? (hb > 4 ? hashn(jb.data + q, hb) : hash4(jb.data + q))
-                                                                        : kInvalidKey);
+        k4[k] = grp | ((q + (uint32_t)hb <= jb.n && !jb.uncompressed) ? hashn(jb.data + q, hb) : kInvalidKey);
       }
     }
     *reinterpret_cast<uint4 *>(keys + g) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
@@ -379,10 +378,9 @@ void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_j
   hipLaunchKernelGGL(cdict_matches_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, matches);
 }
 
-void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, uint32_t *keys,
+void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
                       uint32_t *vals) {
   const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total / 4 + 255) / 256);
-  static const int hb = getenv("MIB_HASH_BYTES") ? std::min(7, std::max(4, atoi(getenv("MIB_HASH_BYTES")))) : kHashBytes;
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, hb, keys, vals);
 }
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,

@@ -1,5 +1,7 @@
 // The parse: the wave-per-segment shortest-path DP and the
 // backtrack that turns its choices into commands.
+#include <hipcub/hipcub.hpp>
+
 #include "enc_common.h"
 
 namespace mib {
@@ -107,7 +109,7 @@ __device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches,
 struct alignas(16) StageEnt {   // one position's parse inputs in LDS (48 B: two b128 reads and a b64)
   uint32_t m[kMaxMatches];   // (clipped length << 24) | distance, 0 = none
   uint32_t mc[kMaxMatches];  // distance | distance-cost code << 24 (quarter bits)
-  uint32_t info;             // nm | maxlen << 8 (clipped to the segment)
+  uint32_t info;             // nm | maxlen << 8 | shortest usable length << 16
   float lc;                  // literal cost
   uint32_t pad[2];
 };
@@ -629,6 +631,150 @@ __global__ __launch_bounds__(256) void cost_model_kernel(const uint32_t *hist, C
     const float ls = log2f((float)max(sums[2], 1u)), miss = log2f((float)max(sums[2] + sums[4], 1u)) + 2.f;
     m.dist[t] = price(hd[t], ls, miss);
   }
+}
+
+// ---------------------------------------------------------------- 6. last-distance copies
+// The parse prices a copy at the path's last distance with short code 0, but it only sees the
+// distances the match finder offers: the shortest one for each length.  Structured data
+// (fonts) repeats records at a fixed stride with a few bytes changed, so the bytes after a
+// changed one often match again at the previous copy's distance, for fewer bytes than any
+// staircase entry covers -- the reference's parse finds these through its distance-cache
+// candidates (backward-references-hq.ts:283-330 / zopfli's "distance cache" loop).  This pass
+// walks each command's literal run with the distance of the copy before it (the decoder's
+// last distance there): where the run matches at that distance for L >= 2 bytes and the
+// stream's cost model (the second iteration's prices) says a code-0 copy of L bytes plus the
+// shortened command is cheaper than the literals, the command is split.  A code-0 copy never
+// pushes on the distance ring, so every other command's distance code is unchanged.
+// Block per segment, thread per command; two sweeps (count, keeping each command's count in
+// `cnts`, then rewrite in place from the last chunk down: a command only moves up, past the
+// commands split before it; only split commands walk their run again).
+constexpr int kRepT = 256;
+constexpr int kRepChunks = (int)((kSeg / 2 + 4 + kRepT - 1) / kRepT);
+constexpr float kRepMargin = 0.5f;   // bits a split must save
+__device__ __forceinline__ float cmd_bits(const CostModel &m, uint32_t ins, int cc, bool last) {
+  const int ic = ins_code_sel(ins);
+  const int cmd = combine_codes(ic, cc, last);
+  return m.cmd[cmd] + (float)ins_extra_sel(ic) + (last && cmd >= 128 ? m.dist[0] : 0.f);
+}
+// the greedy walk of one literal run [s, e) at distance d: calls out(ins, L) per split, returns
+// the literals left before the command's own copy
+template <class F>
+__device__ __forceinline__ uint32_t rep_walk(const Job &jb, const CostModel &m, uint32_t s, uint32_t e, uint32_t d,
+                                             bool skip_first, int cc_k, bool last_k, F out) {
+  const uint8_t *data = jb.data;
+  uint32_t q = skip_first ? s + 1 : s;
+  while (q + 2 <= e) {
+    const uint8_t *a = data + q, *b = a - d;
+    if (a[0] != b[0] || a[1] != b[1]) {
+      q++;
+      continue;
+    }
+    uint32_t L = 2 + match_len(a + 2, b + 2, e - q - 2);
+    if (jb.parts) L = min(L, part_cap(jb.abs_base + q, d, jb.part_bits, jb.part_lag));
+    if (L >= 2) {
+      float lits = 0.f;
+      for (uint32_t j = 0; j < L; j++) lits += m.lit[a[j]];
+      const int cc = copy_code(L);
+      const float before = cmd_bits(m, e - s, cc_k, last_k);
+      const float after = cmd_bits(m, q - s, cc, true) + (float)copy_extra(cc) + cmd_bits(m, e - q - L, cc_k, last_k);
+      if (lits + before - after > kRepMargin) {
+        out(q - s, L);
+        s = q + L;
+        q = s + 1;   // (byte s mismatches: the copy was measured to its end)
+        continue;
+      }
+    }
+    q++;
+  }
+  return e - s;
+}
+__global__ __launch_bounds__(kRepT) void rep_kernel(const Job *jobs, Seg *segs, const CostModel *model, RawCmd *raw,
+                                                     uint32_t *cnts) {
+  typedef hipcub::BlockScan<uint32_t, kRepT> Scan;
+  __shared__ typename Scan::TempStorage scan_tmp;
+  __shared__ uint32_t chunk_pos[kRepChunks + 1], chunk_split[kRepChunks + 1];
+  Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
+  const uint32_t n = sg.ncmd;
+  if (jb.uncompressed || n == 0) return;
+  const CostModel &m = model[sg.job];
+  const uint32_t t = threadIdx.x, nch = (n + kRepT - 1) / kRepT;
+  const uint32_t maxback = (1u << jb.lgwin) - 16;
+  RawCmd *r = raw + sg.cmd_off;
+  // command k: its run [pos, pos + ins), the distance before it, its copy's codes
+  // (d: read before any command of the chunk moves)
+  auto plan = [&](uint32_t k, const RawCmd &c, uint32_t d, uint32_t pos, auto out) -> uint32_t {
+    const uint32_t reach = min(maxback, pos + jb.hist);   // (bytes before data[0]: a streaming chunk's history)
+    if (!c.ins || !d || d > reach || is_word(jb, d)) return c.ins;
+    return rep_walk(jb, m, pos, pos + c.ins, d, k > 0, copy_code(c.len), c.dist == d, out);
+  };
+  // sweep 1: positions and split counts per chunk
+  uint32_t run = sg.start;
+  for (uint32_t ch = 0; ch < nch; ch++) {
+    const uint32_t k = ch * kRepT + t;
+    RawCmd c{0, 0, 0};
+    uint32_t d = 0;
+    if (k < n) {
+      c = r[k];
+      d = k ? r[k - 1].dist : sg.prev_dist;
+    }
+    uint32_t off, tot;
+    Scan(scan_tmp).ExclusiveSum(c.ins + c.len, off, tot);
+    __syncthreads();
+    uint32_t cnt = 0;
+    if (k < n) {
+      plan(k, c, d, run + off, [&](uint32_t, uint32_t) { cnt++; });
+      cnts[sg.cmd_off + k] = cnt;
+    }
+    uint32_t coff, ctot;
+    Scan(scan_tmp).ExclusiveSum(cnt, coff, ctot);
+    __syncthreads();
+    if (t == 0) {
+      chunk_pos[ch] = run;
+      chunk_split[ch] = ctot;
+    }
+    run += tot;
+  }
+  __syncthreads();
+  if (t == 0) {   // splits before each chunk
+    uint32_t acc = 0;
+    for (uint32_t ch = 0; ch < nch; ch++) {
+      const uint32_t v = chunk_split[ch];
+      chunk_split[ch] = acc;
+      acc += v;
+    }
+    chunk_split[nch] = acc;
+  }
+  __syncthreads();
+  if (chunk_split[nch] == 0) return;
+  // sweep 2, last chunk first: read the chunk into registers, then write it moved up
+  for (int ch = (int)nch - 1; ch >= 0; ch--) {
+    const uint32_t k = (uint32_t)ch * kRepT + t;
+    RawCmd c{0, 0, 0};
+    uint32_t d = 0;
+    if (k < n) {
+      c = r[k];
+      d = k ? r[k - 1].dist : sg.prev_dist;   // (below the chunk, or in it: nothing moved yet)
+    }
+    uint32_t off, tot;
+    Scan(scan_tmp).ExclusiveSum(c.ins + c.len, off, tot);
+    __syncthreads();
+    const uint32_t cnt = k < n ? cnts[sg.cmd_off + k] : 0u;
+    uint32_t coff, ctot;
+    Scan(scan_tmp).ExclusiveSum(cnt, coff, ctot);
+    __syncthreads();   // (every read of the chunk is done)
+    if (k < n) {
+      uint32_t w = k + chunk_split[ch] + coff;
+      uint32_t left = c.ins;
+      if (cnt) left = plan(k, c, d, chunk_pos[ch] + off, [&](uint32_t ins, uint32_t L) { r[w++] = RawCmd{ins, L, d}; });
+      r[w] = RawCmd{left, c.len, c.dist};
+    }
+    __syncthreads();
+  }
+  if (t == 0) sg.ncmd = n + chunk_split[nch];
+}
+void launch_rep(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const CostModel *model, RawCmd *raw, uint32_t *cnts) {
+  if (nsegs) hipLaunchKernelGGL(rep_kernel, dim3(nsegs), dim3(kRepT), 0, st, jobs, segs, model, raw, cnts);
 }
 
 #ifdef MIB_PROF

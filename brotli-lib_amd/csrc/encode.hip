@@ -9,7 +9,7 @@
 // symbols -- restructured for the GPU (kernels in enc_match / enc_parse / enc_entropy /
 // enc_emit.hip):
 //
-//   hash_keys + radix sort   every position of every stream gets key (stream group | hash4),
+//   hash_keys + radix sort   every position of every stream gets key (stream group | hash of 6 bytes, 4 for fonts),
 //                            <= 24 bits; a stable device radix sort lays each bucket out as
 //                            flat chains, one per stream, positions ascending
 //   find_matches             thread per sorted entry, LDS tile of the chain: the staircase of
@@ -178,6 +178,7 @@ bool wants_parts(const StreamDesc &d) {
 
 struct Params {
   int quality, lgwin, npostfix, ndirect;
+  bool font;
 };
 
 Params make_params(const mib_enc_opts *o) {
@@ -186,11 +187,24 @@ Params make_params(const mib_enc_opts *o) {
   p.lgwin = std::max(10, std::min(24, o ? o->lgwin : 22));
   p.npostfix = 0;
   p.ndirect = 0;
+  p.font = o && o->mode == MIB_MODE_FONT;
   if (p.quality >= 4 && o && o->mode == MIB_MODE_FONT) {   // sanitizeParams (enc-constants.ts:117-127)
     p.npostfix = 1;
     p.ndirect = 12;
   }
   return p;
+}
+
+// The last-distance copies pass (rep_kernel) and 4-byte bucket keys: FONT mode, whose glyph
+// records repeat with a few bytes changed (C3: -0.9 % and -1.8 % bytes; text gains < 0.01 %
+// from the pass and loses from the shorter keys).  MIB_REP / MIB_HASH_BYTES override.
+bool rep_pass(const Params &p) {
+  static const int v = getenv("MIB_REP") ? atoi(getenv("MIB_REP")) : -1;
+  return v < 0 ? p.font : v != 0;
+}
+int hash_bytes(const Params &p) {
+  static const int v = getenv("MIB_HASH_BYTES") ? std::min(6, std::max(4, atoi(getenv("MIB_HASH_BYTES")))) : -1;
+  return v > 0 ? v : p.font ? 4 : kHashBytes;
 }
 
 // The static dictionary for the match finder (§8 f3), once per device: the word-list offsets
@@ -443,7 +457,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
     const int depth = (int)env_u32("MIB_DEPTH", (uint32_t)depth_for_quality(prm.quality), 1, 64);   // override: experiments
     tm.start("hash_keys");
-    launch_hash_keys(st, d_jobs, d_seg_job, total, gshift, keys, vals);
+    launch_hash_keys(st, d_jobs, d_seg_job, total, gshift, hash_bytes(prm), keys, vals);
     tm.stop();
     tm.start("radix_sort");
     CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, key_bits, st));
@@ -479,6 +493,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     }
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
+    if (two_pass && rep_pass(prm)) launch_rep(st, d_jobs, d_segs, nsegs, model, raw, cmd_pos);   // (cmd_pos: scratch until codes)
     launch_ring_scan(st, d_jobs, (int)k, d_segs, nsegs, raw, push);
     launch_context_mode(st, d_jobs, d_mbs, nmbs);
     launch_codes(st, d_jobs, d_segs, d_mbs, nsegs, raw, cmds, cmd_pos, units, unit_h);

@@ -51,7 +51,7 @@ def test_c3_glyf_batch_font_mode():
     ref = sum(len(_oracle.encode(bufs[i], 11, 22, 2)) for i in range(0, 8))
     ours = sum(len(outs[i]) for i in range(0, 8))
     print('C3 ratio %.4f; first 8: GPU %d vs ref-fixed %d bytes (%.4f)' % (ratio, ours, ref, ours / ref))
-    assert ours < 1.05 * ref
+    assert ours < 0.92 * ref   # (measured 0.83: the FONT-mode 4-byte keys and last-distance copies)
 
 
 def test_c4_per_gpu_shard_1024x1mib_q11():
