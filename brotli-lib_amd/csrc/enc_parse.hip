@@ -114,7 +114,7 @@ struct alignas(16) StageEnt {   // one position's parse inputs in LDS (48 B: two
   uint32_t pad[2];
 };
 __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (distance << 32) | length, 0 = literal
-  const uint32_t cl = m & 0xFFFF;
+  const uint32_t cl = (m >> 16) ? 0u : m & 0xFFFF;   // (a literal edge: insert length << 16 | its codes)
   return cl ? (((uint64_t)d << 32) | cl) : 0ull;
 }
 __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
@@ -206,7 +206,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
       }
   }
   wave_sync();
-  // the pending nodes: cost, last distance, (copy length that reached it | insert length << 16)
+  // the pending nodes: cost, last distance, and the copy length that reached it, or (a literal
+  // edge) insert length << 16 | its insert code | the code's extra bits << 8
   float wc[kC];
   uint32_t wd[kC], wm[kC];
 #pragma unroll
@@ -299,16 +300,19 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     const uint32_t minlen = info >> 16;   // 4, or a dictionary word's length: that length only
     const float litcost = e.lc;
     const uint32_t ins = mm >> 16;
-    // insert code and extra bits: a table for short inserts, the closed form (rare) past it
-    int ic;
-    uint32_t iextra;
-    if (__builtin_expect(ins < (uint32_t)kInsTab, 1)) {
-      const uint32_t v = itab[ins];
-      ic = (int)(v & 0xFF);
-      iextra = v >> 8;
+    // the node's insert code and extra bits came with it (its literal edge carried them: see
+    // nx); a copy's end node has none
+    const int ic = ins ? (int)(mm & 0xFF) : 0;
+    const uint32_t iextra = ins ? (mm >> 8) & 0xFF : 0u;
+    // the codes of insert length ins + 1, for the literal edge out of i: looked up now, beside
+    // the copy prices' lookup, so the next step has no insert-code lookup on its serial path
+    const uint32_t ins1 = min(ins + 1, 65535u);
+    uint32_t nx;
+    if (__builtin_expect(ins1 < (uint32_t)kInsTab, 1)) {
+      nx = itab[ins1];
     } else {
-      ic = ins_code_sel(ins);
-      iextra = ins_extra_sel(ic);
+      const int c1 = ins_code_sel(ins1);
+      nx = (uint32_t)c1 | (ins_extra_sel(c1) << 8);
     }
     const float base = ci + (float)iextra;
     DPMARK(1);
@@ -391,7 +395,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
       DPCOUNT(5, 1);
       const uint32_t l = (uint32_t)(kL * c) + hl - off;   // wraps (huge) for consumed nodes
       float cand = kInf;
-      uint32_t nd = ld, nmeta = min(ins + 1, 65535u) << 16;
+      uint32_t nd = ld, nmeta = (ins1 << 16) | nx;
       if (l == 1 && act) cand = ci + litcost;
       if (l >= minlen && l <= maxlen) {
         uint32_t x = 0;
@@ -534,6 +538,51 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
   }
 }
 
+
+// ---------------------------------------------------------------- 4b. parse pieces
+// A call with few segments (one long stream: C2, a streaming chunk) leaves most SIMDs
+// without a DP wave, so its final parse runs on 2 or 4 pieces per segment (encode.hip
+// dp_piece_shift).  The pieces' commands are then joined per segment: moved to the front of
+// the segment's slice, each piece's trailing literals carried into the next piece's first
+// command, as carry_kernel does between segments.  Wave per segment.
+__global__ __launch_bounds__(64) void merge_pieces_kernel(Seg *segs, const Seg *pieces, int ps, RawCmd *raw) {
+  Seg &sg = segs[blockIdx.x];
+  const int P = 1 << ps;
+  const uint32_t lane = threadIdx.x;
+  RawCmd *dst = raw + sg.cmd_off;
+  uint32_t n = 0, carry = 0, last = 0;
+  for (int k = 0; k < P; k++) {
+    const Seg &pc = pieces[(size_t)blockIdx.x * P + k];
+    const RawCmd *src = raw + pc.cmd_off;   // (at or above dst + n: chunks are read before they are written)
+    const uint32_t m = pc.ncmd;
+    for (uint32_t q0 = 0; q0 < m; q0 += 64) {
+      const uint32_t q = q0 + lane;
+      RawCmd t{0, 0, 0};
+      if (q < m) t = src[q];
+      wave_sync();
+      if (q < m) {
+        if (q == 0) t.ins += carry;
+        dst[n + q] = t;
+      }
+      wave_sync();
+    }
+    if (m) {
+      n += m;
+      carry = pc.tail_lits;
+      last = pc.last_dist;
+    } else {
+      carry += pc.tail_lits;
+    }
+  }
+  if (lane == 0) {
+    sg.ncmd = n;
+    sg.tail_lits = carry;
+    sg.last_dist = n ? last : 0u;
+  }
+}
+void launch_merge_pieces(hipStream_t st, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw) {
+  if (nsegs) hipLaunchKernelGGL(merge_pieces_kernel, dim3(nsegs), dim3(64), 0, st, segs, pieces, ps, raw);
+}
 
 // ---------------------------------------------------------------- 5. second-iteration prices
 // ZopfliCostModel.setFromCommands + setCostFromHistogram (zopfli-cost-model.ts:68-159):

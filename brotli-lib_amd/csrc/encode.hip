@@ -198,6 +198,15 @@ Params make_params(const mib_enc_opts *o) {
 // The last-distance copies pass (rep_kernel) and 4-byte bucket keys: FONT mode, whose glyph
 // records repeat with a few bytes changed (C3: -0.9 % and -1.8 % bytes; text gains < 0.01 %
 // from the pass and loses from the shorter keys).  MIB_REP / MIB_HASH_BYTES override.
+// Parse pieces per segment (2^shift): the DP is one wave per (two) segments and latency-bound,
+// so a call with few segments runs it at low occupancy -- C2's 64 MiB stream is 1,024
+// segments, one wave per SIMD.  Pieces cut the parse more often (a piece's first node starts
+// a fresh path; copies stop at the piece end).  MIB_DP_PIECES=0..2 overrides.
+int dp_piece_shift(int nsegs) {
+  static const int v = getenv("MIB_DP_PIECES") ? std::min(2, std::max(0, atoi(getenv("MIB_DP_PIECES")))) : -1;
+  if (v >= 0) return v;
+  return nsegs >= 8192 ? 0 : nsegs >= 2048 ? 1 : 2;
+}
 bool rep_pass(const Params &p) {
   static const int v = getenv("MIB_REP") ? atoi(getenv("MIB_REP")) : -1;
   return v < 0 ? p.font : v != 0;
@@ -349,7 +358,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
           sg.end = (uint32_t)std::min<uint64_t>(mb.end, s0 + kSeg);
           sg.mb = (uint32_t)mbs.size();
           sg.cmd_off = (uint32_t)cmd_total;
-          cmd_total += (sg.end - sg.start) / 2 + 4;
+          cmd_total += (sg.end - sg.start) / 2 + 12;   // (+ 8: up to four parse pieces' slices)
           segs.push_back(sg);
         }
         mb.nseg = (uint32_t)segs.size() - mb.first_seg;
@@ -390,6 +399,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += ns1 * part_push_bytes();
   const bool two_pass = prm.quality >= 11 && zopfli_iterations() > 1;   // backward-references-hq.ts:562-605
   need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
+  need += ns1 * sizeof(Seg) * 4;   // parse pieces
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
   if (!ws) {
@@ -435,6 +445,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   // zopfli_sample() bytes of every segment (its own copy of the segment table)
   const bool sampled = two_pass && zopfli_sample() < kSeg;
   Seg *d_sample = sampled ? ar.take<Seg>(ns1) : nullptr;
+  // the final parse on 2^ps pieces per segment when there are few segments (merge_pieces_kernel)
+  const int ps = dp_piece_shift(nsegs);
+  Seg *d_pieces = ps ? ar.take<Seg>(ns1 << ps) : nullptr;
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
   Timer tm{ctx, st, mib_ctx_profiling(ctx) != 0, {}};
@@ -447,6 +460,24 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     for (Seg &sg : sample) sg.end = std::min(sg.end, sg.start + zopfli_sample());
     CK(hipMemcpyAsync(d_sample, sample.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
   }
+  std::vector<Seg> pieces;
+  if (ps && nsegs) {
+    const uint32_t plen = kSeg >> ps;
+    for (const Seg &sg : segs) {
+      uint32_t off = sg.cmd_off;
+      for (int q = 0; q < (1 << ps); q++) {
+        Seg pc = sg;
+        pc.start = std::min(sg.end, sg.start + (uint32_t)q * plen);
+        pc.end = std::min(sg.end, pc.start + plen);
+        pc.cmd_off = off;
+        off += (pc.end - pc.start) / 2 + 2;   // (backtrack_kernel's capacity)
+        pieces.push_back(pc);
+      }
+    }
+    CK(hipMemcpyAsync(d_pieces, pieces.data(), sizeof(Seg) * pieces.size(), hipMemcpyHostToDevice, st));
+  }
+  Seg *const d_fin = ps ? d_pieces : d_segs;   // the final parse's segment table
+  const int nfin = nsegs << ps;
   CK(hipMemcpyAsync(d_seg_job, seg_job.data(), seg_job.size() * 4, hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
   if (nsegs) {
@@ -474,23 +505,25 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
     tm.stop();
     tm.start(two_pass ? "dp_sample" : "dp_parse");
-    Seg *s1 = sampled ? d_sample : d_segs;
-    launch_dp(st, d_jobs, s1, nsegs, lit_h, nullptr, matches, choice, any_cdict);
+    Seg *s1 = sampled ? d_sample : two_pass ? d_segs : d_fin;
+    const int n1 = s1 == d_fin ? nfin : nsegs;
+    launch_dp(st, d_jobs, s1, n1, lit_h, nullptr, matches, choice, any_cdict);
     tm.stop();
     tm.start("backtrack");
-    launch_backtrack(st, d_jobs, s1, nsegs, choice, raw);
+    launch_backtrack(st, d_jobs, s1, n1, choice, raw);
     tm.stop();
     if (two_pass) {   // iteration 2: prices from the first parse's commands
       tm.start("cost_model");
       launch_cost_model(st, d_jobs, (int)k, s1, nsegs, raw, model_h, model);
       tm.stop();
       tm.start("dp_parse");
-      launch_dp(st, d_jobs, d_segs, nsegs, lit_h, model, matches, choice, any_cdict);
+      launch_dp(st, d_jobs, d_fin, nfin, lit_h, model, matches, choice, any_cdict);
       tm.stop();
       tm.start("backtrack");
-      launch_backtrack(st, d_jobs, d_segs, nsegs, choice, raw);
+      launch_backtrack(st, d_jobs, d_fin, nfin, choice, raw);
       tm.stop();
     }
+    if (ps) launch_merge_pieces(st, d_segs, nsegs, d_pieces, ps, raw);
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
     if (two_pass && rep_pass(prm)) launch_rep(st, d_jobs, d_segs, nsegs, model, raw, cmd_pos);   // (cmd_pos: scratch until codes)
@@ -654,6 +687,7 @@ struct DevDict {
   }
 };
 
+constexpr uint64_t kMaxChunk = 256ull << 20;   // BrotliEncoder: the largest device encode it waits for
 uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096 + 16 + sizeof(PartHead) + ((n + kSeg - 1) / kSeg) * sizeof(PartEntry); }
 
 }  // namespace
@@ -667,7 +701,9 @@ struct mib_encoder {
   uint32_t prev_bytes = 0;        // the last two bytes handed to the engine (literal contexts)
   uint64_t block = 1 << 16;       // the reference's 2^lgblock (enc-constants.ts:129-147)
   uint64_t chunk = 32ull << 20;   // input per device encode: whole blocks, at least this much
-                                  // (512 parse segments: 8 MiB left 7/8 of the chip idle in the DP)
+                                  // (512 parse segments: 8 MiB left 7/8 of the chip idle in the DP);
+                                  // it grows with the stream (kMaxChunk)
+  bool chunk_fixed = false;       // MIB_STREAM_CHUNK set: no growth
   // device state (the default context's device): the window of history plus the chunk,
   // ping-ponged so the next chunk's history is one device copy; the bucket table of earlier
   // positions; the output buffer
@@ -854,6 +890,10 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
       e->cur ^= 1;
       e->hist = keep;
       e->abs += n;
+      // a long stream gets longer device encodes: as much as it has already encoded, up to
+      // kMaxChunk (a 32 MiB encode is 512 parse segments, a quarter of the DP's waves; C5's
+      // 1 GiB stream takes 7 encodes instead of 32)
+      if (!e->chunk_fixed) e->chunk = std::max(e->chunk, std::min<uint64_t>(kMaxChunk, e->abs / e->block * e->block));
       e->pending.erase(e->pending.begin(), e->pending.begin() + (ptrdiff_t)n);
     }
     CK(hipStreamSynchronize(st));
@@ -904,6 +944,7 @@ mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
     if (prm.quality >= 9 && prm.lgwin > lgblock) lgblock = std::min(18, prm.lgwin);
   }
   e->block = 1ull << lgblock;
+  e->chunk_fixed = getenv("MIB_STREAM_CHUNK") != nullptr;
   e->chunk = (uint64_t)env_u32("MIB_STREAM_CHUNK", (uint32_t)(e->chunk >> 20), 1, 4096) << 20;   // MiB (tests, experiments)
   e->chunk = std::max<uint64_t>(e->block, e->chunk);
   return e;
