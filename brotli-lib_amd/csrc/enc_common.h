@@ -115,7 +115,7 @@ __device__ __forceinline__ bool is_word(const Job &jb, uint32_t d) { return jb.d
 struct Seg {
   uint32_t job, start, end;   // stream-local [start, end)
   uint32_t mb;                // metablock (global index)
-  uint32_t cmd_off;           // command slice (capacity (end-start)/2 + 12: its parse pieces' slices fit)
+  uint32_t cmd_off;           // command slice (capacity (end-start)/2 + 20: its parse pieces' slices fit)
   uint32_t ncmd;              // backtrack: copy commands
   uint32_t tail_lits;         // backtrack: literals after the last copy (all of them if none)
   uint32_t last_dist;         // backtrack: distance of the last copy (0: none)

@@ -198,14 +198,17 @@ Params make_params(const mib_enc_opts *o) {
 // The last-distance copies pass (rep_kernel) and 4-byte bucket keys: FONT mode, whose glyph
 // records repeat with a few bytes changed (C3: -0.9 % and -1.8 % bytes; text gains < 0.01 %
 // from the pass and loses from the shorter keys).  MIB_REP / MIB_HASH_BYTES override.
-// Parse pieces per segment (2^shift): the DP is one wave per (two) segments and latency-bound,
-// so a call with few segments runs it at low occupancy -- C2's 64 MiB stream is 1,024
-// segments, one wave per SIMD.  Pieces cut the parse more often (a piece's first node starts
-// a fresh path; copies stop at the piece end).  MIB_DP_PIECES=0..2 overrides.
+// Parse pieces per segment (2^shift, 8 KiB pieces): the DP is one wave per two segments and
+// latency-bound, so a call with few segments runs it at low occupancy (C2's 64 MiB stream is
+// 1,024 segments, one wave per SIMD), and even a full batch finishes its waves unevenly.
+// Pieces cut the parse more often (a piece's first node starts a fresh path; copies stop at
+// the piece end): C4 dp 123 -> 105 ms for +0.03 % bytes, C2 39 -> 8.5 ms.
+// MIB_DP_PIECES=0..3 overrides.
+constexpr int kMaxPieceShift = 3;
 int dp_piece_shift(int nsegs) {
-  static const int v = getenv("MIB_DP_PIECES") ? std::min(2, std::max(0, atoi(getenv("MIB_DP_PIECES")))) : -1;
-  if (v >= 0) return v;
-  return nsegs >= 8192 ? 0 : nsegs >= 2048 ? 1 : 2;
+  static const int v = getenv("MIB_DP_PIECES") ? std::min(kMaxPieceShift, std::max(0, atoi(getenv("MIB_DP_PIECES")))) : -1;
+  (void)nsegs;
+  return v >= 0 ? v : kMaxPieceShift;
 }
 bool rep_pass(const Params &p) {
   static const int v = getenv("MIB_REP") ? atoi(getenv("MIB_REP")) : -1;
@@ -358,7 +361,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
           sg.end = (uint32_t)std::min<uint64_t>(mb.end, s0 + kSeg);
           sg.mb = (uint32_t)mbs.size();
           sg.cmd_off = (uint32_t)cmd_total;
-          cmd_total += (sg.end - sg.start) / 2 + 12;   // (+ 8: up to four parse pieces' slices)
+          cmd_total += (sg.end - sg.start) / 2 + 4 + (2 << kMaxPieceShift);   // (room for the parse pieces' slices)
           segs.push_back(sg);
         }
         mb.nseg = (uint32_t)segs.size() - mb.first_seg;
@@ -399,7 +402,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += ns1 * part_push_bytes();
   const bool two_pass = prm.quality >= 11 && zopfli_iterations() > 1;   // backward-references-hq.ts:562-605
   need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
-  need += ns1 * sizeof(Seg) * 4;   // parse pieces
+  need += ns1 * sizeof(Seg) << kMaxPieceShift;   // parse pieces
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
   if (!ws) {
