@@ -147,6 +147,10 @@ constexpr uint64_t kPartFailed = ~0ull;   // a part's progress word when it fail
 __shared__ Lds g_lds;
 
 __shared__ Dec g_dec;   // the decoder state: LDS, so that it is wave-uniform and never waits on HBM stores
+// fast_loop: the source bytes of copies in flight, by LDS-DMA.  global_load_lds_ubyte writes
+// lane l's byte zero-extended to the DWORD at base + 4 l (probed on the MI355X:
+// scripts/probe/glds_probe.hip), so a slot is 64 dwords.
+__shared__ uint32_t g_cpa[64], g_cpb[64];
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
@@ -1687,7 +1691,11 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   uint32_t ncmd = 0;
   // a copy whose source load is in flight: destination, length, the loaded byte per lane
   int pend_cl = 0, pend_dst = 0;
-  int pend_v = 0;
+  // The source bytes of a copy in flight go to one of two LDS slots by DMA (pend_slot: which
+  // one), so the next copy's load can be issued before the copy in flight is completed.  (In
+  // registers, the loop-carried move of the newly loaded value waited for the load at the back
+  // edge, whatever the order of the code.)
+  int pend_slot = 0;
   auto shift16 = [&]() {   // the reference's acc/ho step, fed from the buffer; next half-word requested
     buf = (buf >> 16) | ((uint64_t)(uint32_t)U((int)pf) << 48);
     ho++;
@@ -1723,11 +1731,17 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     bo += (e1 >> 12) + 8;
     return e1 & 0xFFF;
   };
-  auto finish_copy = [&]() {   // complete the copy in flight: stores, literal context
+  // complete the copy in flight: stores, literal context.  Its bytes arrive in LDS by DMA,
+  // which the compiler does not wait for: behind_next -- the next copy's DMA was the last
+  // memory instruction issued, so everything but the newest one must have landed; else all.
+  auto finish_copy = [&](bool behind_next = false) {
     if (pend_cl) {
-      if (lane < pend_cl) ring[pend_dst + lane] = (uint8_t)pend_v;
-      c2b = pend_cl >= 2 ? __builtin_amdgcn_readlane(pend_v, pend_cl - 2) : c1;
-      c1 = __builtin_amdgcn_readlane(pend_v, pend_cl - 1);
+      if (behind_next) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int v = (int)(pend_slot ? g_cpb[lane] : g_cpa[lane]);
+      if (lane < pend_cl) ring[pend_dst + lane] = (uint8_t)v;
+      c2b = pend_cl >= 2 ? __builtin_amdgcn_readlane(v, pend_cl - 2) : c1;
+      c1 = __builtin_amdgcn_readlane(v, pend_cl - 1);
       pend_cl = 0;
     }
   };
@@ -1902,8 +1916,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       else dr3 = distance;
     }
     FMARK(2);
-    // ---- copy (no wrap, no fence): the previous copy is completed first (this one may read it)
-    finish_copy();
+    // ---- copy (no wrap, no fence)
     {
       const int cl = copy_len, dist = distance;
       // Every copy load below is unconditional (lanes past the copy read an in-range byte):
@@ -1912,10 +1925,22 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       // register -- it did so inside the literal loop, once per literal.
       if (cl <= 64) {   // one lane per byte: issue the load, complete later
         const int q = dist >= cl ? lane : lane % dist;
-        pend_v = (int)ring[src + (lane < cl ? q : 0)];
+        // A copy's source that ends before the copy in flight's destination does not need its
+        // bytes: its load is issued first and the copy in flight completed behind it, so the
+        // two loads overlap (C4: 62 % of commands have no literals, copy after copy).
+        // Otherwise (it may read them) the copy in flight is completed first.
+        if (src + cl > pend_dst) finish_copy();
+        const int at = src + (lane < cl ? q : 0);
+        typedef __attribute__((address_space(3))) void LV;
+        typedef __attribute__((address_space(1))) void GV;
+        if (pend_slot) __builtin_amdgcn_global_load_lds((GV *)(ring + at), (LV *)g_cpa, 1, 0, 0);   // lane l -> dword l
+        else __builtin_amdgcn_global_load_lds((GV *)(ring + at), (LV *)g_cpb, 1, 0, 0);
+        finish_copy(true);
+        pend_slot ^= 1;
         pend_dst = pos;
         pend_cl = cl;
       } else {
+        finish_copy();   // (this copy may read it)
         int lastv = 0;
         const int nit = U((cl + 63) >> 6);
         const int last = cl - 1;
