@@ -540,13 +540,17 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
 
 
 // ---------------------------------------------------------------- 4b. parse pieces
-// A call with few segments (one long stream: C2, a streaming chunk) leaves most SIMDs
-// without a DP wave, so its final parse runs on 2 or 4 pieces per segment (encode.hip
-// dp_piece_shift).  The pieces' commands are then joined per segment: moved to the front of
-// the segment's slice, each piece's trailing literals carried into the next piece's first
-// command, as carry_kernel does between segments.  Wave per segment.
-__global__ __launch_bounds__(64) void merge_pieces_kernel(Seg *segs, const Seg *pieces, int ps, RawCmd *raw) {
+// The final parse runs on 8 KiB pieces (encode.hip dp_piece_shift: a call with few segments
+// leaves SIMDs without a DP wave, and shorter pieces finish a batch's waves more evenly).
+// The pieces' commands are then joined per segment: moved to the front of the segment's
+// slice, each piece's trailing literals carried into the next piece's first command, as
+// carry_kernel does between segments; a copy that ends a piece and one that starts the next
+// at the same distance become one copy (a run of zeros stays one command per segment).
+// Wave per segment.
+__global__ __launch_bounds__(64) void merge_pieces_kernel(const Job *jobs, Seg *segs, const Seg *pieces, int ps,
+                                                          RawCmd *raw) {
   Seg &sg = segs[blockIdx.x];
+  const Job &jb = jobs[sg.job];
   const int P = 1 << ps;
   const uint32_t lane = threadIdx.x;
   RawCmd *dst = raw + sg.cmd_off;
@@ -554,7 +558,16 @@ __global__ __launch_bounds__(64) void merge_pieces_kernel(Seg *segs, const Seg *
   for (int k = 0; k < P; k++) {
     const Seg &pc = pieces[(size_t)blockIdx.x * P + k];
     const RawCmd *src = raw + pc.cmd_off;   // (at or above dst + n: chunks are read before they are written)
-    const uint32_t m = pc.ncmd;
+    uint32_t m = pc.ncmd;
+    if (m && n && carry == 0) {   // the previous piece ended in a copy: does this one continue it?
+      const RawCmd f = src[0], p = dst[n - 1];
+      if (f.ins == 0 && f.dist == p.dist && !is_word(jb, f.dist)) {
+        wave_sync();
+        if (lane == 0) dst[n - 1].len = p.len + f.len;
+        src++;
+        m--;
+      }
+    }
     for (uint32_t q0 = 0; q0 < m; q0 += 64) {
       const uint32_t q = q0 + lane;
       RawCmd t{0, 0, 0};
@@ -566,7 +579,7 @@ __global__ __launch_bounds__(64) void merge_pieces_kernel(Seg *segs, const Seg *
       }
       wave_sync();
     }
-    if (m) {
+    if (pc.ncmd) {
       n += m;
       carry = pc.tail_lits;
       last = pc.last_dist;
@@ -580,8 +593,8 @@ __global__ __launch_bounds__(64) void merge_pieces_kernel(Seg *segs, const Seg *
     sg.last_dist = n ? last : 0u;
   }
 }
-void launch_merge_pieces(hipStream_t st, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw) {
-  if (nsegs) hipLaunchKernelGGL(merge_pieces_kernel, dim3(nsegs), dim3(64), 0, st, segs, pieces, ps, raw);
+void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw) {
+  if (nsegs) hipLaunchKernelGGL(merge_pieces_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, pieces, ps, raw);
 }
 
 // ---------------------------------------------------------------- 5. second-iteration prices

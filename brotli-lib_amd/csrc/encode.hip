@@ -526,7 +526,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
       launch_backtrack(st, d_jobs, d_fin, nfin, choice, raw);
       tm.stop();
     }
-    if (ps) launch_merge_pieces(st, d_segs, nsegs, d_pieces, ps, raw);
+    if (ps) launch_merge_pieces(st, d_jobs, d_segs, nsegs, d_pieces, ps, raw);
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
     if (two_pass && rep_pass(prm)) launch_rep(st, d_jobs, d_segs, nsegs, model, raw, cmd_pos);   // (cmd_pos: scratch until codes)
