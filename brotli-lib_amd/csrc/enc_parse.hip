@@ -1,6 +1,7 @@
 // The parse: the wave-per-segment shortest-path DP and the
 // backtrack that turns its choices into commands.
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
 
 #include "enc_common.h"
 
@@ -849,7 +850,11 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 #endif
 // dp_kernel<2> when there are enough segments to fill the chip (1024 SIMDs: 256 CUs x 4),
 // else dp_kernel<1>
-static int dp_ks(int nsegs) { return nsegs < 2048 ? 1 : 2; }
+static int dp_ks(int nsegs) {
+  static const int v = getenv("MIB_DP_KS") ? atoi(getenv("MIB_DP_KS")) : 0;   // experiments
+  if (v == 1 || v == 2) return v;
+  return nsegs < 2048 ? 1 : 2;
+}
 static int dp_workgroups(int nsegs) {
   const int spw = kDpWaves * dp_ks(nsegs);
   return (nsegs + spw - 1) / spw;
