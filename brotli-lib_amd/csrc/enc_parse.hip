@@ -594,6 +594,36 @@ __global__ __launch_bounds__(64) void merge_pieces_kernel(const Job *jobs, Seg *
     sg.last_dist = n ? last : 0u;
   }
 }
+// the sampled copy of the segment table (each segment's first `sample` bytes) and the parse
+// pieces (2^ps per segment: kSeg >> ps bytes each, command slices back to back inside the
+// segment's, backtrack_kernel's capacity each); thread per segment
+__global__ void derive_segs_kernel(const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nsegs) return;
+  const Seg sg = segs[i];
+  if (d_sample) {
+    Seg sm = sg;
+    sm.end = min(sg.end, sg.start + sample);
+    d_sample[i] = sm;
+  }
+  if (pieces) {
+    const uint32_t plen = kSeg >> ps;
+    uint32_t off = sg.cmd_off;
+    for (int q = 0; q < (1 << ps); q++) {
+      Seg pc = sg;
+      pc.start = min(sg.end, sg.start + (uint32_t)q * plen);
+      pc.end = min(sg.end, pc.start + plen);
+      pc.cmd_off = off;
+      off += (pc.end - pc.start) / 2 + 2;
+      pieces[((size_t)i << ps) + q] = pc;
+    }
+  }
+}
+void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces) {
+  if (!d_sample && !ps) return;
+  hipLaunchKernelGGL(derive_segs_kernel, dim3((nsegs + 255) / 256), dim3(256), 0, st, segs, nsegs, sample, d_sample, ps,
+                     ps ? pieces : nullptr);
+}
 void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw) {
   if (nsegs) hipLaunchKernelGGL(merge_pieces_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, pieces, ps, raw);
 }

@@ -457,28 +457,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   CK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(Job) * k, hipMemcpyHostToDevice, st));
   if (nsegs) CK(hipMemcpyAsync(d_segs, segs.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
   if (nmbs) CK(hipMemcpyAsync(d_mbs, mbs.data(), sizeof(Mb) * nmbs, hipMemcpyHostToDevice, st));
-  std::vector<Seg> sample;
-  if (sampled && nsegs) {
-    sample = segs;
-    for (Seg &sg : sample) sg.end = std::min(sg.end, sg.start + zopfli_sample());
-    CK(hipMemcpyAsync(d_sample, sample.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
-  }
-  std::vector<Seg> pieces;
-  if (ps && nsegs) {
-    const uint32_t plen = kSeg >> ps;
-    for (const Seg &sg : segs) {
-      uint32_t off = sg.cmd_off;
-      for (int q = 0; q < (1 << ps); q++) {
-        Seg pc = sg;
-        pc.start = std::min(sg.end, sg.start + (uint32_t)q * plen);
-        pc.end = std::min(sg.end, pc.start + plen);
-        pc.cmd_off = off;
-        off += (pc.end - pc.start) / 2 + 2;   // (backtrack_kernel's capacity)
-        pieces.push_back(pc);
-      }
-    }
-    CK(hipMemcpyAsync(d_pieces, pieces.data(), sizeof(Seg) * pieces.size(), hipMemcpyHostToDevice, st));
-  }
+  // the sampled first iteration's and the parse pieces' segment tables, derived on the device
+  // (the pieces' table of a C4 call is 12.6 MB: built on the host it was a host loop and a
+  // pageable copy every call)
+  if (nsegs) launch_derive_segs(st, d_segs, nsegs, sampled ? zopfli_sample() : 0u, d_sample, ps, d_pieces);
   Seg *const d_fin = ps ? d_pieces : d_segs;   // the final parse's segment table
   const int nfin = nsegs << ps;
   CK(hipMemcpyAsync(d_seg_job, seg_job.data(), seg_job.size() * 4, hipMemcpyHostToDevice, st));
