@@ -204,11 +204,11 @@ Params make_params(const mib_enc_opts *o) {
 // Pieces cut the parse more often (a piece's first node starts a fresh path; copies stop at
 // the piece end): C4 dp 123 -> 105 ms for +0.03 % bytes, C2 39 -> 8.5 ms.
 // MIB_DP_PIECES=0..3 overrides.
-constexpr int kMaxPieceShift = 3;
+constexpr int kMaxPieceShift = 4;
 int dp_piece_shift(int nsegs) {
   static const int v = getenv("MIB_DP_PIECES") ? std::min(kMaxPieceShift, std::max(0, atoi(getenv("MIB_DP_PIECES")))) : -1;
   (void)nsegs;
-  return v >= 0 ? v : kMaxPieceShift;
+  return v >= 0 ? v : 3;
 }
 bool rep_pass(const Params &p) {
   static const int v = getenv("MIB_REP") ? atoi(getenv("MIB_REP")) : -1;
