@@ -4,6 +4,8 @@
 // Every stage here is parallel over segments (a block each) or over (metablock, alphabet);
 // the only per-stream serial steps (carry, offsets, dist_ring) touch O(segments) values.
 #include <hipcub/hipcub.hpp>
+#include <cstdlib>
+#include <algorithm>
 
 #include "enc_common.h"
 
@@ -45,7 +47,7 @@ __global__ void carry_kernel(Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
 // chooseContextMode (context.ts:180-227) on the metablock's first min(length, 4096) bytes:
 // up to 1024 samples classified as ASCII / UTF-8 lead / continuation, small-delta pairs.
 // Lane per metablock.  Values: 0 LSB6, 1 MSB6, 2 UTF8, 3 SIGNED (RFC 7932 section 7.1).
-__global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs) {
+__global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs, int force) {
   int m = blockIdx.x * blockDim.x + threadIdx.x;
   if (m >= nmbs) return;
   Mb &mb = mbs[m];
@@ -76,7 +78,7 @@ __global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs) {
   else if (lead > 0 && (double)cont > lead * 0.5) mode = 2;
   else if ((double)signed_pat > total * 0.3) mode = 3;
   else if ((double)ascii > total * 0.7) mode = 2;
-  mb.ctx_mode = (uint32_t)mode;
+  mb.ctx_mode = (uint32_t)(force >= 0 ? force : mode);
 }
 
 // ---------------------------------------------------------------- codes + unit histograms
@@ -328,8 +330,8 @@ __device__ __forceinline__ float hist_cost(float bits, int nnz) {
 }
 
 // Block per (metablock, literal | distance, block type): the type's context histograms.  A
-// literal block type may keep at most kMaxLitTrees / (literal block types) codes: past that
-// cap the cheapest merge is taken even when it costs bits.
+// literal block type may keep at most lit_cap / (literal block types) codes (launch_cluster):
+// past that cap the cheapest merge is taken even when it costs bits.
 // 16 waves, and a working set (64 histograms + the a < b pair savings) small enough for two
 // blocks per CU (44 VGPRs: 8 waves per SIMD): one block's barriers and LDS round trips in the
 // merge loop overlap the other's
@@ -337,7 +339,8 @@ constexpr int kCluT = 1024;
 constexpr int kCluPairs = kLitCtx * (kLitCtx - 1) / 2;
 // pair (a, b), a < b, in the triangular savings table; lexicographic, as a * 64 + b orders them
 __device__ __forceinline__ int tri(int a, int b) { return a * (2 * kLitCtx - a - 1) / 2 + b - a - 1; }
-__global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
+__global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd,
+                                                         int lit_cap) {
   constexpr int kMaxH = kLitCtx;
   // rows padded by one word: lanes reading one symbol of 64 different histograms hit 64 banks
   __shared__ uint32_t h[kMaxH][257];
@@ -362,7 +365,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     return;
   }
   const int nh = kind == 0 ? kLitCtx : kDistCtx;
-  const int cap = kind == 0 ? kMaxLitTrees / nbt : kDistCtx;
+  const int cap = kind == 0 ? max(1, lit_cap / nbt) : kDistCtx;
   const int A = kind == 0 ? 256 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
   const int stride = kind == 0 ? 256 : 128;
   uint32_t *src = kind == 0 ? hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256
@@ -1516,10 +1519,19 @@ void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, con
   hipLaunchKernelGGL(dist_ring_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, cmds);
 }
 void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
-  hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs);
+  static const int force = getenv("MIB_CTX_MODE") ? atoi(getenv("MIB_CTX_MODE")) & 3 : -1;   // experiments
+  hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, force);
 }
+// Literal prefix codes per metablock: at most kLitTreeCap.  The decoder keeps a metablock's
+// tables in its LDS table area only when they fit (12,224 entries, >= 256 per code); past
+// that every symbol lookup is an HBM load.  With up to 64 codes some C3 fonts overflowed it,
+// and the batch kernel waits for its slowest stream: C3 decode 76 -> 46 ms at 32 codes, and
+// the stream is smaller too (0.4585 -> 0.4582: fewer codes to send); 24: 0.45816 / 45.6 ms;
+// C4 never needs more than 24.  MIB_LIT_TREES overrides (4..64).
+constexpr int kLitTreeCap = 24;
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
-  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd);
+  static const int cap = getenv("MIB_LIT_TREES") ? std::min(kMaxLitTrees, std::max(4, atoi(getenv("MIB_LIT_TREES")))) : kLitTreeCap;
+  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, cap);
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
