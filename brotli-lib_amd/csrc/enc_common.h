@@ -84,6 +84,7 @@ struct Job {                // one stream (or streaming chunk) to encode
   const uint8_t *cdict;     // custom dictionary (device), or null (see kCDictMark)
   uint32_t cdict_len;
   uint32_t cdict_tail4;     // its last four bytes (little endian)
+  uint32_t font;            // FONT mode: signed literal contexts unless the bytes read as UTF-8
 };
 
 // Custom-dictionary copies (mib_enc_opts.dict; the reference decoder's compound dictionary,
