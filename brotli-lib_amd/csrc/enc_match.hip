@@ -66,7 +66,9 @@ constexpr int kPreW = 4;   // staged prefix: 4 x 8 bytes
 __device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, uint64_t *o) {
   if (avail >= 36) {   // nine aligned words (all inside the stream) and funnel shifts
     const uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    // (global, not flat: the stream bytes are device memory; a flat load also counts on lgkmcnt)
+    typedef const __attribute__((address_space(1))) uint32_t GU32;
+    GU32 *w = (GU32 *)(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
     uint32_t v[9];
 #pragma unroll
