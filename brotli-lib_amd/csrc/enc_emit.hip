@@ -136,6 +136,48 @@ __device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb,
   }
 }
 
+// Item k of command q when it carries no block switch (the common case): its bits and its
+// whole bit string (<= 15 + 24 + 24 bits), so the write pass ORs it without looking the codes up
+// again; an item with a switch returns false and is written by write_item.
+__device__ __forceinline__ bool item_packed(const Codes &cd, const Mb &mb, const uint8_t *cmap, const uint8_t *lut, const Job &jb,
+                                            const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q, uint32_t k,
+                                            uint32_t &bits, uint64_t &val) {
+  const Unit &u = su[unit_of(sg, p)];
+  if (k == 0) {
+    if (switch_at(u, 1, q)) return false;
+    const int ct = u.type[1];
+    const int ic = ins_code(c.ins);
+    const uint32_t clen = c.copy ? c.copy : 2;
+    const int cc = copy_code(clen);
+    const uint32_t n0 = cd.cd[ct][c.cmd_prefix], n1 = kInsExtra[ic], n2 = kCopyExtra[cc];
+    val = (uint64_t)cd.cc[ct][c.cmd_prefix] | ((uint64_t)(c.ins - kInsBase[ic]) << n0) | ((uint64_t)(clen - kCopyBase[cc]) << (n0 + n1));
+    bits = n0 + n1 + n2;
+    return true;
+  }
+  if (k <= c.ins) {
+    const uint32_t lp = p + k - 1;
+    const Unit &ul = su[unit_of(sg, lp)];
+    if (lit_switch_at(ul, lp)) return false;
+    const uint32_t lit = jb.data[lp];
+    const int tree = literal_tree(cmap, lut, ul, prev2(jb, lp));
+    bits = cd.ld[tree][lit];
+    val = cd.lc[tree][lit];
+    return true;
+  }
+  if (!c.copy || c.cmd_prefix < 128) {
+    bits = 0;
+    val = 0;
+    return true;
+  }
+  if (switch_at(u, 2, q)) return false;
+  const uint32_t dcode = c.dist_prefix & 0x3FF;
+  const int tree = mb.dist_cmap[u.type[2] * kDistCtx + dist_ctx(c.copy)];
+  const uint32_t n0 = cd.dd[tree][dcode];
+  val = (uint64_t)cd.dcd[tree][dcode] | ((uint64_t)c.dist_extra << n0);
+  bits = n0 + (c.dist_prefix >> 10);
+  return true;
+}
+
 // Block per segment.  The segment's commands are taken kBlock at a time and expanded into
 // their items (header, literals, distance); kEmitItems items per lane per tile get their bit
 // offsets from a block scan and are ORed into an LDS window, which is then stored as whole
@@ -186,6 +228,8 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
     __syncthreads();
     for (uint32_t i0 = 0; i0 < nitems; i0 += kBlock * kEmitItems) {
       uint32_t bits[kEmitItems], qj[kEmitItems], kk[kEmitItems];
+      uint64_t val[kEmitItems];
+      bool packed[kEmitItems];
       const uint32_t first = i0 + (uint32_t)t * kEmitItems;
       uint32_t j = first < nitems ? map.find(first, nb) : 0;
       for (int e = 0; e < kEmitItems; e++) {
@@ -193,13 +237,16 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
         bits[e] = 0;
         qj[e] = j;
         kk[e] = 0;
+        val[e] = 0;
+        packed[e] = true;
         if (i < nitems) {
           while (map.off[j + 1] <= i) j++;
           qj[e] = j;
           kk[e] = i - map.off[j];
           const Cmd &k = sh_c[j];
           const uint32_t p = sh_p[j];
-          bits[e] = item_bits(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
+          packed[e] = item_packed(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e], bits[e], val[e]);
+          if (!packed[e]) bits[e] = item_bits(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
         }
       }
       uint32_t boff[kEmitItems], total;
@@ -211,6 +258,14 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
       __syncthreads();
       for (int e = 0; e < kEmitItems; e++) {
         if (!bits[e]) continue;
+        if (packed[e]) {   // the whole item: at most 63 bits over three words
+          const uint32_t b = rel0 + boff[e], w = b >> 5, sh = b & 31;
+          const uint64_t lo = val[e] << sh;
+          atomicOr(win + w, (uint32_t)lo);
+          if (bits[e] + sh > 32) atomicOr(win + w + 1, (uint32_t)(lo >> 32));
+          if (bits[e] + sh > 64) atomicOr(win + w + 2, (uint32_t)(val[e] >> (64 - sh)));
+          continue;
+        }
         const uint32_t jj = qj[e];
         const Cmd &k = sh_c[jj];
         const uint32_t p = sh_p[jj];
