@@ -84,7 +84,8 @@ struct Job {                // one stream (or streaming chunk) to encode
   const uint8_t *cdict;     // custom dictionary (device), or null (see kCDictMark)
   uint32_t cdict_len;
   uint32_t cdict_tail4;     // its last four bytes (little endian)
-  uint32_t font;            // FONT mode: signed literal contexts unless the bytes read as UTF-8
+  uint32_t font;            // FONT mode (last-distance copies pass, 4-byte keys)
+  uint32_t hq;              // quality >= 10 (context mode rule)
 };
 
 // Custom-dictionary copies (mib_enc_opts.dict; the reference decoder's compound dictionary,

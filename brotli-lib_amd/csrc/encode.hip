@@ -309,6 +309,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.ndirect = (uint32_t)prm.ndirect;
     jb.uncompressed = (prm.quality == 0 || n < 64) ? 1 : 0;
     jb.font = prm.font ? 1 : 0;
+    jb.hq = prm.quality >= 10 ? 1 : 0;
     jb.hdr_lgwin = sd[j].hdr_lgwin;
     jb.final_ = sd[j].final_;
     for (int q = 0; q < 4; q++) jb.dc_in[q] = jb.dc_out[q] = sd[j].dc[q];
