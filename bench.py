@@ -218,9 +218,11 @@ def run_stream(args, rank, world, local):
     opts = {'quality': q, 'lgwin': lg, 'mode': 1, 'customDictionary': cdict}
     step = MIB
 
+    view = memoryview(data)   # update() gets views of the stream, as Uint8Array.subarray gives
+
     def enc():
         e = brotli_amd.BrotliEncoder(opts)
-        parts = [e.update(data[p:p + step]) for p in range(0, size, step)]
+        parts = [e.update(view[p:p + step]) for p in range(0, size, step)]
         parts.append(e.finish())
         return b''.join(parts)
     for _ in range(max(1, args.warmup)):

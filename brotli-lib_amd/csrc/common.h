@@ -4,6 +4,13 @@
 
 #include "../../include/brotli_amd.h"
 
+// a result buffer (mib_buf.data) from the allocator mib_set_allocator chose (runtime.cpp)
+extern "C" uint8_t *mib_buf_alloc(size_t n);
+// out <- a new result buffer holding len bytes copied from device memory: 0 or MIB_E_*
+extern "C" int mib_buf_from_device(mib_buf *out, const void *d_src, uint64_t len);
+// *outs[i] <- len[i] bytes from d_src[i], i < k (one bulk copy when they are small)
+extern "C" int mib_bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len);
+
 namespace mib {
 
 // One stream to decode.  Filled by the host, read/written by decode kernels.

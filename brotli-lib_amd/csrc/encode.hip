@@ -29,6 +29,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <memory>
 #include <mutex>
 #include <vector>
@@ -675,25 +676,32 @@ struct DevDict {
 };
 
 constexpr uint64_t kMaxChunk = 256ull << 20;   // BrotliEncoder: the largest device encode it waits for
+// BrotliEncoder: update() pieces up to half this size gather in a pinned host stage and reach
+// the device one stage at a time (a copy call and its wait cost ~70 us: C5's 1 MiB pieces
+// spent 80 ms of a 600 ms encode there); the stages of all encoders share a pinned budget
+constexpr uint64_t kStage = 8ull << 20;
+constexpr uint64_t kStageBudget = 256ull << 20;
+std::atomic<uint64_t> g_stage_bytes{0};
 uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096 + 16 + sizeof(PartHead) + ((n + kSeg - 1) / kSeg) * sizeof(PartEntry); }
 
 }  // namespace
 
 struct mib_encoder {
   mib_enc_opts opts;
-  std::vector<uint8_t> pending;   // input not yet handed to the device
+  uint64_t pend = 0;              // input not yet encoded: on the device, at buf[cur] + hist
   bool started = false;
   bool finished = false;
   int32_t dc[4] = {4, 11, 15, 16};
   uint32_t prev_bytes = 0;        // the last two bytes handed to the engine (literal contexts)
+  uint64_t window = 1 << 22;      // 2^lgwin: the history kept for the next chunk
   uint64_t block = 1 << 16;       // the reference's 2^lgblock (enc-constants.ts:129-147)
   uint64_t chunk = 32ull << 20;   // input per device encode: whole blocks, at least this much
                                   // (512 parse segments: 8 MiB left 7/8 of the chip idle in the DP);
                                   // it grows with the stream (kMaxChunk)
   bool chunk_fixed = false;       // MIB_STREAM_CHUNK set: no growth
-  // device state (the default context's device): the window of history plus the chunk,
-  // ping-ponged so the next chunk's history is one device copy; the bucket table of earlier
-  // positions; the output buffer
+  // device state (the default context's device): the window of history, then the pending
+  // input (update() copies each piece straight here), ping-ponged so the next chunk's history
+  // is one device copy; the bucket table of earlier positions
   int device = -1;
   uint8_t *buf[2] = {nullptr, nullptr};
   uint64_t buf_cap = 0;
@@ -704,6 +712,8 @@ struct mib_encoder {
   uint32_t *tab = nullptr;
   std::vector<uint8_t> dict;      // customDictionary (the encoder's own copy) and its device copy
   DevDict ddict;
+  uint8_t *stage = nullptr;       // small update() pieces gather here (pinned host memory) ...
+  uint64_t staged = 0;            // ... these many bytes, still to go behind the pending input
 };
 extern "C" {
 
@@ -775,74 +785,90 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
   std::vector<uint64_t> ooff(k + 1, 0);
   rc = encode_streams(c, o, sd.data(), k, d_out, cap, ooff.data(), nullptr, st);
   if (rc == 0) {
-    std::vector<uint8_t> host(ooff[k]);
-    if (ooff[k] && hipMemcpy(host.data(), d_out, ooff[k], hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
-    for (size_t i = 0; rc == 0 && i < k; i++) {
-      uint64_t len = ooff[i + 1] - ooff[i];
-      out[i].data = (uint8_t *)malloc(len ? len : 1);
-      out[i].size = len;
-      if (len) memcpy(out[i].data, host.data() + ooff[i], len);
+    std::vector<mib_buf *> outs(k);
+    std::vector<const uint8_t *> src(k);
+    std::vector<uint64_t> lens(k);
+    for (size_t i = 0; i < k; i++) {
+      outs[i] = &out[i];
+      src[i] = d_out + ooff[i];
+      lens[i] = ooff[i + 1] - ooff[i];
       if (status) status[i] = 0;
     }
+    rc = mib_bufs_from_device(k, outs.data(), src.data(), lens.data());
   }
   hipStreamSynchronize(st);
   dd.release();
   return rc;
 }
 
-// BrotliEncoder on the device: encoders es[0..k) (same options) each encode ns[i] bytes of
-// their pending input in ONE launch sequence.  A chunk's matches reach the encoder's history
-// (the last 2^lgwin bytes, kept in HBM) through the sorted chunk and the bucket table, so the
-// stream is what a one-shot encode with the same window would produce, cut into chunks.
-static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *finals, size_t k,
-                       std::vector<uint8_t> *accs) {
-  DefaultLock use;
-  mib_ctx *c = mib_default_ctx();
-  if (!c) return MIB_E_NO_DEVICE;
-  const int dev = mib_ctx_device_of(c);
-  CK(hipSetDevice(dev));
+// The encoder's device buffers on the default context's device (dev), with room for
+// `need` bytes of history + pending input (+ the zero tail the kernels read past a chunk).
+static int encoder_room(mib_encoder *e, int dev, uint64_t need, hipStream_t st) {
+  if (e->device >= 0 && e->device != dev) return MIB_E_INVALID_ARG;
+  e->device = dev;
+  need += 320;
+  if (e->buf_cap < need) {   // first use, a grown chunk, or one large update()
+    need = std::max(need, e->window + e->chunk + e->block + 320);
+    uint8_t *nb[2] = {nullptr, nullptr};
+    for (int b = 0; b < 2; b++)
+      if (hipMalloc(&nb[b], need) != hipSuccess) {
+        if (nb[0]) hipFree(nb[0]);
+        return MIB_E_OUT_OF_MEMORY;
+      }
+    if (e->hist + e->pend) CK(hipMemcpyAsync(nb[0], e->buf[e->cur], e->hist + e->pend, hipMemcpyDeviceToDevice, st));
+    CK(hipStreamSynchronize(st));
+    for (int b = 0; b < 2; b++)
+      if (e->buf[b]) hipFree(e->buf[b]);
+    e->buf[0] = nb[0];
+    e->buf[1] = nb[1];
+    e->cur = 0;
+    e->buf_cap = need;
+  }
+  if (!e->tab) {
+    if (hipMalloc(&e->tab, sizeof(uint32_t) * kHistWays << kHashBits) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
+    CK(hipMemsetAsync(e->tab, 0xFF, sizeof(uint32_t) * kHistWays << kHashBits, st));
+  }
+  if (!e->ddict.d && e->dict.size() >= 4) {
+    const int r = e->ddict.upload(e->dict.data(), e->dict.size(), st);
+    if (r) return r;
+  }
+  return 0;
+}
+
+// The encoder's staged bytes -> its device buffer, behind the pending input.  The copy runs
+// from pinned memory, asynchronously: the stage is reused only after the stream is synchronised.
+static int flush_stage(mib_encoder *e, int dev, hipStream_t st) {
+  if (!e->staged) return 0;
+  const int rc = encoder_room(e, dev, e->hist + e->pend + e->staged, st);
+  if (rc) return rc;
+  CK(hipMemcpyAsync(e->buf[e->cur] + e->hist + e->pend, e->stage, e->staged, hipMemcpyHostToDevice, st));
+  e->pend += e->staged;
+  e->staged = 0;
+  return 0;
+}
+
+// BrotliEncoder on the device: encoders es[0..k) (same options) each encode the first ns[i]
+// bytes of their pending input in ONE launch sequence; outs[i] gets encoder i's bytes.  A
+// chunk's matches reach the encoder's history (the last 2^lgwin bytes, kept in HBM) through
+// the sorted chunk and the bucket table, so the stream is what a one-shot encode with the same
+// window would produce, cut into chunks.  Caller: DefaultLock held, device current.
+static int encoder_run(mib_ctx *c, mib_encoder *const *es, const uint64_t *ns, const bool *finals, size_t k,
+                       mib_buf *const *outs) {
   hipStream_t st = (hipStream_t)mib_ctx_stream_of(c);
   const Params prm = make_params(&es[0]->opts);
-  const uint64_t window = 1ull << prm.lgwin;
   uint64_t cap = 0;
-  for (size_t i = 0; i < k; i++) {
-    mib_encoder *e = es[i];
-    if (e->device >= 0 && e->device != dev) return MIB_E_INVALID_ARG;
-    const uint64_t need = window + std::max<uint64_t>(ns[i], e->chunk) + 256;
-    if (e->buf_cap < need) {   // (first use, or a final chunk larger than the others)
-      uint8_t *nb[2] = {nullptr, nullptr};
-      for (int b = 0; b < 2; b++)
-        if (hipMalloc(&nb[b], need) != hipSuccess) {
-          if (nb[0]) hipFree(nb[0]);
-          return MIB_E_OUT_OF_MEMORY;
-        }
-      if (e->hist) CK(hipMemcpyAsync(nb[0], e->buf[e->cur], e->hist, hipMemcpyDeviceToDevice, st));
-      CK(hipStreamSynchronize(st));
-      for (int b = 0; b < 2; b++)
-        if (e->buf[b]) hipFree(e->buf[b]);
-      e->buf[0] = nb[0];
-      e->buf[1] = nb[1];
-      e->cur = 0;
-      e->buf_cap = need;
-    }
-    if (!e->tab) {
-      if (hipMalloc(&e->tab, sizeof(uint32_t) * kHistWays << kHashBits) != hipSuccess) return MIB_E_OUT_OF_MEMORY;
-      CK(hipMemsetAsync(e->tab, 0xFF, sizeof(uint32_t) * kHistWays << kHashBits, st));
-    }
-    if (!e->ddict.d && e->dict.size() >= 4) {
-      const int r = e->ddict.upload(e->dict.data(), e->dict.size(), st);
-      if (r) return r;
-    }
-    e->device = dev;
-    cap += out_bound(ns[i]);
-  }
+  for (size_t i = 0; i < k; i++) cap += out_bound(ns[i]);
   uint8_t *d_out = mib_ctx_stage(c, 3, cap + 64);
   if (!d_out) return MIB_E_OUT_OF_MEMORY;
   std::vector<StreamDesc> sd(k);
   for (size_t i = 0; i < k; i++) {
     mib_encoder *e = es[i];
     uint8_t *base = e->buf[e->cur] + e->hist;
-    if (ns[i]) CK(hipMemcpyAsync(base, e->pending.data(), ns[i], hipMemcpyHostToDevice, st));
+    // the input past this chunk moves to the other buffer (behind the history kept there),
+    // and the chunk is followed by zeros, as a one-shot encode's input is
+    const uint64_t keep = std::min<uint64_t>(e->window, e->hist + ns[i]);
+    if (e->pend > ns[i])
+      CK(hipMemcpyAsync(e->buf[e->cur ^ 1] + keep, base + ns[i], e->pend - ns[i], hipMemcpyDeviceToDevice, st));
     CK(hipMemsetAsync(base + ns[i], 0, 64, st));
     fill_desc(sd[i], base, ns[i], prm, false);
     sd[i].hdr_lgwin = e->started ? 0 : (uint32_t)prm.lgwin;
@@ -858,34 +884,41 @@ static int encoder_run(mib_encoder *const *es, const uint64_t *ns, const bool *f
   std::vector<uint64_t> ooff(k + 1, 0);
   std::vector<int32_t> dcs(4 * std::max<size_t>(k, 1));
   int rc = encode_streams(c, &es[0]->opts, sd.data(), k, d_out, cap, ooff.data(), (int32_t(*)[4])dcs.data(), st);
-  if (rc == 0) {
-    std::vector<uint8_t> host(ooff[k]);
-    if (ooff[k] && hipMemcpy(host.data(), d_out, ooff[k], hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
-    for (size_t i = 0; rc == 0 && i < k; i++) {
-      mib_encoder *e = es[i];
-      accs[i].insert(accs[i].end(), host.data() + ooff[i], host.data() + ooff[i + 1]);
-      e->obytes += ooff[i + 1] - ooff[i];
-      for (int q = 0; q < 4; q++) e->dc[q] = dcs[4 * i + q];
-      const uint64_t n = ns[i];
-      for (uint64_t q = n - std::min<uint64_t>(n, 2); q < n; q++)   // the chunk's last bytes
-        e->prev_bytes = ((e->prev_bytes << 8) & 0xFF00) | e->pending[q];
-      e->started = true;
-      // the next chunk's history: the last 2^lgwin bytes, moved to the other buffer's front
-      const uint64_t keep = std::min<uint64_t>(window, e->hist + n);
-      if (keep)
-        CK(hipMemcpyAsync(e->buf[e->cur ^ 1], e->buf[e->cur] + e->hist + n - keep, keep, hipMemcpyDeviceToDevice, st));
-      e->cur ^= 1;
-      e->hist = keep;
-      e->abs += n;
-      // a long stream gets longer device encodes: as much as it has already encoded, up to
-      // kMaxChunk (a 32 MiB encode is 512 parse segments, a quarter of the DP's waves; C5's
-      // 1 GiB stream takes 7 encodes instead of 32)
-      if (!e->chunk_fixed) e->chunk = std::max(e->chunk, std::min<uint64_t>(kMaxChunk, e->abs / e->block * e->block));
-      e->pending.erase(e->pending.begin(), e->pending.begin() + (ptrdiff_t)n);
-    }
-    CK(hipStreamSynchronize(st));
+  if (rc) return rc;
+  std::vector<const uint8_t *> src(k);
+  std::vector<uint64_t> lens(k);
+  std::vector<uint8_t> last(2 * k);   // each chunk's last two bytes (the next chunk's literal context)
+  for (size_t i = 0; i < k; i++) {
+    src[i] = d_out + ooff[i];
+    lens[i] = ooff[i + 1] - ooff[i];
+    const uint64_t m = std::min<uint64_t>(ns[i], 2);
+    if (m) CK(hipMemcpyAsync(&last[2 * i + 2 - m], es[i]->buf[es[i]->cur] + es[i]->hist + ns[i] - m, m,
+                             hipMemcpyDeviceToHost, st));
   }
-  return rc;
+  CK(hipStreamSynchronize(st));
+  if ((rc = mib_bufs_from_device(k, outs, src.data(), lens.data()))) return rc;
+  for (size_t i = 0; i < k; i++) {
+    mib_encoder *e = es[i];
+    const uint64_t n = ns[i];
+    e->obytes += lens[i];
+    for (int q = 0; q < 4; q++) e->dc[q] = dcs[4 * i + q];
+    for (uint64_t q = 2 - std::min<uint64_t>(n, 2); q < 2; q++) e->prev_bytes = ((e->prev_bytes << 8) & 0xFF00) | last[2 * i + q];
+    e->started = true;
+    // the next chunk's history: the last 2^lgwin bytes, moved to the other buffer's front
+    const uint64_t keep = std::min<uint64_t>(e->window, e->hist + n);
+    if (keep)
+      CK(hipMemcpyAsync(e->buf[e->cur ^ 1], e->buf[e->cur] + e->hist + n - keep, keep, hipMemcpyDeviceToDevice, st));
+    e->cur ^= 1;
+    e->hist = keep;
+    e->abs += n;
+    e->pend -= n;
+    // a long stream gets longer device encodes: as much as it has already encoded, up to
+    // kMaxChunk (a 32 MiB encode is 512 parse segments, a quarter of the DP's waves; C5's
+    // 1 GiB stream takes 7 encodes instead of 32)
+    if (!e->chunk_fixed) e->chunk = std::max(e->chunk, std::min<uint64_t>(kMaxChunk, e->abs / e->block * e->block));
+  }
+  CK(hipStreamSynchronize(st));
+  return 0;
 }
 
 int mib_encode(const uint8_t *in, size_t n, const mib_enc_opts *o, mib_buf *out) {
@@ -931,18 +964,11 @@ mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
     if (prm.quality >= 9 && prm.lgwin > lgblock) lgblock = std::min(18, prm.lgwin);
   }
   e->block = 1ull << lgblock;
+  e->window = 1ull << prm.lgwin;
   e->chunk_fixed = getenv("MIB_STREAM_CHUNK") != nullptr;
   e->chunk = (uint64_t)env_u32("MIB_STREAM_CHUNK", (uint32_t)(e->chunk >> 20), 1, 4096) << 20;   // MiB (tests, experiments)
   e->chunk = std::max<uint64_t>(e->block, e->chunk);
   return e;
-}
-
-static int take_acc(std::vector<uint8_t> &acc, mib_buf *out) {
-  out->data = (uint8_t *)malloc(acc.size() ? acc.size() : 1);
-  if (!out->data) return MIB_E_OUT_OF_MEMORY;
-  out->size = acc.size();
-  if (acc.size()) memcpy(out->data, acc.data(), acc.size());
-  return 0;
 }
 
 static bool same_opts(const mib_enc_opts &a, const mib_enc_opts &b) {
@@ -959,39 +985,68 @@ int mib_encoder_update_batch(mib_encoder *const *es, const mib_span *in, size_t 
     for (size_t j = 0; j < i; j++)
       if (es[j] == es[i]) return MIB_E_INVALID_ARG;
   }
-  std::vector<std::vector<uint8_t>> accs(k);
-  std::vector<mib_encoder *> run;
-  std::vector<uint64_t> ns;
-  std::vector<size_t> idx;
+  DefaultLock use;
+  mib_ctx *c = mib_default_ctx();
+  if (!c) return MIB_E_NO_DEVICE;
+  const int dev = mib_ctx_device_of(c);
+  CK(hipSetDevice(dev));
+  hipStream_t st = (hipStream_t)mib_ctx_stream_of(c);
+  // a small piece that completes no chunk gathers in the encoder's stage; the others go
+  // straight to its device buffer, behind the input already there
+  bool copied = false;
   for (size_t i = 0; i < k; i++) {
     mib_encoder *e = es[i];
-    e->pending.insert(e->pending.end(), in[i].data, in[i].data + in[i].size);
+    const uint64_t n = in[i].size;
+    int rc;
+    if (n && n <= kStage / 2 && e->pend + e->staged + n < e->chunk) {
+      if (!e->stage && g_stage_bytes.fetch_add(kStage) + kStage <= kStageBudget) {
+        if (hipHostMalloc(&e->stage, kStage, hipHostMallocDefault) != hipSuccess) e->stage = nullptr;
+      }
+      if (!e->stage) g_stage_bytes.fetch_sub(kStage);   // (over budget / no pinned memory: no stage)
+    }
+    if (e->stage && n && n <= kStage / 2 && e->pend + e->staged + n < e->chunk) {
+      if (e->staged + n > kStage) {   // a full stage goes to the device first
+        if ((rc = flush_stage(e, dev, st))) return rc;
+        CK(hipStreamSynchronize(st));
+      }
+      memcpy(e->stage + e->staged, in[i].data, n);
+      e->staged += n;
+      continue;
+    }
+    if ((rc = flush_stage(e, dev, st)) || (rc = encoder_room(e, dev, e->hist + e->pend + n, st))) return rc;
+    if (n) CK(hipMemcpyAsync(e->buf[e->cur] + e->hist + e->pend, in[i].data, n, hipMemcpyHostToDevice, st));
+    e->pend += n;
+    copied = true;
   }
+  if (copied) CK(hipStreamSynchronize(st));   // (the caller's buffers and the stages are free again)
   // encoders with a full chunk pending, grouped by options, one launch sequence per group
-  std::vector<bool> done(k, false);
+  std::vector<bool> done(k, false), ran(k, false);
+  std::vector<mib_encoder *> run;
+  std::vector<uint64_t> ns;
+  std::vector<mib_buf *> outs;
   for (size_t i = 0; i < k; i++) {
     if (done[i]) continue;
     run.clear();
     ns.clear();
-    idx.clear();
+    outs.clear();
     for (size_t j = i; j < k; j++) {
       mib_encoder *e = es[j];
       if (done[j] || !same_opts(e->opts, es[i]->opts)) continue;
       done[j] = true;
-      if (e->pending.size() < e->chunk) continue;
+      if (e->pend < e->chunk) continue;
       run.push_back(e);
-      ns.push_back(e->pending.size() / e->block * e->block);
-      idx.push_back(j);
+      ns.push_back(e->pend / e->block * e->block);
+      outs.push_back(&out[j]);
+      ran[j] = true;
     }
     if (run.empty()) continue;
-    std::vector<std::vector<uint8_t>> acc(run.size());
     std::unique_ptr<bool[]> fin(new bool[run.size()]());
-    int rc = encoder_run(run.data(), ns.data(), fin.get(), run.size(), acc.data());
+    int rc = encoder_run(c, run.data(), ns.data(), fin.get(), run.size(), outs.data());
     if (rc) return rc;
-    for (size_t q = 0; q < run.size(); q++) accs[idx[q]].swap(acc[q]);
   }
-  for (size_t i = 0; i < k; i++) {
-    int rc = take_acc(accs[i], &out[i]);
+  for (size_t i = 0; i < k; i++) {   // the others: no bytes yet
+    if (ran[i]) continue;
+    int rc = mib_buf_from_device(&out[i], nullptr, 0);
     if (rc) return rc;
   }
   return 0;
@@ -1007,15 +1062,20 @@ int mib_encoder_finish(mib_encoder *e, mib_buf *out) {
   if (!e || !out) return MIB_E_INVALID_ARG;
   out->data = nullptr;
   out->size = 0;
-  std::vector<uint8_t> acc;
-  if (!e->finished) {
-    const uint64_t n = e->pending.size();
-    const bool fin = true;
-    int rc = encoder_run(&e, &n, &fin, 1, &acc);
-    if (rc) return rc;
-    e->finished = true;
-  }
-  return take_acc(acc, out);
+  if (e->finished) return mib_buf_from_device(out, nullptr, 0);
+  DefaultLock use;
+  mib_ctx *c = mib_default_ctx();
+  if (!c) return MIB_E_NO_DEVICE;
+  const int dev = mib_ctx_device_of(c);
+  CK(hipSetDevice(dev));
+  hipStream_t st = (hipStream_t)mib_ctx_stream_of(c);
+  int rc;
+  if ((rc = flush_stage(e, dev, st)) || (rc = encoder_room(e, dev, e->hist + e->pend, st))) return rc;
+  const uint64_t n = e->pend;
+  const bool fin = true;
+  if ((rc = encoder_run(c, &e, &n, &fin, 1, &out))) return rc;
+  e->finished = true;
+  return 0;
 }
 
 void mib_encoder_free(mib_encoder *e) {
@@ -1026,6 +1086,10 @@ void mib_encoder_free(mib_encoder *e) {
       if (e->buf[b]) hipFree(e->buf[b]);
     if (e->tab) hipFree(e->tab);
     e->ddict.release();
+  }
+  if (e->stage) {
+    hipHostFree(e->stage);
+    g_stage_bytes.fetch_sub(kStage);
   }
   delete e;
 }

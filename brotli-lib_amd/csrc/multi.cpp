@@ -17,6 +17,10 @@
 
 #include "../../include/brotli_amd.h"
 
+// runtime.cpp: result buffers from device memory (mib_set_allocator's allocator)
+extern "C" int mib_buf_from_device(mib_buf *out, const void *d_src, uint64_t len);
+extern "C" int mib_bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len);
+
 namespace {
 
 constexpr int kMaxShards = 64;
@@ -73,17 +77,16 @@ int encode_shard(mib_ctx *c, const mib_span *in, const std::vector<size_t> &idx,
     if (in[idx[q]].size && hipMemcpy(din.u8() + ioff[q], in[idx[q]].data, in[idx[q]].size, hipMemcpyHostToDevice) != hipSuccess)
       return MIB_E_NO_DEVICE;
   if ((rc = mib_ctx_encode(c, o, din.u8(), ioff.data(), k, dout.u8(), cap, ooff.data(), nullptr))) return rc;
-  std::vector<uint8_t> host(ooff[k]);
-  if (ooff[k] && hipMemcpy(host.data(), dout.u8(), ooff[k], hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
+  std::vector<mib_buf *> outs(k);
+  std::vector<const uint8_t *> src(k);
+  std::vector<uint64_t> lens(k);
   for (size_t q = 0; q < k; q++) {
-    const uint64_t len = ooff[q + 1] - ooff[q];
-    mib_buf &b = out[idx[q]];
-    b.data = (uint8_t *)malloc(len ? len : 1);
-    if (!b.data) return MIB_E_OUT_OF_MEMORY;
-    b.size = len;
-    if (len) memcpy(b.data, host.data() + ooff[q], len);
+    outs[q] = &out[idx[q]];
+    src[q] = dout.u8() + ooff[q];
+    lens[q] = ooff[q + 1] - ooff[q];
     status[idx[q]] = 0;
   }
+  if ((rc = mib_bufs_from_device(k, outs.data(), src.data(), lens.data()))) return rc;
   return 0;
 }
 
@@ -114,11 +117,7 @@ int decode_shard(mib_ctx *c, const mib_span *in, const std::vector<size_t> &idx,
     const size_t i = idx[q];
     status[i] = st[q];
     if (st[q] == 0) {
-      const uint64_t len = (uint64_t)sizes[q];
-      out[i].data = (uint8_t *)malloc(len ? len : 1);
-      if (!out[i].data) return MIB_E_OUT_OF_MEMORY;
-      out[i].size = len;
-      if (len && hipMemcpy(out[i].data, dout.u8() + ooff[q], len, hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
+      if ((rc = mib_buf_from_device(&out[i], dout.u8() + ooff[q], (uint64_t)sizes[q]))) return rc;
     } else if (st[q] == MIB_E_NEED_SPACE) {
       status[i] = mib_decode(in[i].data, in[i].size, nullptr, 0, -1, -1, &out[i]);   // the growing single-stream path
     }

@@ -403,8 +403,65 @@ const char *mib_strerror(int code) {
   return buf;
 }
 
+static mib_alloc_func g_alloc = nullptr;
+static mib_free_func g_free = nullptr;
+static void *g_opaque = nullptr;
+
+void mib_set_allocator(mib_alloc_func alloc_func, mib_free_func free_func, void *opaque) {
+  const bool both = alloc_func && free_func;
+  g_alloc = both ? alloc_func : nullptr;
+  g_free = both ? free_func : nullptr;
+  g_opaque = both ? opaque : nullptr;
+}
+
+uint8_t *mib_buf_alloc(size_t n) {
+  return (uint8_t *)(g_alloc ? g_alloc(g_opaque, n) : malloc(n ? n : 1));
+}
+
+int mib_buf_from_device(mib_buf *out, const void *d_src, uint64_t len) {
+  out->data = mib_buf_alloc(len);
+  out->size = 0;
+  if (!out->data) return MIB_E_OUT_OF_MEMORY;
+  out->size = len;
+  if (len && hipMemcpy(out->data, d_src, len, hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
+  return 0;
+}
+
+int mib_bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len) {
+  if (!k) return 0;
+  const uint8_t *lo = d_src[0], *hi = d_src[0];
+  uint64_t sum = 0;
+  for (size_t i = 0; i < k; i++) {
+    lo = std::min(lo, d_src[i]);
+    hi = std::max(hi, d_src[i] + len[i]);
+    sum += len[i];
+  }
+  // large results: one copy each, straight into the result buffer; many small ones: one copy
+  // of the span that holds them all, then host copies (a copy call costs ~10 us)
+  if (sum / k >= (256u << 10) || (uint64_t)(hi - lo) > 4 * sum + (1u << 20)) {
+    for (size_t i = 0; i < k; i++) {
+      const int rc = mib_buf_from_device(outs[i], d_src[i], len[i]);
+      if (rc) return rc;
+    }
+    return 0;
+  }
+  std::vector<uint8_t> host(hi - lo);
+  if (hipMemcpy(host.data(), lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
+  for (size_t i = 0; i < k; i++) {
+    outs[i]->data = mib_buf_alloc(len[i]);
+    outs[i]->size = 0;
+    if (!outs[i]->data) return MIB_E_OUT_OF_MEMORY;
+    outs[i]->size = len[i];
+    if (len[i]) memcpy(outs[i]->data, host.data() + (d_src[i] - lo), len[i]);
+  }
+  return 0;
+}
+
 void mib_buf_free(mib_buf *b) {
-  if (b && b->data) free(b->data);
+  if (b && b->data) {
+    if (g_free) g_free(g_opaque, b->data);
+    else free(b->data);
+  }
   if (b) {
     b->data = nullptr;
     b->size = 0;
@@ -759,11 +816,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
       ps[0] = PartStream{d_in, n, d_out, &plan, d_dict, dict ? dict_n : 0};
       rc = decode_parts(c, ps, ok, c->stream);
       if (rc == 0 && ok[0]) {
-        const uint64_t len = (uint64_t)plan.total;
-        out->data = (uint8_t *)malloc(len);
-        out->size = len;
-        if (hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost) != hipSuccess) rc = MIB_E_NO_DEVICE;
-        return rc;
+        return mib_buf_from_device(out, d_out, (uint64_t)plan.total);
       }
       rc = 0;
     }
@@ -798,13 +851,11 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
     }
     if (rc == 0) {
       uint64_t len = (uint64_t)jobs[0].result_len;
-      out->data = (uint8_t *)malloc(len ? len : 1);
-      out->size = len;
-      if (len) hipMemcpy(out->data, d_out, len, hipMemcpyDeviceToHost);
       if (max_out >= 0 && (int64_t)len > max_out) {   // the header can lie about the size (decode.ts:57-62)
-        mib_buf_free(out);
         out->size = len;
         rc = MIB_E_OUTPUT_LIMIT;
+      } else {
+        rc = mib_buf_from_device(out, d_out, len);
       }
     }
     break;
@@ -845,15 +896,18 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
   }
   rc = decode_jobs(c, jobs, c->stream);
   if (rc == 0) {
+    std::vector<mib_buf *> outs;
+    std::vector<const uint8_t *> src;
+    std::vector<uint64_t> lens;
     for (size_t i = 0; i < k; i++) {
       status[i] = jobs[i].status;
       if (jobs[i].status == 0) {
-        uint64_t len = (uint64_t)jobs[i].result_len;
-        out[i].data = (uint8_t *)malloc(len ? len : 1);
-        out[i].size = len;
-        if (len) hipMemcpy(out[i].data, d_out + ooff[i], len, hipMemcpyDeviceToHost);
+        outs.push_back(&out[i]);
+        src.push_back(d_out + ooff[i]);
+        lens.push_back((uint64_t)jobs[i].result_len);
       }
     }
+    if ((rc = mib_bufs_from_device(outs.size(), outs.data(), src.data(), lens.data()))) return rc;
     // then (the staging buffers are reused) the streams that outgrew their slots, alone
     // through the growing single-stream path
     for (size_t i = 0; i < k; i++)

@@ -542,7 +542,7 @@ extern "C" int mib_woff2_transform_glyf(const uint8_t *ttf, size_t n, mib_buf *o
     put16(&host[4], ng);
     put16(&host[6], long_loca ? 1 : 0);
     for (int s = 0; s < kStreams; s++) put32(&host[8 + 4 * s], tot[s]);
-    out->data = (uint8_t *)malloc(total);
+    out->data = mib_buf_alloc(total);
     if (!out->data) {
       rc = MIB_E_OUT_OF_MEMORY;
       break;
@@ -627,15 +627,15 @@ extern "C" int mib_woff2_transform_hmtx(const uint8_t *ttf, size_t n, mib_buf *o
       break;
     }
     hipLaunchKernelGGL(hmtx_write_kernel, grid, block, 0, st, ng, d_font + gl + ll, nhm, keep, d_out);
-    out->data = (uint8_t *)malloc(total);
+    out->data = mib_buf_alloc(total);
     if (!out->data) {
       rc = MIB_E_OUT_OF_MEMORY;
       break;
     }
+    out->size = total;
     hipMemcpyAsync(out->data, d_out, total, hipMemcpyDeviceToHost, st);
     if (hipStreamSynchronize(st) != hipSuccess) {
-      free(out->data);
-      out->data = nullptr;
+      mib_buf_free(out);
       rc = MIB_E_NO_DEVICE;
       break;
     }

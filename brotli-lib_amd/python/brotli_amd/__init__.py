@@ -58,6 +58,42 @@ class _KTime(ctypes.Structure):
 
 _lib = None
 
+# Results come back as bytes objects the library writes into (mib_set_allocator): the device
+# copies its output straight into the object returned, no copy through a C buffer.
+_ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_FREE_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = [ctypes.c_char_p, ctypes.c_ssize_t]
+_results = {}   # address -> the bytes object the library is filling / has filled
+_HUGE = 2 << 20
+_madvise = ctypes.CDLL(None, use_errno=True).madvise
+_madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+
+
+def _alloc(opaque, size):
+    try:
+        b = _new_bytes(None, max(1, size))   # (a fresh object: b'' is a shared singleton)
+    except MemoryError:
+        return None
+    addr = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value
+    _results[addr] = b
+    if size >= _HUGE and os.environ.get('MIB_PY_HUGEPAGE') != '0':
+        # large results: the copy into fresh memory is page-fault bound; 2 MiB pages fault 512x less
+        lo = (addr + _HUGE - 1) & ~(_HUGE - 1)
+        hi = (addr + size) & ~(_HUGE - 1)
+        if hi > lo:
+            _madvise(lo, hi - lo, 14)   # MADV_HUGEPAGE
+    return addr
+
+
+def _free(opaque, addr):
+    _results.pop(addr, None)
+
+
+_alloc_cb = _ALLOC_FN(_alloc)
+_free_cb = _FREE_FN(_free)
+
 
 def _L():
     global _lib
@@ -113,6 +149,8 @@ def _L():
         lib.mib_part_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         lib.mib_default_ctx.restype = ctypes.c_void_p
         lib.mib_ctx_clear_times.argtypes = [ctypes.c_void_p]
+        lib.mib_set_allocator.argtypes = [_ALLOC_FN, _FREE_FN, ctypes.c_void_p]
+        lib.mib_set_allocator(_alloc_cb, _free_cb, None)
         _lib = lib
     return _lib
 
@@ -123,9 +161,12 @@ def _err(code, what=''):
 
 
 def _take(buf):
-    data = ctypes.string_at(buf.data, buf.size) if buf.size else b''
-    _L().mib_buf_free(ctypes.byref(buf))
-    return data
+    addr = ctypes.cast(buf.data, ctypes.c_void_p).value
+    b = _results.pop(addr, None) if addr else None
+    if b is None:
+        return b''
+    buf.data = None
+    return b if len(b) == buf.size else b[:buf.size]
 
 
 def _opts(options):
@@ -150,6 +191,30 @@ def _opts(options):
     return o
 
 
+def _in(x):
+    """(argument, length, keep-alive) for an input buffer, without copying it: bytes as is,
+    any other C-contiguous buffer (bytearray, memoryview slices, numpy, array) by address."""
+    if isinstance(x, bytes):
+        return x, len(x), x
+    try:
+        mv = memoryview(x)
+    except TypeError:
+        b = bytes(bytearray(x))
+        return b, len(b), b
+    if not mv.c_contiguous:
+        b = mv.tobytes()
+        return b, len(b), b
+    import numpy as np
+    a = np.frombuffer(mv.cast('B') if mv.format != 'B' or mv.ndim != 1 else mv, dtype=np.uint8)
+    if a.size == 0:
+        return b'', 0, a
+    return ctypes.c_char_p(a.ctypes.data), a.size, a
+
+
+def _addr(arg):
+    return ctypes.cast(arg if isinstance(arg, ctypes.c_char_p) else ctypes.c_char_p(arg), ctypes.c_void_p)
+
+
 def _bytes(x):
     """Uint8Array / Int8Array equivalents: any buffer (bytes, bytearray, memoryview, array('b'),
     numpy int8/uint8) is taken as its raw bytes, as decode.ts:31-33 views an Int8Array."""
@@ -162,9 +227,9 @@ def _bytes(x):
 
 
 def brotliEncode(input, options=None):
-    data = _bytes(input)
+    data, n, _keep = _in(input)
     buf = _Buf()
-    rc = _L().mib_encode(data, len(data), ctypes.byref(_opts(options)), ctypes.byref(buf))
+    rc = _L().mib_encode(data, n, ctypes.byref(_opts(options)), ctypes.byref(buf))
     if rc:
         raise _err(rc)
     return _take(buf)
@@ -179,9 +244,9 @@ class BrotliEncoder:
             raise BrotliError('brotli_amd: encoder creation failed')
 
     def update(self, chunk):
-        data = _bytes(chunk)
+        data, n, _keep = _in(chunk)
         buf = _Buf()
-        rc = _L().mib_encoder_update(self._h, data, len(data), ctypes.byref(buf))
+        rc = _L().mib_encoder_update(self._h, data, n, ctypes.byref(buf))
         if rc:
             raise _err(rc)
         return _take(buf)
@@ -203,9 +268,9 @@ def encoder_update_batch(encoders, chunks):
     """Advance independent BrotliEncoders by one chunk each in one GPU launch sequence;
     returns each encoder's update() result."""
     k = len(encoders)
-    keep = [_bytes(b) for b in chunks]
+    keep = [_in(b) for b in chunks]
     hs = (ctypes.c_void_p * k)(*[e._h for e in encoders])
-    spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
+    spans = (_Span * k)(*[_Span(_addr(a), n) for a, n, _ in keep])
     outs = (_Buf * k)()
     rc = _L().mib_encoder_update_batch(hs, spans, k, outs)
     if rc:
@@ -214,13 +279,13 @@ def encoder_update_batch(encoders, chunks):
 
 
 def brotliDecodedSize(data):
-    data = _bytes(data)
-    return int(_L().mib_decoded_size(data, len(data)))
+    data, n, _keep = _in(data)
+    return int(_L().mib_decoded_size(data, n))
 
 
 def brotliDecode(buffer, options=None):
     """decode.ts:18-65: options = {'maxOutputSize', 'customDictionary'} or a legacy int size."""
-    data = _bytes(buffer)
+    data, n, _keep = _in(buffer)
     exact, max_out, dic = -1, -1, None
     if isinstance(options, int) and not isinstance(options, bool):
         exact = options
@@ -230,7 +295,7 @@ def brotliDecode(buffer, options=None):
         if options.get('customDictionary') is not None:
             dic = _bytes(options['customDictionary'])
     buf = _Buf()
-    rc = _L().mib_decode(data, len(data), dic, len(dic) if dic is not None else 0, max_out, exact, ctypes.byref(buf))
+    rc = _L().mib_decode(data, n, dic, len(dic) if dic is not None else 0, max_out, exact, ctypes.byref(buf))
     if rc == -103:   # MIB_E_OUTPUT_LIMIT: the reference's wrapper message
         raise BrotliError('Decompressed size %d exceeds limit %d' % (buf.size, max_out), rc)
     if rc:
@@ -242,8 +307,8 @@ def encode_batch(buffers, options=None, gpus=None):
     """Encode independent buffers in one GPU launch sequence; returns list of bytes.  gpus:
     shard the batch over that many GPUs (0: every visible one; mib_encode_batch_n)."""
     k = len(buffers)
-    keep = [_bytes(b) for b in buffers]
-    spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
+    keep = [_in(b) for b in buffers]
+    spans = (_Span * k)(*[_Span(_addr(a), n) for a, n, _ in keep])
     outs = (_Buf * k)()
     st = (ctypes.c_int * k)()
     if gpus is None:
@@ -252,11 +317,10 @@ def encode_batch(buffers, options=None, gpus=None):
         rc = _L().mib_encode_batch_n(spans, k, ctypes.byref(_opts(options)), int(gpus), outs, st)
     if rc:
         raise _err(rc)
-    res = []
+    res = [_take(outs[i]) for i in range(k)]
     for i in range(k):
         if st[i]:
             raise _err(st[i])
-        res.append(_take(outs[i]))
     return res
 
 
@@ -264,8 +328,8 @@ def decode_batch(buffers, gpus=None):
     """Decode independent streams on the GPU; returns a list of bytes or BrotliError.  gpus:
     shard the batch over that many GPUs (0: every visible one; mib_decode_batch_n)."""
     k = len(buffers)
-    keep = [_bytes(b) for b in buffers]
-    spans = (_Span * k)(*[_Span(ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p), len(b)) for b in keep])
+    keep = [_in(b) for b in buffers]
+    spans = (_Span * k)(*[_Span(_addr(a), n) for a, n, _ in keep])
     outs = (_Buf * k)()
     st = (ctypes.c_int * k)()
     if gpus is None:
@@ -297,6 +361,7 @@ def woff2_transform_hmtx(ttf):
     if rc:
         raise _err(rc)
     if not buf.size:
+        _L().mib_buf_free(ctypes.byref(buf))
         return None
     return _take(buf)
 

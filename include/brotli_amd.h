@@ -108,6 +108,15 @@ int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, i
 int mib_device_count(void);
 
 void mib_buf_free(mib_buf *b);
+/* The allocator behind every mib_buf the library returns (default malloc / free), in the
+ * convention of brotli's own C API (brotli_alloc_func / brotli_free_func with an opaque
+ * pointer, c/include/brotli/types.h): a binding can hand results over without a copy (the
+ * Python mirror allocates its bytes objects this way).  Process-wide; set it before any
+ * other call and free every buffer with the allocator that made it.  NULL, NULL: malloc /
+ * free again.  alloc may return NULL (MIB_E_OUT_OF_MEMORY). */
+typedef void *(*mib_alloc_func)(void *opaque, size_t size);
+typedef void (*mib_free_func)(void *opaque, void *address);
+void mib_set_allocator(mib_alloc_func alloc_func, mib_free_func free_func, void *opaque);
 
 /* ---- device-resident batches (inputs already in HBM; used by bench.py and the
  *      multi-GPU driver).  d_* are device pointers on the context's device; offsets are
