@@ -88,6 +88,14 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint32_t hq;              // quality >= 10 (context mode rule)
 };
 
+// Per 64 KiB of global positions: where its stream's bytes are, so the match finder's gather
+// needs one lookup, not the segment's stream and then its Job (a dependent pair of loads)
+struct SegRef {
+  const uint8_t *base;      // the stream's data - pos_base (byte of global position g: base + g)
+  uint32_t pos_base;        // the stream's first global position
+  uint32_t end;             // pos_base + its length (0 bytes for an uncompressed stream)
+};
+
 // Custom-dictionary copies (mib_enc_opts.dict; the reference decoder's compound dictionary,
 // engine.ts:142-159,903-1011).  A copy of length L at stream position p with distance
 // d = min(p, max backward distance) + L is read by the decoder from dictionary offset
@@ -434,8 +442,9 @@ struct ItemMap {
 void launch_dict_matches(hipStream_t st, const Job *jobs, int njobs, uint32_t span, const uint32_t *dict_tab,
                          const uint8_t *dict_data, uint32_t *matches);
 void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, uint32_t *matches);
-void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
-                         const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches);
+void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
+                         const uint32_t *skeys, const uint32_t *svals, uint32_t total, int depth, uint32_t max_dist,
+                         bool hist, bool parts, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total);

@@ -89,9 +89,9 @@ __device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, 
 // kHist: streaming chunks with a history table; kParts: some stream carries a part index
 // (lagging external sources) -- separate builds of the walk
 template <bool kHist, bool kParts>
-__global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const uint32_t *sorted_keys,
-                                                             const uint32_t *sorted_vals, uint32_t total, int depth,
-                                                             uint32_t *matches) {
+__global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
+                                                             const uint32_t *sorted_keys, const uint32_t *sorted_vals,
+                                                             uint32_t total, int depth, uint32_t max_dist, uint32_t *matches) {
   __shared__ uint32_t skey[kTile + kBack];
   __shared__ uint32_t spos[kTile + kBack];
   __shared__ uint64_t spre[kPreW][kTile + kBack];
@@ -104,9 +104,8 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       key = sorted_keys[r];
       g = sorted_vals[r];
       if ((key & kInvalidKey) == 0) {
-        const Job &jb = jobs[pos_job[g >> kSegBits]];
-        uint32_t p = g - jb.pos_base;
-        load_prefix32(jb.data + p, jb.n - p, pre);
+        const SegRef sr = seg_ref[g >> kSegBits];
+        load_prefix32(sr.base + g, sr.end - g, pre);
       }
     }
     skey[t] = key;
@@ -121,14 +120,15 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
   const uint32_t key = skey[me], g = spos[me];
   int cnt = 0;
   if ((key & kInvalidKey) == 0) {
-    const Job &jb = jobs[pos_job[g >> kSegBits]];
-    const uint32_t p = g - jb.pos_base;
-    const uint32_t max_dist = (1u << jb.lgwin) - 16;
-    const uint32_t seg_end = min(((p >> kSegBits) + 1) << kSegBits, jb.n);
-    const uint32_t limit = seg_end - p;   // copies never cross a parse segment
-    const uint8_t *cur = jb.data + p;
+    const SegRef sr = seg_ref[g >> kSegBits];
+    const uint32_t p = g - sr.pos_base;
+    // (pos_base is a multiple of the segment: the segment's end in global positions)
+    const uint32_t limit = min(((g >> kSegBits) + 1) << kSegBits, sr.end) - g;   // copies never cross a parse segment
+    const uint8_t *cur = sr.base + g;
+    const Job &jb = jobs[(kHist || kParts) ? pos_job[g >> kSegBits] : 0];   // (the streaming / part-index fields)
     const bool parts = kParts && jb.parts;
-    const uint32_t pA = jb.abs_base + p, pbits = kParts ? jb.part_bits : 16u, plag = kParts ? jb.part_lag : 0u;
+    const uint32_t pA = (kHist || kParts) ? jb.abs_base + p : 0u, pbits = kParts ? jb.part_bits : 16u,
+                   plag = kParts ? jb.part_lag : 0u;
     uint32_t best = 3;
     uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
     if constexpr (!kHist) {
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       const int dmax = min(depth, kBack);
       for (int t = 1; t <= dmax; t++) {
         const int e = me - t;
-        if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
+        if (skey[e] != key || spos[e] < sr.pos_base) break;   // bucket or stream changes
         const uint32_t d = g - spos[e];
         if (d > max_dist || best >= limit) break;
         const uint32_t pc = parts ? part_cap(pA, d, pbits, plag) : ~0u;   // part index: lagging source
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       bool stop = false;
       for (; t <= dmax; t++) {
         const int e = me - t;
-        if (skey[e] != key || spos[e] < jb.pos_base) break;   // bucket or stream changes
+        if (skey[e] != key || spos[e] < sr.pos_base) break;   // bucket or stream changes
         const uint32_t d = g - spos[e];
         if (d > max_dist || best >= limit) {
           stop = true;
@@ -385,17 +385,18 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
   const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total / 4 + 255) / 256);
   hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, hb, keys, vals);
 }
-void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
-                         const uint32_t *svals, uint32_t total, int depth, bool hist, bool parts, uint32_t *matches) {
+void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
+                         const uint32_t *skeys, const uint32_t *svals, uint32_t total, int depth, uint32_t max_dist,
+                         bool hist, bool parts, uint32_t *matches) {
   const dim3 g((total + kTile - 1) / kTile), b(kTile);
-  if (hist && parts)
-    hipLaunchKernelGGL((find_matches_kernel<true, true>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
-  else if (hist)
-    hipLaunchKernelGGL((find_matches_kernel<true, false>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
-  else if (parts)
-    hipLaunchKernelGGL((find_matches_kernel<false, true>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
-  else
-    hipLaunchKernelGGL((find_matches_kernel<false, false>), g, b, 0, st, jobs, pos_job, skeys, svals, total, depth, matches);
+#define MIB_FM(H, P)                                                                                                   \
+  hipLaunchKernelGGL((find_matches_kernel<H, P>), g, b, 0, st, jobs, pos_job, seg_ref, skeys, svals, total, depth, \
+                     max_dist, matches)
+  if (hist && parts) MIB_FM(true, true);
+  else if (hist) MIB_FM(true, false);
+  else if (parts) MIB_FM(false, true);
+  else MIB_FM(false, false);
+#undef MIB_FM
 }
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total) {

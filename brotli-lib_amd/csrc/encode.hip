@@ -297,6 +297,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   std::vector<Seg> segs;
   std::vector<Mb> mbs;
   std::vector<uint32_t> seg_job;   // per 64 KiB of global positions: its stream
+  std::vector<SegRef> seg_ref;     // ... and where its bytes are
   uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0;
   bool any_hist = false, any_parts = false, any_dict = false, any_cdict = false;
   for (size_t j = 0; j < k; j++) {
@@ -374,7 +375,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.nseg = (uint32_t)segs.size() - jb.seg_base;
     jb.nmb = (uint32_t)mbs.size() - jb.mb_base;
     const uint64_t span = ((n + kSeg - 1) / kSeg) * kSeg + kSeg;   // + a spare segment: end node, padding
-    for (uint64_t q = 0; q < span / kSeg; q++) seg_job.push_back((uint32_t)j);
+    for (uint64_t q = 0; q < span / kSeg; q++) {
+      seg_job.push_back((uint32_t)j);
+      seg_ref.push_back(SegRef{jb.data - (uintptr_t)pos_total, (uint32_t)pos_total, (uint32_t)(pos_total + (jb.uncompressed ? 0 : n))});
+    }
     pos_total += span;
     jb.out_off = out_scratch;
     jb.out_cap = n + n / 8 + 4096 + idx_extra;
@@ -386,10 +390,11 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   const size_t nm1 = std::max<size_t>(1, mbs.size()), ns1 = std::max<size_t>(1, segs.size());
 
   const uint64_t last_job = k ? k - 1 : 0;
-  int gshift = 0;   // stream groups of the sort key: at most 2^kGroupKeyBits of them
-  while ((last_job >> gshift) >= (1u << kGroupKeyBits)) gshift++;
+  static const int gbits = (int)env_u32("MIB_GROUP_BITS", kGroupKeyBits, 0, 12);
+  int gshift = 0;   // stream groups of the sort key: at most 2^gbits of them
+  while ((last_job >> gshift) >= (1u << gbits)) gshift++;
   int key_bits = kHashBits + 1;
-  while (key_bits < (int)kHashBits + 1 + kGroupKeyBits && ((last_job >> gshift) >> (key_bits - kHashBits - 1)) != 0) key_bits++;
+  while (key_bits < (int)kHashBits + 1 + gbits && ((last_job >> gshift) >> (key_bits - kHashBits - 1)) != 0) key_bits++;
   size_t sort_tmp = 0;
   CK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                         (uint32_t *)nullptr, (int)total, 0, key_bits, st));
@@ -398,7 +403,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += (size_t)total * kMatchRec * 4;
   need += ((size_t)total + 1) * 8;
   need += cmd_total * (sizeof(RawCmd) + sizeof(Cmd) + 4);
-  need += k * (sizeof(Job) + 1024 + 8) + ns1 * sizeof(Seg) + seg_job.size() * 4;
+  need += k * (sizeof(Job) + 1024 + 8) + ns1 * sizeof(Seg) + seg_job.size() * (4 + sizeof(SegRef)) + 256;
   need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + kTreeSlots * kTreeBytes + 4 * (kLitSlots * 256 + kMaxBT * 704 + kMaxBT * kDistCtx * 128));
   need += ns1 * kSubPerSeg * (sizeof(Unit) + kSubHist * 4);
   need += out_scratch + 64;
@@ -433,6 +438,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   Seg *d_segs = ar.take<Seg>(ns1);
   Mb *d_mbs = ar.take<Mb>(nm1);
   uint32_t *d_seg_job = ar.take<uint32_t>(seg_job.size());
+  SegRef *d_seg_ref = ar.take<SegRef>(seg_ref.size());
   uint32_t *lit_h = ar.take<uint32_t>(k * 256);
   uint32_t *hl = ar.take<uint32_t>(nm1 * kLitSlots * 256);
   uint32_t *hc = ar.take<uint32_t>(nm1 * kMaxBT * 704);
@@ -467,6 +473,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   Seg *const d_fin = ps ? d_pieces : d_segs;   // the final parse's segment table
   const int nfin = nsegs << ps;
   CK(hipMemcpyAsync(d_seg_job, seg_job.data(), seg_job.size() * 4, hipMemcpyHostToDevice, st));
+  CK(hipMemcpyAsync(d_seg_ref, seg_ref.data(), seg_ref.size() * sizeof(SegRef), hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
   if (nsegs) {
     CK(hipMemsetAsync(lit_h, 0, k * 256 * 4, st));
@@ -484,7 +491,8 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.start("find_matches");
     const DictDev *dd = any_dict ? dict_device(mib_ctx_device_of(ctx)) : nullptr;
     if (any_dict && !dd) return MIB_E_OUT_OF_MEMORY;
-    launch_find_matches(st, d_jobs, d_seg_job, skeys, svals, total, depth, any_hist, any_parts, matches);
+    launch_find_matches(st, d_jobs, d_seg_job, d_seg_ref, skeys, svals, total, depth, (1u << prm.lgwin) - 16, any_hist,
+                        any_parts, matches);
     if (dd) launch_dict_matches(st, d_jobs, (int)k, dict_span(), dd->tab, dd->data, matches);
     if (any_cdict) launch_cdict_matches(st, d_jobs, d_seg_job, total, matches);
     if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
