@@ -18,8 +18,12 @@ namespace enc {
 // path of encode.ts:240-262).  Also the decoder's last distance at each segment start: the
 // distance ring's slot 0 always holds the previous copy's distance (a code-0 command does not
 // push, but reuses exactly that distance), so code 0 is decidable per segment in parallel.
-__global__ void carry_kernel(Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
+//
+// Wave per stream, 64 segments per step: both are prefix scans over the metablock's segments
+// (carry: a segment with copies resets it to its trailing literals, one without adds them; last
+// distance: a segment with copies sets it).
+__global__ __launch_bounds__(64) void carry_kernel(Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
+  const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= njobs) return;
   Job &jb = jobs[j];
   if (jb.uncompressed) return;
@@ -27,19 +31,48 @@ __global__ void carry_kernel(Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
   for (uint32_t m = 0; m < jb.nmb; m++) {
     const Mb &mb = mbs[jb.mb_base + m];
     uint32_t carry = 0;
-    for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
-      Seg &sg = segs[s];
-      sg.carry_in = carry;
-      sg.prev_dist = pd;
-      sg.extra_ins = 0;
-      if (sg.ncmd) {
-        carry = sg.tail_lits;
-        pd = sg.last_dist;
-      } else {
-        carry += sg.tail_lits;
+    const uint32_t end = mb.first_seg + mb.nseg;
+    for (uint32_t c0 = mb.first_seg; c0 < end; c0 += 64) {
+      const uint32_t s = c0 + lane;
+      const bool live = s < end;
+      uint32_t ncmd = 0, tail = 0, last = 0;
+      if (live) {
+        ncmd = segs[s].ncmd;
+        tail = segs[s].tail_lits;
+        last = segs[s].last_dist;
       }
+      // (reset?, value) summaries, composed by an inclusive wave scan
+      uint32_t cr = ncmd ? 1u : 0u, cv = tail, pr = cr, pv = last;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t ycr = (uint32_t)__shfl_up((int)cr, o), ycv = (uint32_t)__shfl_up((int)cv, o);
+        const uint32_t ypr = (uint32_t)__shfl_up((int)pr, o), ypv = (uint32_t)__shfl_up((int)pv, o);
+        if (lane >= o) {
+          if (!cr) {
+            cv += ycv;
+            cr = ycr;
+          }
+          if (!pr) {
+            pv = ypv;
+            pr = ypr;
+          }
+        }
+      }
+      uint32_t ecr = (uint32_t)__shfl_up((int)cr, 1), ecv = (uint32_t)__shfl_up((int)cv, 1);
+      uint32_t epr = (uint32_t)__shfl_up((int)pr, 1), epv = (uint32_t)__shfl_up((int)pv, 1);
+      if (lane == 0) ecr = ecv = epr = epv = 0;
+      if (live) {
+        Seg &sg = segs[s];
+        sg.carry_in = ecr ? ecv : carry + ecv;
+        sg.prev_dist = epr ? epv : pd;
+        sg.extra_ins = 0;
+      }
+      const uint32_t lcr = (uint32_t)__shfl((int)cr, 63), lcv = (uint32_t)__shfl((int)cv, 63);
+      const uint32_t lpr = (uint32_t)__shfl((int)pr, 63), lpv = (uint32_t)__shfl((int)pv, 63);
+      carry = lcr ? lcv : carry + lcv;
+      pd = lpr ? lpv : pd;
     }
-    if (carry) segs[mb.first_seg + mb.nseg - 1].extra_ins = carry;
+    if (carry && lane == 0) segs[end - 1].extra_ins = carry;
   }
 }
 
@@ -1455,24 +1488,37 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
   if (t == 0) sg.bits = total;
 }
 
-// ---------------------------------------------------------------- offsets: lane per stream
-__global__ void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
-  int j = blockIdx.x * blockDim.x + threadIdx.x;
+// ---------------------------------------------------------------- offsets: wave per stream
+// Bit offsets of the metablocks and segments: prefix sums of the sizes, 64 segments a step.
+__global__ __launch_bounds__(64) void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
+  const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= njobs) return;
   Job &jb = jobs[j];
   if (jb.uncompressed) return;
   uint64_t pos = jb.parts ? jb.idx_bits : 0;   // window bits + part index block first
   for (uint32_t m = 0; m < jb.nmb; m++) {
     Mb &mb = mbs[jb.mb_base + m];
-    mb.bit_off = pos;
-    pos += mb.hdr_bits;
-    for (int q = 0; q < kTreeSlots; q++) pos += mb.tree_bits[q];
-    for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
-      segs[s].bit_off = pos;
-      pos += segs[s].bits;
+    if (lane == 0) mb.bit_off = pos;
+    uint64_t hb = lane < kTreeSlots ? mb.tree_bits[lane] : 0;
+    for (int q = lane + 64; q < kTreeSlots; q += 64) hb += mb.tree_bits[q];
+    for (int o = 32; o; o >>= 1) hb += __shfl_xor(hb, o);
+    pos += mb.hdr_bits + hb;
+    const uint32_t end = mb.first_seg + mb.nseg;
+    for (uint32_t c0 = mb.first_seg; c0 < end; c0 += 64) {
+      const uint32_t s = c0 + lane;
+      const uint64_t bits = s < end ? segs[s].bits : 0;
+      uint64_t inc = bits;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (s < end) segs[s].bit_off = pos + inc - bits;
+      pos += __shfl(inc, 63);
     }
     if (mb.is_last) pos = (pos + 7) & ~7ull;
   }
+  if (lane != 0) return;
   const uint64_t trailer = pos;
   if (!jb.final_) pos = (pos + 6 + 7) & ~7ull;   // empty metadata block: ISLAST 0, MNIBBLES 0, MSKIPBYTES 0
   // the stored form is never larger than n + 5 bytes per 16 MiB block + window header + tail
@@ -1493,7 +1539,7 @@ __global__ void offsets_kernel(Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t
 
 // ---------------------------------------------------------------- launchers
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs) {
-  hipLaunchKernelGGL(carry_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, mbs);
+  hipLaunchKernelGGL(carry_kernel, dim3(njobs), dim3(64), 0, st, jobs, njobs, segs, mbs);
 }
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
@@ -1554,7 +1600,7 @@ void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int
     hipLaunchKernelGGL(sizes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
 }
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
-  hipLaunchKernelGGL(offsets_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, mbs, segs, out);
+  hipLaunchKernelGGL(offsets_kernel, dim3(njobs), dim3(64), 0, st, jobs, njobs, mbs, segs, out);
 }
 
 }  // namespace enc

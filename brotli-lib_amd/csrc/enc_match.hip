@@ -58,7 +58,6 @@ __global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint3
 // HBM unless a match reaches 32 bytes; only such matches extend through global memory.  The
 // staircase of strictly increasing lengths (shortest distance for each length) is kept,
 // longest last.
-constexpr int kTile = 256;
 constexpr int kBack = 64;
 constexpr int kPreW = 4;   // staged prefix: 4 x 8 bytes
 
@@ -88,7 +87,7 @@ __device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, 
 
 // kHist: streaming chunks with a history table; kParts: some stream carries a part index
 // (lagging external sources) -- separate builds of the walk
-template <bool kHist, bool kParts>
+template <int kTile, bool kHist, bool kParts>
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                                                              const uint32_t *sorted_keys, const uint32_t *sorted_vals,
                                                              uint32_t total, int depth, uint32_t max_dist, uint32_t *matches) {
@@ -388,14 +387,23 @@ void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, 
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                          const uint32_t *skeys, const uint32_t *svals, uint32_t total, int depth, uint32_t max_dist,
                          bool hist, bool parts, uint32_t *matches) {
-  const dim3 g((total + kTile - 1) / kTile), b(kTile);
-#define MIB_FM(H, P)                                                                                                   \
-  hipLaunchKernelGGL((find_matches_kernel<H, P>), g, b, 0, st, jobs, pos_job, seg_ref, skeys, svals, total, depth, \
-                     max_dist, matches)
-  if (hist && parts) MIB_FM(true, true);
-  else if (hist) MIB_FM(true, false);
-  else if (parts) MIB_FM(false, true);
-  else MIB_FM(false, false);
+  // tile of sorted entries per block: each tile also stages the kBack entries before it
+  // (MIB_FM_TILE: experiment knob, 256 / 512 / 1024)
+  static const int tile = getenv("MIB_FM_TILE") ? atoi(getenv("MIB_FM_TILE")) : 256;
+#define MIB_FM(T, H, P)                                                                                                 \
+  hipLaunchKernelGGL((find_matches_kernel<T, H, P>), dim3((total + T - 1) / T), dim3(T), 0, st, jobs, pos_job, seg_ref, \
+                     skeys, svals, total, depth, max_dist, matches)
+#define MIB_FM_T(T)                            \
+  do {                                         \
+    if (hist && parts) MIB_FM(T, true, true);  \
+    else if (hist) MIB_FM(T, true, false);     \
+    else if (parts) MIB_FM(T, false, true);    \
+    else MIB_FM(T, false, false);              \
+  } while (0)
+  if (tile >= 1024) MIB_FM_T(1024);
+  else if (tile >= 512) MIB_FM_T(512);
+  else MIB_FM_T(256);
+#undef MIB_FM_T
 #undef MIB_FM
 }
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,

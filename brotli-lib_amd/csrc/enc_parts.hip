@@ -89,42 +89,108 @@ __global__ __launch_bounds__(64) void raw_push_kernel(const Job *jobs, const Seg
   ps.n = total;
   if (lane == 0) out[blockIdx.x] = ps;
 }
-__global__ void ring_scan_kernel(Job *jobs, int njobs, Seg *segs, const PushSum *push) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// Ring composition: the ring after pushes A then B (B's pushes are the more recent).
+__device__ __forceinline__ PushSum push_then(const PushSum &a, const PushSum &b) {
+  PushSum r;
+  r.n = min(a.n + b.n, 1u << 30);
+#pragma unroll
+  for (uint32_t q = 0; q < 4; q++) r.d[q] = q < b.n ? b.d[q] : a.d[min(q - min(b.n, 4u), 3u)];
+  return r;
+}
+__device__ __forceinline__ PushSum shfl_up_push(const PushSum &x, int o) {
+  PushSum r;
+  r.n = (uint32_t)__shfl_up((int)x.n, o);
+#pragma unroll
+  for (int q = 0; q < 4; q++) r.d[q] = (uint32_t)__shfl_up((int)x.d[q], o);
+  return r;
+}
+// Wave-wide inclusive scan of the 64 lanes' push summaries (lane l: segments ..l composed)
+__device__ __forceinline__ PushSum scan_pushes(PushSum x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const PushSum y = shfl_up_push(x, o);
+    if (lane >= o) x = push_then(y, x);
+  }
+  return x;
+}
+// the ring before a segment: the stream's incoming ring, then the pushes of the segments
+// before it (an exclusive scan; ring as a PushSum with n >= 4)
+__device__ __forceinline__ PushSum push_exclusive(const PushSum &carry, const PushSum &inc, int lane) {
+  PushSum ex = shfl_up_push(inc, 1);
+  if (lane == 0) ex.n = 0;
+  return push_then(carry, ex);
+}
+// Wave per stream, 64 segments per step (a scan of their push summaries).
+__global__ __launch_bounds__(64) void ring_scan_kernel(Job *jobs, int njobs, Seg *segs, const PushSum *push) {
+  const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= njobs) return;
   const Job &jb = jobs[j];
   if (jb.uncompressed) return;
-  uint32_t ring[4];
-  for (int q = 0; q < 4; q++) ring[q] = (uint32_t)jb.dc_in[q];
-  for (uint32_t s = jb.seg_base; s < jb.seg_base + jb.nseg; s++) {
-    for (int q = 0; q < 4; q++) segs[s].ring_in[q] = ring[q];
-    const PushSum &ps = push[s];
-    if (ps.n >= 4) {
-      for (int q = 0; q < 4; q++) ring[q] = ps.d[q];
-    } else if (ps.n) {
-      uint32_t r[4];
-      for (uint32_t q = 0; q < 4; q++) r[q] = q < ps.n ? ps.d[q] : ring[q - ps.n];
-      for (int q = 0; q < 4; q++) ring[q] = r[q];
-    }
+  PushSum carry;
+  carry.n = 4;
+  for (int q = 0; q < 4; q++) carry.d[q] = (uint32_t)jb.dc_in[q];
+  const uint32_t end = jb.seg_base + jb.nseg;
+  for (uint32_t c0 = jb.seg_base; c0 < end; c0 += 64) {
+    const uint32_t s = c0 + lane;
+    PushSum x;
+    x.n = 0;
+    for (int q = 0; q < 4; q++) x.d[q] = 0;
+    if (s < end) x = push[s];
+    const PushSum inc = scan_pushes(x, lane);
+    const PushSum before = push_exclusive(carry, inc, lane);
+    if (s < end)
+      for (int q = 0; q < 4; q++) segs[s].ring_in[q] = before.d[q];
+    PushSum last;
+    last.n = (uint32_t)__shfl((int)inc.n, 63);
+    for (int q = 0; q < 4; q++) last.d[q] = (uint32_t)__shfl((int)inc.d[q], 63);
+    carry = push_then(carry, last);
   }
 }
 void launch_ring_scan(hipStream_t st, Job *jobs, int njobs, Seg *segs, int nsegs, const RawCmd *raw, PushSum *push) {
   hipLaunchKernelGGL(raw_push_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, raw, push);
-  hipLaunchKernelGGL(ring_scan_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, push);
+  hipLaunchKernelGGL(ring_scan_kernel, dim3(njobs), dim3(64), 0, st, jobs, njobs, segs, push);
 }
 
-// Wave per stream: the entries in stream order, then the metadata block (window bits, header,
-// payload) at the front of the stream's output slice.  The walk is serial in its state (ring,
-// block types, remaining block lengths) but not in its inputs: the lanes stage 64 segments at
-// a time (Seg, pushes, block-split units, the two bytes before the entry) in LDS, so the walk
-// pays one memory round trip per 64 segments instead of several per segment.
+// Block state of one category (type, previous type, remaining block length) as a composable
+// summary of a run of segments: sw -- the run switches blocks (type, prev and blen are then
+// the state after it; prev_in: prev is the type the run started with), else blen is the
+// number of symbols the run consumes.  A metablock start is a switch to the header's state.
+struct BlkSum {
+  uint32_t blen;
+  uint32_t sw, type, prev, prev_in;
+};
+__device__ __forceinline__ BlkSum blk_then(const BlkSum &a, const BlkSum &b) {
+  if (!b.sw) {
+    BlkSum r = a;
+    r.blen = a.sw ? a.blen - b.blen : a.blen + b.blen;
+    return r;
+  }
+  BlkSum r = b;
+  if (b.prev_in && a.sw) {
+    r.prev = a.type;
+    r.prev_in = 0;
+  }
+  return r;
+}
+__device__ __forceinline__ BlkSum shfl_up_blk(const BlkSum &x, int o) {
+  BlkSum r;
+  r.blen = (uint32_t)__shfl_up((int)x.blen, o);
+  r.sw = (uint32_t)__shfl_up((int)x.sw, o);
+  r.type = (uint32_t)__shfl_up((int)x.type, o);
+  r.prev = (uint32_t)__shfl_up((int)x.prev, o);
+  r.prev_in = (uint32_t)__shfl_up((int)x.prev_in, o);
+  return r;
+}
+
+// Wave per stream: the metadata block (window bits, header, payload) at the front of the
+// stream's output slice, then the entries.  The state an entry records (ring, block types,
+// remaining block lengths) is a prefix over the stream's segments: 64 segments per step, each
+// lane summarises its segment (pushes; its block-split units, behind a reset where a
+// metablock starts), a wave scan composes the summaries, and the lanes where a part starts
+// write their entries.
 constexpr int kPiChunk = 64;
 __global__ __launch_bounds__(kPiChunk) void part_index_kernel(const Job *jobs, int njobs, const Mb *mbs, const Seg *segs,
                                                               const Unit *units, const PushSum *push, uint8_t *out) {
-  __shared__ Seg s_seg[kPiChunk];
-  __shared__ PushSum s_push[kPiChunk];
-  __shared__ Unit s_unit[kPiChunk * kSubPerSeg];
-  __shared__ uint32_t s_p12[kPiChunk];
   const int j = blockIdx.x, lane = threadIdx.x;
   if (j >= njobs) return;
   const Job &jb = jobs[j];
@@ -154,77 +220,107 @@ __global__ __launch_bounds__(kPiChunk) void part_index_kernel(const Job *jobs, i
     for (int i = 0; i < (int)sizeof(h); i++) pay[i] = hb[i];
   }
   uint8_t *ent = pay + sizeof(PartHead);
-  uint32_t ring[4];
-  for (int q = 0; q < 4; q++) ring[q] = (uint32_t)jb.dc_in[q];
   const uint64_t bit0 = 8 * jb.out_base;
   const uint32_t seg_end = jb.seg_base + jb.nseg;
-  uint32_t c0 = ~0u;   // first segment staged in LDS
-  for (uint32_t m = 0; m < jb.nmb; m++) {
-    const Mb &mb = mbs[jb.mb_base + m];
-    uint32_t type[3] = {0, 0, 0}, prev[3] = {1, 1, 1}, blen[3];
-    for (int c = 0; c < 3; c++) blen[c] = mb.nbt[c] > 1 ? mb.first_count[c] : (1u << 28);
-    for (uint32_t s = mb.first_seg; s < mb.first_seg + mb.nseg; s++) {
-      if (c0 == ~0u || s - c0 >= (uint32_t)kPiChunk) {   // (uniform) stage the next 64 segments
-        c0 = s;
-        __syncthreads();
-        const uint32_t ls = c0 + lane;
-        if (ls < seg_end) {
-          const Seg sg = segs[ls];
-          s_seg[lane] = sg;
-          s_push[lane] = push[ls];
-          const Mb &lm = mbs[sg.mb];
-          const uint32_t p = ls == lm.first_seg ? lm.start : sg.start - sg.carry_in;
-          s_p12[lane] = prev2(jb, p);
-        }
-        for (int i = lane; i < kPiChunk * kSubPerSeg; i += kPiChunk)
-          if (c0 + i / kSubPerSeg < seg_end) s_unit[i] = units[(size_t)c0 * kSubPerSeg + i];
-        __syncthreads();
-      }
-      const uint32_t k = s - c0;
-      const Seg &sg = s_seg[k];
-      const bool at_mb = s == mb.first_seg;
-      if (lane == 0 && (s - jb.seg_base) % every == 0) {   // a part starts at this segment
-        PartEntry e;
-        const bool has_cmd = sg.ncmd + (sg.extra_ins ? 1 : 0) > 0;
-        const uint32_t p = at_mb ? mb.start : sg.start - sg.carry_in;
-        e.flags = at_mb ? (kPartValid | kPartAtMb) : has_cmd ? kPartValid : 0u;
-        e.bit = bit0 + (at_mb ? mb.bit_off : sg.bit_off);
-        e.pos = (uint64_t)jb.abs_base + p;
-        e.mb_bit = bit0 + mb.bit_off;
-        e.mb_pos = (uint64_t)jb.abs_base + mb.start;
-        for (int q = 0; q < 4; q++) e.ring[q] = ring[q];
-        for (int c = 0; c < 3; c++) {
-          e.blen[c] = at_mb ? 0 : blen[c];
-          e.type[c] = (uint8_t)(at_mb ? 0 : type[c]);
-          e.prev[c] = (uint8_t)(at_mb ? 0 : prev[c]);
-        }
-        const uint32_t p12 = s_p12[k];
-        e.p1 = (uint8_t)(p12 & 0xFF);
-        e.p2 = (uint8_t)(p12 >> 8);
-        const uint8_t *eb = reinterpret_cast<const uint8_t *>(&e);
-        uint8_t *dst = ent + (size_t)((s - jb.seg_base) / every) * sizeof(PartEntry);
-        for (int i = 0; i < (int)sizeof(e); i++) dst[i] = eb[i];
-      }
-      // the segment's distance pushes and block-split units, in stream order
-      const PushSum &ps = s_push[k];
-      if (ps.n >= 4) {
-        for (int q = 0; q < 4; q++) ring[q] = ps.d[q];
-      } else if (ps.n) {
-        uint32_t r[4];
-        for (uint32_t q = 0; q < 4; q++) r[q] = q < ps.n ? ps.d[q] : ring[q - ps.n];
-        for (int q = 0; q < 4; q++) ring[q] = r[q];
-      }
+  PushSum rcarry;   // the ring before the current 64 segments
+  rcarry.n = 4;
+  for (int q = 0; q < 4; q++) rcarry.d[q] = (uint32_t)jb.dc_in[q];
+  BlkSum bcarry[3];   // the block state before them (the stream's first segment starts a metablock)
+  for (int c = 0; c < 3; c++) bcarry[c] = BlkSum{0u, 1u, 0u, 1u, 0u};
+  for (uint32_t c0 = jb.seg_base; c0 < seg_end; c0 += kPiChunk) {
+    const uint32_t s = c0 + lane;
+    const bool live = s < seg_end;
+    PushSum ps;
+    ps.n = 0;
+    for (int q = 0; q < 4; q++) ps.d[q] = 0;
+    BlkSum bs[3];
+    for (int c = 0; c < 3; c++) bs[c] = BlkSum{0u, 0u, 0u, 0u, 0u};
+    Seg sg{};
+    bool at_mb = false;
+    uint32_t mbi = 0;
+    if (live) {
+      sg = segs[s];
+      ps = push[s];
+      mbi = sg.mb;
+      const Mb &mb = mbs[mbi];
+      at_mb = s == mb.first_seg;
+      if (at_mb)   // the metablock header's state: type 0, previous type 1, the first block's count
+        for (int c = 0; c < 3; c++) bs[c] = BlkSum{mb.nbt[c] > 1 ? mb.first_count[c] : (1u << 28), 1u, 0u, 1u, 0u};
       for (int u = 0; u < kSubPerSeg; u++) {
-        const Unit &un = s_unit[k * kSubPerSeg + u];
+        const Unit &un = units[(size_t)s * kSubPerSeg + u];
         for (int c = 0; c < 3; c++) {
+          BlkSum &x = bs[c];
           if (un.sw_count[c]) {
-            prev[c] = type[c];
-            type[c] = un.type[c];
-            blen[c] = un.sw_count[c];
+            if (x.sw) {
+              x.prev = x.type;
+              x.prev_in = 0;
+            } else {
+              x.prev_in = 1;
+            }
+            x.sw = 1;
+            x.type = un.type[c];
+            x.blen = un.sw_count[c] - un.nsym[c];
+          } else {
+            x.blen = x.sw ? x.blen - un.nsym[c] : x.blen + un.nsym[c];
           }
-          blen[c] -= un.nsym[c];
         }
       }
+    }
+    // inclusive scans, then the state before each segment
+    PushSum pinc = ps;
+    BlkSum binc[3] = {bs[0], bs[1], bs[2]};
+#pragma unroll
+    for (int o = 1; o < kPiChunk; o <<= 1) {
+      const PushSum py = shfl_up_push(pinc, o);
+      if (lane >= o) pinc = push_then(py, pinc);
+      for (int c = 0; c < 3; c++) {
+        const BlkSum by = shfl_up_blk(binc[c], o);
+        if (lane >= o) binc[c] = blk_then(by, binc[c]);
+      }
+    }
+    const PushSum ring = push_exclusive(rcarry, pinc, lane);
+    BlkSum before[3];
+    for (int c = 0; c < 3; c++) {
+      BlkSum ex = shfl_up_blk(binc[c], 1);
+      if (lane == 0) ex = BlkSum{0u, 0u, 0u, 0u, 0u};
+      before[c] = blk_then(bcarry[c], ex);
+    }
+    if (live && (s - jb.seg_base) % every == 0) {   // a part starts at this segment
+      const Mb &mb = mbs[mbi];
+      PartEntry e;
+      const bool has_cmd = sg.ncmd + (sg.extra_ins ? 1 : 0) > 0;
+      const uint32_t p = at_mb ? mb.start : sg.start - sg.carry_in;
+      e.flags = at_mb ? (kPartValid | kPartAtMb) : has_cmd ? kPartValid : 0u;
+      e.bit = bit0 + (at_mb ? mb.bit_off : sg.bit_off);
+      e.pos = (uint64_t)jb.abs_base + p;
+      e.mb_bit = bit0 + mb.bit_off;
+      e.mb_pos = (uint64_t)jb.abs_base + mb.start;
+      for (int q = 0; q < 4; q++) e.ring[q] = ring.d[q];
+      for (int c = 0; c < 3; c++) {
+        e.blen[c] = at_mb ? 0 : before[c].blen;
+        e.type[c] = (uint8_t)(at_mb ? 0 : before[c].type);
+        e.prev[c] = (uint8_t)(at_mb ? 0 : before[c].prev);
+      }
+      const uint32_t p12 = prev2(jb, p);
+      e.p1 = (uint8_t)(p12 & 0xFF);
+      e.p2 = (uint8_t)(p12 >> 8);
+      const uint8_t *eb = reinterpret_cast<const uint8_t *>(&e);
+      uint8_t *dst = ent + (size_t)((s - jb.seg_base) / every) * sizeof(PartEntry);
+      for (int i = 0; i < (int)sizeof(e); i++) dst[i] = eb[i];
+    }
+    // carry the 64 segments' composition into the next step
+    PushSum plast;
+    plast.n = (uint32_t)__shfl((int)pinc.n, kPiChunk - 1);
+    for (int q = 0; q < 4; q++) plast.d[q] = (uint32_t)__shfl((int)pinc.d[q], kPiChunk - 1);
+    rcarry = push_then(rcarry, plast);
+    for (int c = 0; c < 3; c++) {
+      BlkSum bl;
+      bl.blen = (uint32_t)__shfl((int)binc[c].blen, kPiChunk - 1);
+      bl.sw = (uint32_t)__shfl((int)binc[c].sw, kPiChunk - 1);
+      bl.type = (uint32_t)__shfl((int)binc[c].type, kPiChunk - 1);
+      bl.prev = (uint32_t)__shfl((int)binc[c].prev, kPiChunk - 1);
+      bl.prev_in = (uint32_t)__shfl((int)binc[c].prev_in, kPiChunk - 1);
+      bcarry[c] = blk_then(bcarry[c], bl);
     }
   }
 }

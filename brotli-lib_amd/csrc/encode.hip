@@ -349,12 +349,14 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.seg_base = (uint32_t)segs.size();
     jb.mb_base = (uint32_t)mbs.size();
     if (!jb.uncompressed) {
-      for (uint64_t m0 = 0; m0 < n; m0 += kMaxMetablock) {
+      // metablock length: the reference's 16 MiB (MIB_MB_BITS: experiment knob, 2^18..2^24)
+      static const uint64_t mb_max = 1ull << env_u32("MIB_MB_BITS", 24, kSegBits + 2, 24);
+      for (uint64_t m0 = 0; m0 < n; m0 += mb_max) {
         Mb mb;
         memset(&mb, 0, sizeof(mb));
         mb.job = (uint32_t)j;
         mb.start = (uint32_t)m0;
-        mb.end = (uint32_t)std::min<uint64_t>(n, m0 + kMaxMetablock);
+        mb.end = (uint32_t)std::min<uint64_t>(n, m0 + mb_max);
         mb.first_seg = (uint32_t)segs.size();
         mb.is_last = (mb.end == n && jb.final_) ? 1 : 0;
         for (uint64_t s0 = m0; s0 < mb.end; s0 += kSeg) {

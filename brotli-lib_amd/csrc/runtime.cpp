@@ -558,7 +558,9 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
   ring_bytes = (ring_bytes + 255) & ~(uint64_t)255;
   uint64_t per_block = ring_bytes + mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4 + 3092 * 4;   // ... ctx-map table, block trees
   per_block = (per_block + 255) & ~(uint64_t)255;
-  int grid = (int)std::min<size_t>(k, 2048);
+  // (MIB_DEC_GRID: experiment knob, a smaller persistent grid -- fewer decoder waves per CU)
+  static const size_t grid_cap = getenv("MIB_DEC_GRID") ? (size_t)std::max(1, atoi(getenv("MIB_DEC_GRID"))) : 2048;
+  int grid = (int)std::min<size_t>(k, std::min<size_t>(grid_cap, 2048));
   int rc;
   if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
   if (k > c->jobs_cap) {
