@@ -658,8 +658,21 @@ __device__ void tree_depths(const uint32_t *h, const int16_t *sorted, int n, uin
   }
 }
 
-__device__ void depths_to_codes(const uint8_t *depth, int len, uint16_t *code) {
-  uint32_t bl[16] = {0}, next[16] = {0};
+// Scratch of the serial tree helpers.  The Huffman kernel keeps one in LDS: as private arrays
+// (dynamically indexed, so in scratch memory) they made serialising a code cost ~600-850 K
+// cycles -- most of the kernel (r03m, scripts/huff_timing.py).
+struct TreeScratch {
+  uint8_t rle_code[720], rle_extra[720];
+  uint32_t clh[18];
+  uint8_t cld[18];
+  uint16_t clc[18];
+  int16_t sorted[18];
+  int16_t left[40], val[40];
+  uint32_t cnt[40];
+  uint32_t bl[16], next[16];
+};
+__device__ void depths_to_codes(const uint8_t *depth, int len, uint16_t *code, uint32_t *bl, uint32_t *next) {
+  for (int i = 0; i < 16; i++) bl[i] = next[i] = 0;
   for (int i = 0; i < len; i++) bl[depth[i]]++;
   bl[0] = 0;
   uint32_t c = 0;
@@ -675,12 +688,16 @@ __device__ void depths_to_codes(const uint8_t *depth, int len, uint16_t *code) {
     code[i] = (uint16_t)r;
   }
 }
+__device__ void depths_to_codes(const uint8_t *depth, int len, uint16_t *code) {
+  uint32_t bl[16], next[16];
+  depths_to_codes(depth, len, code, bl, next);
+}
 
 // small serial Huffman for the 18 code-length codes (limit 5)
-__device__ void small_depths(const uint32_t *h, int len, int limit, uint8_t *depth) {
-  int16_t sorted[18];
-  uint32_t cnt[40];
-  int16_t left[40], val[40];
+__device__ void small_depths(const uint32_t *h, int len, int limit, uint8_t *depth, TreeScratch &ts) {
+  int16_t *sorted = ts.sorted;
+  uint32_t *cnt = ts.cnt;
+  int16_t *left = ts.left, *val = ts.val;
   for (int i = 0; i < len; i++) depth[i] = 0;
   int n = 0;
   for (int i = len - 1; i >= 0; i--)
@@ -727,9 +744,8 @@ __device__ void put_varlen_u8(BitW &w, int n) {
 
 // complex prefix code serialisation: run-length code the depths (16 / 17), then a
 // depth-5 code for those (writeHuffmanTree / storeHuffmanTreeOfHuffmanTree)
-__device__ void store_complex(BitW &w, const uint8_t *depth, int asize) {
-  uint8_t rle_code[720];
-  uint8_t rle_extra[720];
+__device__ void store_complex(BitW &w, const uint8_t *depth, int asize, TreeScratch &ts) {
+  uint8_t *rle_code = ts.rle_code, *rle_extra = ts.rle_extra;
   int nr = 0;
   int nl = asize;
   while (nl > 0 && depth[nl - 1] == 0) nl--;
@@ -798,7 +814,8 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize) {
       prev = v;
     }
   }
-  uint32_t clh[18] = {0};
+  uint32_t *clh = ts.clh;
+  for (int k = 0; k < 18; k++) clh[k] = 0;
   for (int k = 0; k < nr; k++) clh[rle_code[k]]++;
   int ncodes = 0, first = 0;
   for (int k = 0; k < 18; k++)
@@ -806,10 +823,10 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize) {
       if (!ncodes) first = k;
       ncodes++;
     }
-  uint8_t cld[18];
-  uint16_t clc[18];
-  small_depths(clh, 18, 5, cld);
-  depths_to_codes(cld, 18, clc);
+  uint8_t *cld = ts.cld;
+  uint16_t *clc = ts.clc;
+  small_depths(clh, 18, 5, cld, ts);
+  depths_to_codes(cld, 18, clc, ts.bl, ts.next);
   const int order[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
   const uint32_t sym[6] = {0, 7, 3, 2, 1, 15};
   const int blen[6] = {2, 4, 3, 2, 2, 4};
@@ -838,7 +855,8 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize) {
 // One prefix code: simple form for up to 4 used symbols (zero-length codeword for one),
 // complex form otherwise (buildAndStoreHuffmanTree, context-map.ts:215-347).  `depth`
 // holds the code lengths (computed by the caller for n >= 2); `code` is filled.
-__device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uint8_t *depth, uint16_t *code, int asize) {
+__device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uint8_t *depth, uint16_t *code, int asize,
+                           TreeScratch &ts, bool codes_done) {
   if (n <= 1) {
     w.put(4, 1);
     w.put(max_bits, n ? (uint32_t)nzs[0] : 0u);
@@ -846,7 +864,7 @@ __device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uin
     for (int i = 0; i < asize; i++) code[i] = 0;
     return;
   }
-  depths_to_codes(depth, asize, code);
+  if (!codes_done) depths_to_codes(depth, asize, code, ts.bl, ts.next);
   if (n <= 4) {
     int s4[4];
     for (int i = 0; i < n; i++) s4[i] = nzs[i];
@@ -864,7 +882,11 @@ __device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uin
     if (n == 4) w.put(1, depth[s4[0]] == 1 ? 1 : 0);
     return;
   }
-  store_complex(w, depth, asize);
+  store_complex(w, depth, asize, ts);
+}
+__device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uint8_t *depth, uint16_t *code, int asize) {
+  TreeScratch ts;
+  store_code(w, n, nzs, max_bits, depth, code, asize, ts, false);
 }
 
 // serial length-limited Huffman depths for small alphabets (<= 80 symbols)
@@ -908,6 +930,12 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
 // type), distance (block type, cluster); slots beyond the metablock's counts are empty.
 // blocks per metablock: the used codes only (literal codes are at most kMaxLitTrees in all)
 constexpr int kHuffBlocks = kMaxLitTrees + kMaxBT + kMaxBT * kDistCtx;
+#ifdef MIB_PROF   // timing experiment: trees, count-limit attempts, cycles in rank sort / tree / store, per block
+__device__ unsigned long long g_huff_prof[8];
+#define HPT() __builtin_amdgcn_s_memtime()
+#else
+#define HPT() 0ull
+#endif
 __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                                                      const uint32_t *hc, const uint32_t *hd, Codes *codes,
                                                      uint8_t *trees) {
@@ -920,6 +948,7 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ uint16_t code[704];
   __shared__ uint8_t buf[kTreeBytes];
   __shared__ int sh_ok;
+  __shared__ TreeScratch ts;
   const int m = blockIdx.x / kHuffBlocks, r = blockIdx.x % kHuffBlocks;
   const int lane = threadIdx.x;
   Mb &mb = mbs[m];
@@ -974,8 +1003,11 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   wave_sync();
   int max_bits = 0;
   for (int c = asize - 1; c; c >>= 1) max_bits++;
+  uint64_t hp0 = HPT(), hp_sort = 0, hp_tree = 0, hp_att = 0;
   if (n > 1) {
     for (uint32_t lc = 1;; lc *= 2) {
+      hp_att++;
+      const uint64_t ta = HPT();
       for (int a = lane; a < n; a += 64) {
         const int si = nzs[a];
         const uint32_t ci = h[si] > lc ? h[si] : lc;
@@ -988,6 +1020,8 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
         sorted[r] = (int16_t)si;
       }
       wave_sync();
+      const uint64_t tb = HPT();
+      hp_sort += tb - ta;
       if (lane == 0) {
         bool ok;
         tree_depths(h, sorted, n, lc, 15, depth, cnt, left, val, &ok);
@@ -996,14 +1030,64 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
         sh_ok = ok ? 1 : 0;
       }
       wave_sync();
+      hp_tree += HPT() - tb;
       if (sh_ok) break;
     }
   }
+  const uint64_t tc = HPT();
+  if (n > 1) {
+    // canonical codes (convertBitDepthsToSymbols, entropy-encode.ts:234-258) by the wave: the
+    // codes of each length in symbol order, 64 symbols a step
+    uint32_t cntd = 0;   // lane d (1..15): symbols of length d
+    for (int c0 = 0; c0 < asize; c0 += 64) {
+      const int i = c0 + lane;
+      const int d = i < asize ? depth[i] : 0;
+#pragma unroll
+      for (int dd = 1; dd <= 15; dd++) {
+        const uint64_t m = __ballot(d == dd);   // (every lane: a ballot inside a lane-dependent select would see one lane)
+        cntd += lane == dd ? (uint32_t)__popcll(m) : 0u;
+      }
+    }
+    uint32_t nextd = 0, c = 0;   // lane d: the first code of length d
+#pragma unroll
+    for (int dd = 1; dd <= 15; dd++) {
+      c = (c + (uint32_t)__shfl((int)cntd, dd - 1)) << 1;
+      nextd = lane == dd ? c : nextd;
+    }
+    if (lane == 0) nextd = 0;
+    for (int c0 = 0; c0 < asize; c0 += 64) {
+      const int i = c0 + lane;
+      const int d = i < asize ? depth[i] : 0;
+      uint32_t v = 0;
+#pragma unroll
+      for (int dd = 1; dd <= 15; dd++) {
+        const uint64_t m = __ballot(d == dd);
+        const uint32_t base = (uint32_t)__shfl((int)nextd, dd);
+        if (d == dd) v = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+        nextd += lane == dd ? (uint32_t)__popcll(m) : 0u;
+      }
+      if (i < asize) code[i] = d ? (uint16_t)(__brev(v) >> (32 - d)) : (uint16_t)0;
+    }
+    wave_sync();
+  }
   if (lane == 0) {
     BitW w{buf, 0};
-    store_code(w, n, nzs, max_bits, depth, code, asize);
+    store_code(w, n, nzs, max_bits, depth, code, asize, ts, n > 1);
     mb.tree_bits[t] = (uint32_t)w.pos;
   }
+#ifdef MIB_PROF
+  if (lane == 0) {
+    const uint64_t te = HPT();
+    atomicAdd(&g_huff_prof[0], 1ull);
+    atomicAdd(&g_huff_prof[1], (unsigned long long)hp_att);
+    atomicAdd(&g_huff_prof[2], (unsigned long long)hp_sort);
+    atomicAdd(&g_huff_prof[3], (unsigned long long)hp_tree);
+    atomicAdd(&g_huff_prof[4], (unsigned long long)(te - tc));
+    atomicAdd(&g_huff_prof[5], (unsigned long long)(te - hp0));
+    atomicAdd(&g_huff_prof[6], (unsigned long long)n);
+    if (hp_att > 1) atomicAdd(&g_huff_prof[7], 1ull);
+  }
+#endif
   wave_sync();
   uint8_t *dst = trees + ((size_t)m * kTreeSlots + t) * kTreeBytes;
   for (int i = lane; i < kTreeBytes; i += 64) dst[i] = buf[i];
@@ -1605,3 +1689,11 @@ void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, ui
 
 }  // namespace enc
 }  // namespace mib
+#ifdef MIB_PROF
+extern "C" int mib_debug_read_huff_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_huff_prof), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(mib::enc::g_huff_prof), z, sizeof(z));
+  return 0;
+}
+#endif
