@@ -1115,12 +1115,27 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
 // are built here (serial, <= 26 symbols).
 constexpr int kMaxUnits = (int)(kMaxMetablock >> kSubBits);
 constexpr int kSplitIters = 4;
+constexpr int kPathCL = 16;        // units per chunk of the split's shortest path (at least)
+constexpr int kPathChunks = 128;   // chunks at most (scratch in th: 128 x (16 + 4) floats + 4 x 128 bytes)
 __device__ __forceinline__ float sym_bits(uint32_t c, float log_total) {
   return c ? log_total - __log2f((float)c) : log_total + 2.f;
 }
 // NT threads per (metablock, category) block: 1024 when the blocks do not fill the chip (one
 // long stream: its few metablocks), else 256; the type histograms sum NT / 256 unit ranges in
 // parallel, every float sum keeps the 256-thread grouping (identical output either way)
+#ifdef MIB_PROF   // timing experiment: cycles per phase of the split (thread 0's view)
+__device__ unsigned long long g_split_prof[8];
+#define SPMARK(k)                                       \
+  do {                                                  \
+    if (t == 0) {                                       \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      sp[k] += t_ - sp0;                                \
+      sp0 = t_;                                         \
+    }                                                   \
+  } while (0)
+#else
+#define SPMARK(k) do {} while (0)
+#endif
 template <int NT>
 __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h,
                                                     Codes *codes) {
@@ -1138,6 +1153,9 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
+#ifdef MIB_PROF
+  uint64_t sp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sp0 = __builtin_amdgcn_s_memtime();
+#endif
   const int A = cat == 0 ? 256 : cat == 1 ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
   const int hoff = cat == 0 ? 0 : cat == 1 ? 256 : 256 + 704;
   const float sw_cost = cat == 0 ? 26.0f : 28.1f;
@@ -1147,6 +1165,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   const uint32_t *H = unit_h + (size_t)u0 * kSubHist + hoff;
   for (int i = t; i < nu; i += kSplitT) ns[i] = U[i].nsym[cat];
   __syncthreads();
+  SPMARK(0);
   // seed: the non-empty units in kMaxBT contiguous runs
   if (t == 0) {
     int ne = 0;
@@ -1159,6 +1178,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
     sh_ne = ne;
   }
   __syncthreads();
+  SPMARK(1);
   const int ne = sh_ne;
   int keep = 0;
   if (ne >= 2 * kMaxBT) {
@@ -1189,6 +1209,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
         }
       }
       __syncthreads();
+      SPMARK(2);
       if (t < kMaxBT) {
         uint32_t s = 0;
         for (int x = 0; x < A; x++) s += th[t][x];
@@ -1219,6 +1240,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       for (int x = t; x < A; x += kSplitT)
         for (int q = 0; q < kMaxBT; q++) bc[q][x] = tot[q] ? sym_bits(th[q][x], __log2f((float)tot[q])) : 1e9f;
       __syncthreads();
+      SPMARK(3);
       if (it == kSplitIters) break;
       // every unit's bits under every type: a wave per unit, lanes over the symbols
       for (int i = t >> 6; i < nu; i += kSplitT / 64) {
@@ -1248,46 +1270,143 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
         }
       }
       __syncthreads();
-      // shortest path over the non-empty units with the switch cost (findBlocks' DP)
-      if (t == 0) {
-        float dp[kMaxBT] = {0.f, 0.f, 0.f, 0.f};
-        int last = -1;
-        for (int i = 0; i < nu; i++) {
-          if (!ns[i]) continue;
-          float best = 1e30f;
-          int bq = 0;
-          for (int q = 0; q < kMaxBT; q++)
-            if (dp[q] < best) {
-              best = dp[q];
-              bq = q;
+      SPMARK(4);
+      // shortest path over the non-empty units with the switch cost (findBlocks' DP), in
+      // chunks of kPathCL units so that it is not one thread's serial walk (2,048 units of a
+      // 16 MiB metablock: 6.3 M cycles, most of the kernel).  A unit maps the costs of the four
+      // states to dp'[q] = min(dp[q], min dp + switch) + ucost[q], a (min, +) product: each
+      // chunk composes its units' 4 x 4 matrices, one thread carries the costs across the
+      // chunks, each chunk then replays its units from its start costs as the serial walk does
+      // (the switch bits), and the backtrack runs per chunk from the state handed in from
+      // the right (one thread chains the chunks' exit maps).  Scratch: th, which the next
+      // iteration recomputes.
+      {
+        const int CL = max(kPathCL, (nu + kPathChunks - 1) / kPathChunks);
+        const int nch = (nu + CL - 1) / CL;
+        float *Tm = reinterpret_cast<float *>(&th[0][0]);   // [nch][16]: (q, p) -> cost
+        float *Sd = Tm + kPathChunks * 16;                     // [nch][4]: costs at the chunk start
+        uint8_t *Xm = reinterpret_cast<uint8_t *>(Sd + kPathChunks * 4);   // exit maps
+        uint8_t *Pc = Xm + kPathChunks, *Qp = Pc + kPathChunks, *Ln = Qp + kPathChunks;
+        constexpr float kBig = 1e30f;
+        if (t < nch) {   // chunk transfer matrix
+          float T[16];
+#pragma unroll
+          for (int e = 0; e < 16; e++) T[e] = (e >> 2) == (e & 3) ? 0.f : kBig;
+          const int i1 = min(nu, (t + 1) * CL);
+          for (int i = t * CL; i < i1; i++) {
+            if (!ns[i]) continue;
+            float col[kMaxBT];
+#pragma unroll
+            for (int p = 0; p < kMaxBT; p++) col[p] = fminf(fminf(T[p], T[4 + p]), fminf(T[8 + p], T[12 + p])) + sw_cost;
+#pragma unroll
+            for (int q = 0; q < kMaxBT; q++) {
+              const float u = ucost[i][q];
+#pragma unroll
+              for (int p = 0; p < kMaxBT; p++) T[4 * q + p] = fminf(T[4 * q + p], col[p]) + u;
             }
-          uint8_t b = 0;
-          float nd[kMaxBT];
-          for (int q = 0; q < kMaxBT; q++) {
-            const float stay = dp[q], sw = best + sw_cost;
-            const bool s = last >= 0 && sw < stay;
-            nd[q] = (s ? sw : stay) + ucost[i][q];
-            if (s) b |= (uint8_t)(1 << q);
           }
-          bp[i] = (uint8_t)(b | (bq << 4));
-          for (int q = 0; q < kMaxBT; q++) dp[q] = nd[q];
-          last = i;
+#pragma unroll
+          for (int e = 0; e < 16; e++) Tm[t * 16 + e] = T[e];
         }
-        int cur = 0;
-        for (int q = 1; q < kMaxBT; q++)
-          if (dp[q] < dp[cur]) cur = q;
-        for (int i = nu - 1; i >= 0; i--) {
-          if (!ns[i]) continue;
-          asg[i] = (uint8_t)cur;
-          if (bp[i] >> cur & 1) cur = bp[i] >> 4;
+        __syncthreads();
+        if (t == 0) {   // the costs at every chunk start
+          float dp[kMaxBT] = {0.f, 0.f, 0.f, 0.f};
+          for (int c = 0; c < nch; c++) {
+            float nd[kMaxBT];
+#pragma unroll
+            for (int q = 0; q < kMaxBT; q++) {
+              Sd[c * 4 + q] = dp[q];
+              float v = kBig;
+#pragma unroll
+              for (int p = 0; p < kMaxBT; p++) v = fminf(v, Tm[c * 16 + 4 * q + p] + dp[p]);
+              nd[q] = v;
+            }
+#pragma unroll
+            for (int q = 0; q < kMaxBT; q++) dp[q] = nd[q];
+          }
+          int cur = 0;
+          for (int q = 1; q < kMaxBT; q++)
+            if (dp[q] < dp[cur]) cur = q;
+          Pc[kPathChunks - 1] = (uint8_t)cur;   // (handed to the last chunk below)
         }
-        int prev = asg[0];
-        for (int i = 0; i < nu; i++) {   // empty units follow their predecessor
-          if (!ns[i]) asg[i] = (uint8_t)prev;
-          prev = asg[i];
+        __syncthreads();
+        if (t < nch) {   // replay: the serial walk's switch bits, then the chunk's exit map
+          float dp[kMaxBT];
+#pragma unroll
+          for (int q = 0; q < kMaxBT; q++) dp[q] = Sd[t * 4 + q];
+          const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
+          for (int i = i0; i < i1; i++) {
+            if (!ns[i]) continue;
+            float best = 1e30f;
+            int bq = 0;
+#pragma unroll
+            for (int q = 0; q < kMaxBT; q++)
+              if (dp[q] < best) {
+                best = dp[q];
+                bq = q;
+              }
+            uint8_t bb = 0;
+            float nd[kMaxBT];
+#pragma unroll
+            for (int q = 0; q < kMaxBT; q++) {
+              const float stay = dp[q], sw = best + sw_cost;
+              const bool sv = sw < stay;   // (never at the first unit: every cost is 0 there)
+              nd[q] = (sv ? sw : stay) + ucost[i][q];
+              if (sv) bb |= (uint8_t)(1 << q);
+            }
+            bp[i] = (uint8_t)(bb | (bq << 4));
+#pragma unroll
+            for (int q = 0; q < kMaxBT; q++) dp[q] = nd[q];
+          }
+          uint32_t xm = 0;
+          for (int cin = 0; cin < kMaxBT; cin++) {
+            int cur = cin;
+            for (int i = i1 - 1; i >= i0; i--)
+              if (ns[i] && (bp[i] >> cur & 1)) cur = bp[i] >> 4;
+            xm |= (uint32_t)cur << (2 * cin);
+          }
+          Xm[t] = (uint8_t)xm;
+        }
+        __syncthreads();
+        if (t == 0) {   // the state handed into every chunk from the right
+          int cur = Pc[kPathChunks - 1];
+          for (int c = nch - 1; c >= 0; c--) {
+            Pc[c] = (uint8_t)cur;
+            cur = (Xm[c] >> (2 * cur)) & 3;
+          }
+        }
+        __syncthreads();
+        if (t < nch) {   // the chunk's assignment; its last non-empty unit's type
+          int cur = Pc[t], ln = -1;
+          const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
+          for (int i = i1 - 1; i >= i0; i--) {
+            if (!ns[i]) continue;
+            asg[i] = (uint8_t)cur;
+            if (ln < 0) ln = cur;
+            if (bp[i] >> cur & 1) cur = bp[i] >> 4;
+          }
+          Ln[t] = (uint8_t)(ln < 0 ? 0xFF : ln);
+        }
+        __syncthreads();
+        if (t == 0) {   // empty units follow their predecessor: the type handed into each chunk
+          int prev = asg[0];
+          for (int c = 0; c < nch; c++) {
+            Qp[c] = (uint8_t)prev;
+            if (Ln[c] != 0xFF) prev = Ln[c];
+          }
+        }
+        __syncthreads();
+        if (t < nch) {
+          int prev = Qp[t];
+          const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
+          for (int i = i0; i < i1; i++) {
+            if (!ns[i]) asg[i] = (uint8_t)prev;
+            prev = asg[i];
+          }
         }
       }
       __syncthreads();
+      SPMARK(5);
     }
     // the split's cost: unit bits under the final histograms, switches, one code header per type
     float part = 0.f;   // (the first 256 threads, in the same grouping as ever: identical sums)
@@ -1317,23 +1436,44 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       sh_keep = (used > 1 && split_cost < base_cost) ? 1 : 0;
     }
     __syncthreads();
+    SPMARK(6);
     keep = sh_keep;
   }
-  if (t != 0) return;
-  Codes &cd = codes[m];
+#ifdef MIB_PROF
+  const uint64_t tail0 = __builtin_amdgcn_s_memtime();
+#endif
   if (!keep) {
-    for (int i = 0; i < nu; i++) {
+    for (int i = t; i < nu; i += kSplitT) {
       U[i].type[cat] = 0;
       U[i].sw_count[cat] = 0;
     }
-    mb.nbt[cat] = 1;
-    mb.first_count[cat] = 0;
+    if (t == 0) {
+      mb.nbt[cat] = 1;
+      mb.first_count[cat] = 0;
+    }
     return;
   }
+  // The serial layout works in LDS (the unit costs and switch bits are dead here): per unit
+  // its type, the count of the block a switch there opens, the switch's code; the units are
+  // then written by every thread.  (Writing each unit's fields to HBM inside the serial loop
+  // kept thread 0 waiting on its store queue, ~800 cycles a unit.)
+  uint32_t *lsw = reinterpret_cast<uint32_t *>(&ucost[0][0]);
+  uint8_t *lcode = reinterpret_cast<uint8_t *>(lsw + kMaxUnits);
+  uint8_t *lty = bp;
+  if (t == 0) {
   // renumber by first use
-  int map[kMaxBT] = {-1, -1, -1, -1}, nt = 0;
-  for (int i = 0; i < nu; i++)
-    if (ns[i] && map[asg[i]] < 0) map[asg[i]] = nt++;
+  // (packed 8 bits per type, 0xFF: unused -- an indexed private array lived in scratch memory,
+  // one round trip per unit of this serial loop)
+  uint32_t mapp = 0xFFFFFFFFu;
+  int nt = 0;
+  for (int i = 0; i < nu; i++) {
+    if (!ns[i]) continue;
+    const uint32_t sh = 8u * asg[i];
+    if (((mapp >> sh) & 0xFF) == 0xFF) {
+      mapp = (mapp & ~(0xFFu << sh)) | ((uint32_t)nt << sh);
+      nt++;
+    }
+  }
   // lay out the switches
   uint32_t hcode[kMaxBT + 2] = {0, 0, 0, 0, 0, 0}, hcount[26];
   for (int q = 0; q < 26; q++) hcount[q] = 0;
@@ -1341,20 +1481,19 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   uint32_t count = 0;
   bool started = false;
   for (int i = 0; i < nu; i++) {
-    Unit &u = U[i];
-    u.sw_count[cat] = 0;
+    lsw[i] = 0;
     const uint32_t nsy = ns[i];
     if (!nsy) {
-      u.type[cat] = (uint8_t)cur;
+      lty[i] = (uint8_t)cur;
       continue;
     }
-    const int ty = map[asg[i]];
+    const int ty = (int)((mapp >> (8u * asg[i])) & 0xFF);
     if (started && ty != cur) {
       if (open < 0) mb.first_count[cat] = count;
-      else U[open].sw_count[cat] = count;
+      else lsw[open] = count;
       hcount[block_count_code(count)]++;
       const int code = ty == second ? 0 : ty == (last + 1) % nt ? 1 : ty + 2;
-      u.sw_code[cat] = (uint8_t)code;
+      lcode[i] = (uint8_t)code;
       hcode[code]++;
       second = last;
       last = ty;
@@ -1363,17 +1502,31 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       count = 0;
     }
     started = true;
-    u.type[cat] = (uint8_t)ty;
+    lty[i] = (uint8_t)ty;
     count += nsy;
   }
   if (open < 0) mb.first_count[cat] = count;
-  else U[open].sw_count[cat] = count;
+  else lsw[open] = count;
   hcount[block_count_code(count)]++;
   mb.nbt[cat] = (uint32_t)nt;
+  Codes &cd = codes[m];
   serial_depths(hcode, nt + 2, 15, cd.btd[cat]);
   depths_to_codes(cd.btd[cat], nt + 2, cd.btc[cat]);
   serial_depths(hcount, 26, 15, cd.bcd[cat]);
   depths_to_codes(cd.bcd[cat], 26, cd.bcc[cat]);
+  }
+  __syncthreads();
+  for (int i = t; i < nu; i += kSplitT) {
+    Unit &u = U[i];
+    u.type[cat] = lty[i];
+    u.sw_count[cat] = lsw[i];
+    if (lsw[i]) u.sw_code[cat] = lcode[i];
+  }
+#ifdef MIB_PROF
+  if (t != 0) return;
+  sp[7] += __builtin_amdgcn_s_memtime() - tail0;
+  for (int q = 0; q < 8; q++) atomicAdd(&g_split_prof[q], (unsigned long long)sp[q]);
+#endif
 }
 
 // encodeContextMap (context-map.ts:114-170): NTREES, then (NTREES > 1) move-to-front, runs
@@ -1694,6 +1847,14 @@ extern "C" int mib_debug_read_huff_prof(unsigned long long *out) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_huff_prof), sizeof(unsigned long long) * 8);
   unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   hipMemcpyToSymbol(HIP_SYMBOL(mib::enc::g_huff_prof), z, sizeof(z));
+  return 0;
+}
+#endif
+#ifdef MIB_PROF
+extern "C" int mib_debug_read_split_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_split_prof), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(mib::enc::g_split_prof), z, sizeof(z));
   return 0;
 }
 #endif
