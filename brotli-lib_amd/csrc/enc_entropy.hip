@@ -936,20 +936,25 @@ __device__ unsigned long long g_huff_prof[8];
 #else
 #define HPT() 0ull
 #endif
+// AMAX: the largest alphabet the launch builds codes for -- 256 for the literal slots, 704 for
+// the command and distance ones: the literal codes (most of a metablock's) then need ~10 KiB of
+// LDS instead of ~22, so twice as many of these latency-bound one-wave blocks share a CU.
+// r0: the first slot block of the launch (block r of metablock m = blockIdx.x / nr, r0 + x % nr)
+template <int AMAX>
 __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                                                      const uint32_t *hc, const uint32_t *hd, Codes *codes,
-                                                     uint8_t *trees) {
-  __shared__ uint32_t h[704];
-  __shared__ int16_t nzs[704];
-  __shared__ int16_t sorted[704];
-  __shared__ uint32_t cnt[2 * 704 + 2];
-  __shared__ int16_t left[2 * 704 + 2], val[2 * 704 + 2];
-  __shared__ uint8_t depth[704];
-  __shared__ uint16_t code[704];
+                                                     uint8_t *trees, int r0, int nr) {
+  __shared__ uint32_t h[AMAX];
+  __shared__ int16_t nzs[AMAX];
+  __shared__ int16_t sorted[AMAX];
+  __shared__ uint32_t cnt[2 * AMAX + 2];
+  __shared__ int16_t left[2 * AMAX + 2], val[2 * AMAX + 2];
+  __shared__ uint8_t depth[AMAX];
+  __shared__ uint16_t code[AMAX];
   __shared__ uint8_t buf[kTreeBytes];
   __shared__ int sh_ok;
   __shared__ TreeScratch ts;
-  const int m = blockIdx.x / kHuffBlocks, r = blockIdx.x % kHuffBlocks;
+  const int m = blockIdx.x / nr, r = r0 + (int)(blockIdx.x % nr);
   const int lane = threadIdx.x;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
@@ -982,6 +987,7 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   const bool lit = t < kCmdSlot, dist = t >= kDistSlot;
   const int cl = lit ? t : dist ? t - kDistSlot : t - kCmdSlot;   // slot within its alphabet
   const int asize = lit ? 256 : !dist ? 704 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
+  if (asize > AMAX) return;   // (cannot happen: the literal launch covers the literal slots only)
   const uint32_t *src = lit ? hl + ((size_t)m * kLitSlots + cl) * 256 : !dist ? hc + ((size_t)m * kMaxBT + cl) * 704
                                                                           : hd + ((size_t)m * kMaxBT * kDistCtx + cl) * 128;
   for (int i = lane; i < asize; i += 64) {
@@ -1825,7 +1831,11 @@ void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
-  hipLaunchKernelGGL(huffman_kernel, dim3(nmbs * kHuffBlocks), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees);
+  // one launch for every slot (two launches by alphabet size, the literal one with half the LDS,
+  // were measured: C4 6.0 -> 5.5 ms but C3 8.9 -> 10.2 -- the command / distance blocks, the
+  // longest, then ran as a tail of their own)
+  hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * kHuffBlocks), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, 0,
+                     kHuffBlocks);
   hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
