@@ -79,10 +79,11 @@ def main(tag):
     with open(os.path.join(ROOT, 'profiles', 'pmc_summary.json'), 'w') as f:
         json.dump(summary, f, indent=1, sort_keys=True)
     sq = {}
-    for d in sorted(glob.glob(os.path.join(base, 'sq[12]_*'))):
+    for d in sorted(glob.glob(os.path.join(base, 'sq[12]_*')) + glob.glob(os.path.join(base, 'sqref[12]_*'))):
         if not os.path.isdir(d):
             continue
-        k = os.path.basename(d)[4:]
+        b = os.path.basename(d)
+        k = b[4:] if b.startswith('sq1_') or b.startswith('sq2_') else b[7:] + ' (ref leg: one foreign stream per call)'
         acc = defaultdict(float)
         disp = set()
         for r in rows(os.path.join(d, '**', '*counter_collection.csv')):
@@ -97,7 +98,7 @@ def main(tag):
             e['wait_any_share'] = round(e.get('SQ_WAIT_ANY', 0) / e['SQ_WAVE_CYCLES'], 3)
             e['active_inst_share'] = round(e.get('SQ_ACTIVE_INST_ANY', 0) / e['SQ_WAVE_CYCLES'], 3)
     with open(os.path.join(dst, 'sq_counters.json'), 'w') as f:
-        json.dump({'source': 'rocprofv3 --pmc (two passes of 8 SQ counters) on bench.py c4, --kernel-include-regex',
+        json.dump({'source': 'rocprofv3 --pmc (two passes of 8 SQ counters) on bench.py c4 (and --workload ref where named), --kernel-include-regex',
                    'units': 'SQ units (cycle counters in quad-cycles), per dispatch', 'kernels': sq}, f, indent=1,
                   sort_keys=True)
     for w, v in summary['workloads'].items():
