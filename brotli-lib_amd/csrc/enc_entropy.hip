@@ -379,6 +379,9 @@ constexpr int kCluT = 1024;
 constexpr int kCluPairs = kLitCtx * (kLitCtx - 1) / 2;
 // pair (a, b), a < b, in the triangular savings table; lexicographic, as a * 64 + b orders them
 __device__ __forceinline__ int tri(int a, int b) { return a * (2 * kLitCtx - a - 1) / 2 + b - a - 1; }
+#ifdef MIB_PROF   // timing experiment: thread 0's cycles in costs / initial pairs / best-pair search / merges / output; merges
+__device__ unsigned long long g_clu_prof[8];
+#endif
 __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd,
                                                          int lit_cap) {
   constexpr int kMaxH = kLitCtx;
@@ -396,6 +399,19 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
+#ifdef MIB_PROF
+  uint64_t cp[6] = {0, 0, 0, 0, 0, 0}, cp0 = __builtin_amdgcn_s_memtime();
+#define CLMARK(k)                                         \
+  do {                                                    \
+    if (t == 0) {                                         \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+      cp[k] += t_ - cp0;                                  \
+      cp0 = t_;                                           \
+    }                                                     \
+  } while (0)
+#else
+#define CLMARK(k) do {} while (0)
+#endif
   const int nbt = (int)(kind == 0 ? mb.nbt[0] : mb.nbt[2]);
   if (ty >= nbt) {
     if (t == 0) {
@@ -438,6 +454,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     for (int a = 0; a < nh; a++) na += alive[a];
     sh_alive = na;
   }
+  CLMARK(0);
   // savings of every pair
   auto pair_saving = [&](int a, int b) -> float {
     float sum = 0.f, ent = 0.f;
@@ -469,6 +486,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     if (alive[a] && alive[b]) save[tri(a, b)] = pair_saving(a, b);
   }
   __syncthreads();
+  CLMARK(1);
   for (;;) {
     // best pair
     float bv = -1e30f;
@@ -514,7 +532,11 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     }
     __syncthreads();
     const int best = sh_best;
+    CLMARK(2);
     if (best < 0) break;
+#ifdef MIB_PROF
+    cp[5]++;
+#endif
     const int a = pair_of[best] >> 8, b = pair_of[best] & 0xFF;   // merge b into a
     for (int x = t; x < A; x += kCluT) h[a][x] += h[b][x];
     __syncthreads();
@@ -559,6 +581,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     }
     __syncthreads();
   }
+  CLMARK(3);
   // number the clusters by first use; unused contexts go to cluster 0
   __shared__ int rep_id[kMaxH];
   if (t == 0) {
@@ -584,6 +607,13 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     const int c = alive[a] ? rep_id[a] : -1;
     if (c >= 0 && x < A) src[c * stride + x] = h[a][x];
   }
+#ifdef MIB_PROF
+  CLMARK(4);
+  if (t == 0)
+    for (int q = 0; q < 6; q++) atomicAdd(&g_clu_prof[q], (unsigned long long)cp[q]);
+  if (t == 0) atomicAdd(&g_clu_prof[6], 1ull);
+#endif
+#undef CLMARK
 }
 
 // ---------------------------------------------------------------- distance ring after a chunk
@@ -1865,6 +1895,14 @@ extern "C" int mib_debug_read_split_prof(unsigned long long *out) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_split_prof), sizeof(unsigned long long) * 8);
   unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   hipMemcpyToSymbol(HIP_SYMBOL(mib::enc::g_split_prof), z, sizeof(z));
+  return 0;
+}
+#endif
+#ifdef MIB_PROF
+extern "C" int mib_debug_read_clu_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_clu_prof), sizeof(unsigned long long) * 8);
+  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyToSymbol(HIP_SYMBOL(mib::enc::g_clu_prof), z, sizeof(z));
   return 0;
 }
 #endif
