@@ -166,6 +166,15 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// lane `lane` of v takes the (wave-uniform) value x: one v_writelane_b32 (a compare and a
+// select per literal before)
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t x, uint32_t lane) {
+  // (the lane select goes through m0: two SGPR operands would break the constant-bus limit)
+  const uint32_t xs = (uint32_t)__builtin_amdgcn_readfirstlane((int)x), ls = (uint32_t)__builtin_amdgcn_readfirstlane((int)lane);
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(xs), "s"(ls) : "m0");
+  return v;
+}
+
 // ---------------------------------------------------------------- bit reader
 __device__ __forceinline__ uint32_t half_at(const DecS &s, int h) {
   if (h < 0 || h >= 2080) return 0;   // Int16Array(2080): undefined -> 0
@@ -1317,7 +1326,7 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
                   while (j < end) {
                     LFILL16();
                     const int val = lsym16(root);
-                    ob = lane == (pos & 63) ? (uint32_t)val : ob;
+                    ob = write_lane(ob, (uint32_t)val, (uint32_t)(pos & 63));
                     pos++;
                     j++;
                     c2b = c1;
@@ -1337,7 +1346,7 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
                     LFILL16();
                     c2b = p1;
                     p1 = U(lsym16(root));
-                    ob = lane == (pos & 63) ? (uint32_t)p1 : ob;
+                    ob = write_lane(ob, (uint32_t)p1, (uint32_t)(pos & 63));
                     pos++;
                     j++;
                     if ((pos & 63) == 0) flush();
@@ -1720,16 +1729,14 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   auto sym16 = [&](int root) -> int {
     const uint32_t v = peek32();
     int off = root + (int)(v & 0xFF);
-    const int e0 = U((int)t16[off]);
-    const int nb = e0 >> 12;
-    if (nb <= 8) {
-      bo += nb;
-      return e0 & 0xFFF;
+    int e = U((int)t16[off]);
+    if ((e >> 12) > 8) {   // a second-level table: one branch around it, a common tail
+      off += (e & 0xFFF) + (int)((v & ((1u << (e >> 12)) - 1u)) >> 8);
+      e = U((int)t16[off]);
+      bo += 8;
     }
-    off += (e0 & 0xFFF) + (int)((v & ((1u << nb) - 1u)) >> 8);
-    const int e1 = U((int)t16[off]);
-    bo += (e1 >> 12) + 8;
-    return e1 & 0xFFF;
+    bo += e >> 12;
+    return e & 0xFFF;
   };
   // complete the copy in flight: stores, literal context.  Its bytes arrive in LDS by DMA,
   // which the compiler does not wait for: behind_next -- the next copy's DMA was the last
@@ -1807,7 +1814,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
           while (pos < seg_end) {
             fill();
             const int val = sym16(lit_root);
-            ob = lane == (pos & 63) ? (uint32_t)val : ob;
+            ob = write_lane(ob, (uint32_t)val, (uint32_t)(pos & 63));
             pos++;
             c2b = c1;
             c1 = val;
@@ -1830,7 +1837,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
             c1 = U(sym16(root));
             const uint64_t e = c1 & 2 ? row >> 32 : row;   // lane c1 >> 2 holds entries 4 (c1 >> 2) ..
             root = __builtin_amdgcn_readlane((int)(uint32_t)(e >> (16 * (c1 & 1))), c1 >> 2) & 0xFFFF;
-            ob = lane == (pos & 63) ? (uint32_t)c1 : ob;
+            ob = write_lane(ob, (uint32_t)c1, (uint32_t)(pos & 63));
             pos++;
           }
           if ((pos & 63) == 0) {
