@@ -1688,6 +1688,11 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   auto lut1_of = [lutp](int v) -> int {   // v wave-uniform
     return (int)(((uint32_t)__builtin_amdgcn_readlane((int)lutp, v & 63) >> (8 * (v >> 6))) & 0xFF);
   };
+  // the ring slot idx (0..3) without branches: two bit tests, three selects
+  auto ring_at = [&](int idx) -> int {
+    const int lo = (idx & 1) ? dr1 : dr0, hi = (idx & 1) ? dr3 : dr2;
+    return (idx & 2) ? hi : lo;
+  };
   uint32_t droot01, droot23;
   {
     const int db = s.dist_base, sl = s.dist_ctx_map_slice;
@@ -1864,14 +1869,14 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     const int dbo = bo, dho = ho, dmax = max_dist;
     int dc = dist_code;
     if (dc < 0) {
-      distance = dridx == 0 ? dr0 : dridx == 1 ? dr1 : dridx == 2 ? dr2 : dr3;
+      distance = ring_at(dridx);
     } else {
       fill();
       const uint32_t dpair = dc < 2 ? droot01 : droot23;
       dc = U(sym16((int)((dpair >> (16 * (dc & 1))) & 0xFFFF)));
       if (dc < 16) {
         const int idx = (dridx + (int)((0xfff0006cu >> (2 * dc)) & 3)) & 3;
-        distance = (idx == 0 ? dr0 : idx == 1 ? dr1 : idx == 2 ? dr2 : dr3) + (int)((0xc298b0a626dbull >> (3 * dc)) & 7) - 3;
+        distance = ring_at(idx) + (int)((0xc298b0a626dbull >> (3 * dc)) & 7) - 3;
       } else {
         int eb, doff;
         if (dc < 16 + ndirect) {
@@ -1917,10 +1922,10 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     if (dist_code >= 0) dist_blen--;
     if (dc > 0) {
       dridx = (dridx + 1) & 3;
-      if (dridx == 0) dr0 = distance;
-      else if (dridx == 1) dr1 = distance;
-      else if (dridx == 2) dr2 = distance;
-      else dr3 = distance;
+      dr0 = dridx == 0 ? distance : dr0;   // (selects: the if-chain compiled to branches)
+      dr1 = dridx == 1 ? distance : dr1;
+      dr2 = dridx == 2 ? distance : dr2;
+      dr3 = dridx == 3 ? distance : dr3;
     }
     FMARK(2);
     // ---- copy (no wrap, no fence)
