@@ -377,24 +377,49 @@ __device__ __forceinline__ void replicate(const DecS &s, int32_t *g, int cap, in
     if (i < cap) g[i] = item;
   }
 }
+// The per-length counts and the length-sorted symbol list by the wave (15 ballots per 64
+// symbols); count[] goes to LDS scratch in ctx_root, which build_ctx_tree_base rebuilds after
+// every metablock header (the private count[] / offset[] arrays, indexed by code length, were
+// scratch memory: a scratch round trip per symbol, twice, in every lane).
 template <class L>
 __device__ int build_table(DecS &s, int32_t *group, int cap, int idx, int root, const L *lens, int nsym) {
   int toff = group[idx];
-  int count[16], offset[16];
-  for (int i = 0; i < 16; i++) count[i] = offset[i] = 0;
-  for (int i = 0; i < nsym; i++) count[lens[i]]++;
-  offset[1] = 0;
-  for (int l = 1; l < 15; l++) offset[l + 1] = offset[l] + count[l];
+  uint32_t cnt = 0;   // lane l (1..15): symbols of length l
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    const int i = c0 + LANE;
+    const int l = i < nsym ? (int)lens[i] : 0;
+#pragma unroll
+    for (int ll = 1; ll < 16; ll++) {
+      const uint64_t m = __ballot(l == ll);
+      cnt += LANE == ll ? (uint32_t)__popcll(m) : 0u;
+    }
+  }
+  uint32_t off = 0, run = 0;   // lane l: the first slot of length l in sorted
+#pragma unroll
+  for (int ll = 1; ll < 16; ll++) {
+    off = LANE == ll ? run : off;
+    run += (uint32_t)__shfl((int)cnt, ll);
+  }
+  const int nonzero = (int)run;
   uint16_t *sorted = s.l->sorted;
-  wave_sync();
-  if (LANE == 0)
-    for (int i = 0; i < nsym; i++)
-      if (lens[i]) sorted[offset[lens[i]]++] = (uint16_t)i;
-  for (int i = 0; i < nsym; i++)   // uniform copy of the per-length running offsets
-    if (lens[i]) offset[lens[i]]++;
+  for (int c0 = 0; c0 < nsym; c0 += 64) {
+    const int i = c0 + LANE;
+    const int l = i < nsym ? (int)lens[i] : 0;
+    uint32_t pos = 0;
+#pragma unroll
+    for (int ll = 1; ll < 16; ll++) {
+      const uint64_t m = __ballot(l == ll);
+      const uint32_t base = (uint32_t)__shfl((int)off, ll);
+      if (l == ll) pos = base + (uint32_t)__popcll(m & ((1ull << LANE) - 1));
+      off += LANE == ll ? (uint32_t)__popcll(m) : 0u;
+    }
+    if (l) sorted[pos] = (uint16_t)i;
+  }
+  int *count = reinterpret_cast<int *>(s.l->ctx_root);
+  if (LANE < 16) count[LANE] = LANE ? (int)cnt : 0;
   wave_sync();
   int tbits = root, tsize = 1 << tbits, total = tsize;
-  if (offset[15] == 1) {
+  if (nonzero == 1) {
     replicate(s, group, cap, toff, 1, total, sorted[0]);
     wave_sync();
     return total;
@@ -536,8 +561,9 @@ __device__ int read_huffman_code(DecS &s, int amax, int alimit, int32_t *group, 
     wave_sync();
     return build_table(s, group, cap, idx, 8, lens, alimit);
   }
-  int cl[18];
-  for (int i = 0; i < 18; i++) cl[i] = 0;
+  int *cl = reinterpret_cast<int *>(s.l->ctx_root) + 32;   // (LDS scratch, see build_table)
+  if (LANE < 18) cl[LANE] = 0;
+  wave_sync();
   int space = 32, ncodes = 0;
   for (int i = kind; i < 18; i++) {
     int ci = kCodeLenOrder[i];

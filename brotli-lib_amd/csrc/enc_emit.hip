@@ -229,7 +229,8 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
     for (uint32_t i0 = 0; i0 < nitems; i0 += kBlock * kEmitItems) {
       uint32_t bits[kEmitItems], qj[kEmitItems], kk[kEmitItems];
       uint64_t val[kEmitItems];
-      bool packed[kEmitItems];
+      uint32_t packed = 0;   // bit e: item e was packed (a bit mask: a bool array indexed by the
+                             // loop counter lived in scratch memory, a store and four loads per item)
       const uint32_t first = i0 + (uint32_t)t * kEmitItems;
       uint32_t j = first < nitems ? map.find(first, nb) : 0;
       for (int e = 0; e < kEmitItems; e++) {
@@ -238,15 +239,17 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
         qj[e] = j;
         kk[e] = 0;
         val[e] = 0;
-        packed[e] = true;
+        packed |= 1u << e;
         if (i < nitems) {
           while (map.off[j + 1] <= i) j++;
           qj[e] = j;
           kk[e] = i - map.off[j];
           const Cmd &k = sh_c[j];
           const uint32_t p = sh_p[j];
-          packed[e] = item_packed(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e], bits[e], val[e]);
-          if (!packed[e]) bits[e] = item_bits(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
+          if (!item_packed(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e], bits[e], val[e])) {
+            packed &= ~(1u << e);
+            bits[e] = item_bits(cd, mb, sh_cmap, lut, jb, k, p, sg, sh_u, base + j, kk[e]);
+          }
         }
       }
       uint32_t boff[kEmitItems], total;
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
       __syncthreads();
       for (int e = 0; e < kEmitItems; e++) {
         if (!bits[e]) continue;
-        if (packed[e]) {   // the whole item: at most 63 bits over three words
+        if (packed >> e & 1) {   // the whole item: at most 63 bits over three words
           const uint32_t b = rel0 + boff[e], w = b >> 5, sh = b & 31;
           const uint64_t lo = val[e] << sh;
           atomicOr(win + w, (uint32_t)lo);

@@ -149,7 +149,9 @@ __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *s
     sh_first[t / 3][t % 3] = ~0u;
   }
   if (t == 0) sh_run = sg.start - sg.carry_in;
-  if (t < 4) sh_ring[t] = sg.ring_in[t];
+  // (from global: a lane-indexed read of the by-value copy kept that copy in scratch memory,
+  // and every later field read with it)
+  if (t < 4) sh_ring[t] = segs[blockIdx.x].ring_in[t];
   __syncthreads();
   const RawCmd *r = raw + sg.cmd_off;
   Cmd *out = cmds + sg.cmd_off;
