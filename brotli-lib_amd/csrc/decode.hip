@@ -149,8 +149,9 @@ __shared__ Lds g_lds;
 __shared__ Dec g_dec;   // the decoder state: LDS, so that it is wave-uniform and never waits on HBM stores
 // fast_loop: the source bytes of copies in flight, by LDS-DMA.  global_load_lds_ubyte writes
 // lane l's byte zero-extended to the DWORD at base + 4 l (probed on the MI355X:
-// scripts/probe/glds_probe.hip), so a slot is 64 dwords.
-__shared__ uint32_t g_cpa[64], g_cpb[64];
+// scripts/probe/glds_probe.hip), so a slot is 64 dwords; kCopyQ slots, used round robin.
+constexpr int kCopyQ = 4;
+__shared__ uint32_t g_cp[kCopyQ][64];
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
@@ -169,10 +170,21 @@ __device__ __forceinline__ void wave_sync() {
 // lane `lane` of v takes the (wave-uniform) value x: one v_writelane_b32 (a compare and a
 // select per literal before)
 __device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t x, uint32_t lane) {
-  // (the lane select goes through m0: two SGPR operands would break the constant-bus limit)
+  // The lane select goes through m0 (two SGPR operands would break the constant-bus limit).
+  // m0 is an input operand ("{m0}"), so the compiler itself loads it and knows its value is
+  // gone: the LDS-DMA below sets m0 to its LDS address, and m0 as a clobber is a reserved
+  // register the compiler does not promise to restore (clang warns, and a hoisted m0 would
+  // send a copy's bytes to the wrong LDS words).
   const uint32_t xs = (uint32_t)__builtin_amdgcn_readfirstlane((int)x), ls = (uint32_t)__builtin_amdgcn_readfirstlane((int)lane);
-  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(xs), "s"(ls) : "m0");
+  asm volatile("v_writelane_b32 %0, %1, m0" : "+v"(v) : "s"(xs), "{m0}"(ls));
   return v;
+}
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 3] (the immediate is part of the encoding)
+__device__ __forceinline__ void wait_vm(int n) {
+  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
 }
 
 // ---------------------------------------------------------------- bit reader
@@ -1664,9 +1676,12 @@ __device__ __noinline__ int hot_loop(int fence_in, int rmask_in, int stop_at_bou
 //    the whole root row of literal k + 1 (its p2 = literal k - 1 is known; ctx_root is laid
 //    out [lut1[p2]][p1]), so the next root is a readlane of the decoded symbol -- one LDS
 //    round trip per literal instead of two;
-//  * copies of <= 64 bytes: the source load is issued and the command loop goes on; the
-//    stores and the new (p1, p2) are completed when first needed (the next literals, the
-//    next copy, or the exit), so the load's latency overlaps the next command's header.
+//  * copies of <= 64 bytes: the source load is issued (LDS-DMA into one of kCopyQ slots) and
+//    the command loop goes on; a copy is completed (its stores, and the new (p1, p2)) only
+//    when something needs it: context-modelled literals (their first context is the copy's
+//    last two bytes), a later copy whose source may read its destination, a full queue, or
+//    the exit.  A run of copies (C4: 62 % of commands have no literals) thus keeps up to
+//    kCopyQ source loads in flight instead of waiting for each before the next is issued.
 template <bool kTrivial, bool kPart>
 __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
 #define U(x) __builtin_amdgcn_readfirstlane(x)
@@ -1693,11 +1708,27 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     pseen = g_lds.part_seen[LANE];
   }
   const int npostfix = U(s.npostfix), ndirect = U(s.ndirect), max_back = U(s.max_back);
-  int bo = U(s.bo), ho = U(s.ho), pos = U(s.pos), mbl = U(s.mbl);
-  // buf = half-words ho-2 .. ho+1 (acc is its low half); pf = half-word ho+2, in flight
-  uint64_t buf = (uint64_t)(uint32_t)U((int)s.acc) |
-                 ((uint64_t)((uint32_t)U((int)win16[ho]) | ((uint32_t)U((int)win16[ho + 1]) << 16)) << 32);
-  uint32_t pf = win16[ho + 2];
+  int pos = U(s.pos), mbl = U(s.mbl);
+  // Bit reader.  The reference's reader (acc, bo, ho: engine.ts:1764-1933, fill16 / readFewBits)
+  // is a function of two numbers: the bit position P (bits consumed from win[0]; P = 16 ho - 32
+  // + bo) and the position F of its last fill point -- a fill leaves bo = P mod 16, so then
+  // ho = (F >> 4) + 2 and bo = (F & 15) + (P - F).  The loop reads its bits at P from a 64-bit
+  // window W = bits [Pw, Pw + 64) (Pw a multiple of 32) with the next word N in an SGPR and the
+  // one after it in flight from LDS (Nv), so a refill is a register shift every 32 bits and
+  // never waits for LDS; every fill point of the general loop is the one instruction F = P.
+  // (acc, bo, ho) are rebuilt at the exit only.
+  const int bo_in = U(s.bo), ho_in = U(s.ho);
+  // (right after an input refill acc still holds the two half-words before win[0]: the general
+  // loop reads on until they are behind it)
+  if (ho_in < 2) return 0;
+  int P = 16 * ho_in - 32 + bo_in;
+  int F = P - bo_in + (bo_in & 15);
+  int Pw = P & ~31;
+  typedef const __attribute__((address_space(3))) uint32_t LU32;
+  LU32 *win32 = (LU32 *)g_lds.win;
+  uint64_t W = (uint64_t)(uint32_t)U((int)win32[Pw >> 5]) | ((uint64_t)(uint32_t)U((int)win32[(Pw >> 5) + 1]) << 32);
+  uint32_t N = (uint32_t)U((int)win32[(Pw >> 5) + 2]);
+  uint32_t Nv = win32[(Pw >> 5) + 3];
   int cmd_blen = U(s.cmd_blen), lit_blen = U(s.lit_blen), dist_blen = U(s.dist_blen), max_dist = U(s.max_dist);
   int dr0 = U(s.rings[0]), dr1 = U(s.rings[1]), dr2 = U(s.rings[2]), dr3 = U(s.rings[3]), dridx = U(s.dist_rb_idx);
   int c1 = U(ctx_byte(s, pos - 1, rmask));
@@ -1729,58 +1760,72 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   }
   int insert_len = 0, copy_len = 0, dist_code = 0, distance = 0, j = 0, phase = ST_MAIN_LOOP;
   uint32_t ncmd = 0;
-  // a copy whose source load is in flight: destination, length, the loaded byte per lane
-  int pend_cl = 0, pend_dst = 0;
-  // The source bytes of a copy in flight go to one of two LDS slots by DMA (pend_slot: which
-  // one), so the next copy's load can be issued before the copy in flight is completed.  (In
-  // registers, the loop-carried move of the newly loaded value waited for the load at the back
-  // edge, whatever the order of the code.)
-  int pend_slot = 0;
-  auto shift16 = [&]() {   // the reference's acc/ho step, fed from the buffer; next half-word requested
-    buf = (buf >> 16) | ((uint64_t)(uint32_t)U((int)pf) << 48);
-    ho++;
-    bo -= 16;
-    pf = win16[ho + 2];
+  // Copies whose source load is in flight, oldest first: destination and length (qd*, qc*),
+  // qn of them; the oldest's bytes arrive in LDS slot qhead, the next ones in the slots after
+  // it.  (In registers, the loop-carried move of a newly loaded value waited for the load at
+  // the back edge, whatever the order of the code: hence LDS-DMA.)  Destinations ascend, and
+  // in the context-modelled build no literal lies between two pending copies (literals first
+  // complete every copy), so completing them in order leaves (c1, c2b) = the last two bytes.
+  int qn = 0, qhead = 0;
+  int qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0, qc0 = 0, qc1 = 0, qc2 = 0, qc3 = 0;
+  static_assert(kCopyQ == 4, "the pending queue is four registers deep");
+  auto ensure = [&]() {   // at least 32 bits of W at P (every read is <= 24 bits)
+    if (P - Pw >= 32) {
+      W = (W >> 32) | ((uint64_t)N << 32);
+      Pw += 32;
+      N = (uint32_t)U((int)Nv);
+      Nv = win32[(Pw >> 5) + 3];
+    }
   };
-  auto fill = [&]() {   // fill16: ho stays below 2080 here
-    if (bo >= 16) shift16();
-  };
-  auto peek32 = [&]() -> uint32_t { return (uint32_t)(buf >> (bo & 63)); };
-  auto rbits = [&](int n) -> int {   // n <= 16 after fill()
-    int v = (int)(peek32() & ((1u << n) - 1u));
-    bo += n;
+  auto peek32 = [&]() -> uint32_t { return (uint32_t)(W >> (P - Pw)); };
+  // extra bits after a fill point (the general loop: LFILL16, then lbits, or for more than 16
+  // bits lmany -- whose force16 after the first 16 bits is a fill point too)
+  auto xbits = [&](int n) -> int {
+    ensure();
+    F = n > 16 ? P + 16 : P;
+    const int v = (int)(peek32() & ((1u << n) - 1u));
+    P += n;
     return v;
   };
-  auto rmany = [&](int n) -> int {
-    if (n <= 16) return rbits(n);
-    const int lo = rbits(16);
-    shift16();
-    return lo | (rbits(n - 16) << 16);
-  };
-  auto sym16 = [&](int root) -> int {
+  auto sym16 = [&](int root) -> int {   // after a fill point (F = P)
+    ensure();
     const uint32_t v = peek32();
     int off = root + (int)(v & 0xFF);
     int e = U((int)t16[off]);
     if ((e >> 12) > 8) {   // a second-level table: one branch around it, a common tail
       off += (e & 0xFFF) + (int)((v & ((1u << (e >> 12)) - 1u)) >> 8);
       e = U((int)t16[off]);
-      bo += 8;
+      P += 8;
     }
-    bo += e >> 12;
+    P += e >> 12;
     return e & 0xFFF;
   };
-  // complete the copy in flight: stores, literal context.  Its bytes arrive in LDS by DMA,
-  // which the compiler does not wait for: behind_next -- the next copy's DMA was the last
-  // memory instruction issued, so everything but the newest one must have landed; else all.
-  auto finish_copy = [&](bool behind_next = false) {
-    if (pend_cl) {
-      if (behind_next) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int v = (int)(pend_slot ? g_cpb[lane] : g_cpa[lane]);
-      if (lane < pend_cl) ring[pend_dst + lane] = (uint8_t)v;
-      c2b = pend_cl >= 2 ? __builtin_amdgcn_readlane(v, pend_cl - 2) : c1;
-      c1 = __builtin_amdgcn_readlane(v, pend_cl - 1);
-      pend_cl = 0;
+  auto ho_now = [&]() -> int { return (F >> 4) + 2; };   // the reference's ho
+  // Completing pending copies: their bytes arrive in LDS by DMA, which the compiler does not
+  // wait for.  vmcnt counts loads, stores and LDS-DMA together, in issue order, so the oldest
+  // copy's DMA has landed once at most qn - 1 vector-memory operations are outstanding: the
+  // qn - 1 DMAs issued after it are among the youngest (stores issued after it only make the
+  // wait longer, never too short).
+  auto store_oldest = [&]() {   // the oldest copy's bytes (landed) -> the ring, (p1, p2)
+    const int v = (int)g_cp[qhead][lane];
+    if (lane < qc0) ring[qd0 + lane] = (uint8_t)v;
+    if (!kTrivial) {   // (the trivial-context build never reads the context bytes here)
+      c2b = qc0 >= 2 ? __builtin_amdgcn_readlane(v, qc0 - 2) : c1;
+      c1 = __builtin_amdgcn_readlane(v, qc0 - 1);
+    }
+    qd0 = qd1; qd1 = qd2; qd2 = qd3;
+    qc0 = qc1; qc1 = qc2; qc2 = qc3;
+    qhead = (qhead + 1) & (kCopyQ - 1);
+    qn--;
+  };
+  auto complete_oldest = [&]() {
+    wait_vm(qn - 1);
+    store_oldest();
+  };
+  auto finish_copy = [&]() {   // every pending copy
+    if (qn) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      while (qn) store_oldest();
     }
   };
 #ifdef MIB_PROF
@@ -1798,34 +1843,28 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   for (;;) {
     FMARK(4);
     // ---- command boundary: a block switch or refill goes to the general loop
-    if (mbl <= 0 || cmd_blen == 0 || ho > 2030 - 8) break;
+    if (mbl <= 0 || cmd_blen == 0 || ho_now() > 2030 - 8) break;
     if (part && pos >= pub_next) {   // every output byte below pos is stored: publish
       finish_copy();
       part_publish(pos);
       pub_next = U(s.pub_next);
     }
-    const uint64_t buf0 = buf;
-    const uint32_t pf0 = pf;
-    int bo0 = bo, ho0 = ho;
-    fill();
+    const int P0 = P, F0 = F;
+    F = P;
     const int sym = sym16(cmd_root);
     const int cbits = kCmdLut[4 * sym], ins_off = kCmdLut[4 * sym + 1], copy_off = kCmdLut[4 * sym + 2];
     dist_code = kCmdLut[4 * sym + 3];
-    fill();
-    insert_len = ins_off + rmany(cbits & 0xFF);
-    fill();
-    copy_len = copy_off + rmany(cbits >> 8);
+    insert_len = ins_off + xbits(cbits & 0xFF);
+    copy_len = copy_off + xbits(cbits >> 8);
     // literals and copy must stay inside this block type, the window and the ring
     // (32-bit: pos < 2^30 and each length < 2^24 + 2^15, so the sum cannot overflow; a 64-bit
     // compare is a VALU op on VGPRs here, and the compiler drained vmcnt before it -- every
     // command then waited for the previous command's copy load and stores)
     if (insert_len > lit_blen || pos + insert_len + copy_len >= lim ||
-        ho + ((insert_len * 15) >> 4) > 2030 - 12) {
+        ho_now() + ((insert_len * 15) >> 4) > 2030 - 12) {
       // hand the command over undecoded
-      buf = buf0;
-      pf = pf0;
-      bo = bo0;
-      ho = ho0;
+      P = P0;
+      F = F0;
       break;
     }
     cmd_blen--;
@@ -1843,7 +1882,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
         while (pos < end) {
           const int seg_end = U(min(end, (pos | 63) + 1));
           while (pos < seg_end) {
-            fill();
+            F = P;
             const int val = sym16(lit_root);
             ob = write_lane(ob, (uint32_t)val, (uint32_t)(pos & 63));
             pos++;
@@ -1863,7 +1902,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
           while (pos < seg_end) {
             // the root row of the next literal (its p2 is the current c1), 4 entries per lane
             const uint64_t row = croot64[(lut1_of(c1) << 6) | lane];
-            fill();
+            F = P;
             c2b = c1;
             c1 = U(sym16(root));
             const uint64_t e = c1 & 2 ? row >> 32 : row;   // lane c1 >> 2 holds entries 4 (c1 >> 2) ..
@@ -1889,15 +1928,13 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     // ---- distance: anything unusual hands over with the literals done
     j = insert_len;
     phase = ST_INSERT_LOOP;
-    if (mbl - insert_len <= 0 || (dist_code >= 0 && dist_blen == 0) || ho > 2030 - 8) break;
-    const uint64_t dbuf = buf;
-    const uint32_t dpf = pf;
-    const int dbo = bo, dho = ho, dmax = max_dist;
+    if (mbl - insert_len <= 0 || (dist_code >= 0 && dist_blen == 0) || ho_now() > 2030 - 8) break;
+    const int dP = P, dF = F, dmax = max_dist;
     int dc = dist_code;
     if (dc < 0) {
       distance = ring_at(dridx);
     } else {
-      fill();
+      F = P;
       const uint32_t dpair = dc < 2 ? droot01 : droot23;
       dc = U(sym16((int)((dpair >> (16 * (dc & 1))) & 0xFFFF)));
       if (dc < 16) {
@@ -1913,13 +1950,14 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
           eb = 1 + (hcode >> 1);
           doff = ((((2 + (hcode & 1)) << eb) - 4) << npostfix) + lcode + ndirect + 1;
         }
+        // (the general loop: lbits while they fit its 32-bit accumulator, else a fill first)
         int bv;
-        if (bo + eb <= 32) {
+        if ((F & 15) + (P - F) + eb <= 32) {
+          ensure();
           bv = (int)(peek32() & ((1u << eb) - 1u));
-          bo += eb;
+          P += eb;
         } else {
-          fill();
-          bv = rmany(eb);
+          bv = xbits(eb);
         }
         distance = doff + (bv << npostfix);
       }
@@ -1929,10 +1967,8 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     const int src = (pos - distance) & rmask;
     if (distance < 0 || distance > max_dist || copy_len > mbl - insert_len || src + copy_len >= rmask) {
       // error, dictionary word or wrapping copy: redo the distance in the general loop
-      buf = dbuf;
-      pf = dpf;
-      bo = dbo;
-      ho = dho;
+      P = dP;
+      F = dF;
       max_dist = dmax;
       break;
     }
@@ -1963,20 +1999,26 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       // register -- it did so inside the literal loop, once per literal.
       if (cl <= 64) {   // one lane per byte: issue the load, complete later
         const int q = dist >= cl ? lane : lane % dist;
-        // A copy's source that ends before the copy in flight's destination does not need its
-        // bytes: its load is issued first and the copy in flight completed behind it, so the
-        // two loads overlap (C4: 62 % of commands have no literals, copy after copy).
-        // Otherwise (it may read them) the copy in flight is completed first.
-        if (src + cl > pend_dst) finish_copy();
+        // Pending copies whose destination the source may read are completed first (the
+        // destinations ascend: while the oldest starts below the source's end); then, with the
+        // queue full, the oldest.  Sources far back (C4: half the distances exceed 64 KiB)
+        // need neither, so the loads of a run of copies overlap.
+        while (qn && src + cl > qd0) complete_oldest();
+        if (qn == kCopyQ) complete_oldest();
         const int at = src + (lane < cl ? q : 0);
         typedef __attribute__((address_space(3))) void LV;
         typedef __attribute__((address_space(1))) void GV;
-        if (pend_slot) __builtin_amdgcn_global_load_lds((GV *)(ring + at), (LV *)g_cpa, 1, 0, 0);   // lane l -> dword l
-        else __builtin_amdgcn_global_load_lds((GV *)(ring + at), (LV *)g_cpb, 1, 0, 0);
-        finish_copy(true);
-        pend_slot ^= 1;
-        pend_dst = pos;
-        pend_cl = cl;
+        const int slot = (qhead + qn) & (kCopyQ - 1);
+        __builtin_amdgcn_global_load_lds((GV *)(ring + at), (LV *)g_cp[slot], 1, 0, 0);   // lane l -> dword l
+        qd0 = qn == 0 ? pos : qd0;   // (selects: the new copy is entry qn)
+        qc0 = qn == 0 ? cl : qc0;
+        qd1 = qn == 1 ? pos : qd1;
+        qc1 = qn == 1 ? cl : qc1;
+        qd2 = qn == 2 ? pos : qd2;
+        qc2 = qn == 2 ? cl : qc2;
+        qd3 = qn == 3 ? pos : qd3;
+        qc3 = qn == 3 ? cl : qc3;
+        qn++;
       } else {
         finish_copy();   // (this copy may read it)
         int lastv = 0;
@@ -2028,7 +2070,13 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   }
   finish_copy();
   wave_sync();
-  s.acc = (uint32_t)buf; s.bo = bo; s.ho = ho; s.pos = pos; s.mbl = mbl;
+  {
+    const int ho = ho_now();
+    s.acc = (uint32_t)win16[ho - 2] | ((uint32_t)win16[ho - 1] << 16);
+    s.bo = (F & 15) + (P - F);
+    s.ho = ho;
+  }
+  s.pos = pos; s.mbl = mbl;
   s.cmd_blen = cmd_blen; s.lit_blen = lit_blen; s.dist_blen = dist_blen; s.max_dist = max_dist;
   s.rings[0] = dr0; s.rings[1] = dr1; s.rings[2] = dr2; s.rings[3] = dr3; s.dist_rb_idx = dridx;
   s.insert_len = insert_len; s.copy_len = copy_len; s.dist_code = dist_code; s.j = j;

@@ -69,6 +69,9 @@ struct Job {                // one stream (or streaming chunk) to encode
   int32_t dc_out[4];        // and after the last command
   uint32_t hist;            // streaming: bytes of the stream before data[0] that copies may reach
   uint32_t abs_base;        // streaming: stream position of data[0] (mod 2^32)
+  uint32_t win_abs;         // min(stream position of data[0], 2^24): the window a dictionary
+                            // distance lies beyond is min(win_abs + p, max backward), exact
+                            // past 4 GiB of stream too (max backward < 2^24)
   uint32_t *hist_tab;       // streaming: the encoder's bucket table of earlier positions, or null
   uint32_t dict;            // 1: static-dictionary references allowed (one-shot, lgwin <= 22, q >= 10)
   uint32_t dict_span;       // ... at stream positions below this (where the window is still short)

@@ -156,7 +156,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
   const uint8_t *data = nullptr;
   int ndirect = 0, npostfix = 0;
-  uint32_t parts = 0, abs0 = 0, pbits = 16, plag = 0, maxback = 0, cdl = 0;
+  uint32_t parts = 0, abs0 = 0, wabs = 0, pbits = 16, plag = 0, maxback = 0, cdl = 0;
   bool words = false;
   if (sgi < nsegs) {
     const Seg &sg = segs[sgi];
@@ -169,7 +169,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     ndirect = (int)jb.ndirect;
     npostfix = (int)jb.npostfix;
     parts = jb.parts;
-    abs0 = jb.abs_base;
+    abs0 = jb.abs_base;   // (part alignment: mod 2^32 is exact)
+    wabs = jb.win_abs;     // (dictionary distances: saturated, no wrap past 4 GiB)
     pbits = jb.part_bits;
     plag = jb.part_lag;
     maxback = (1u << jb.lgwin) - 16;
@@ -256,9 +257,9 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         if (KD && md == kCDictMark) {   // a custom-dictionary copy (the only entry): its exact length
           word = ln == match_length(cur.m[q]) ? 1u : 0u;   // cut by the segment end: unusable
           ln = word ? ln : 0u;
-          d = min(abs0 + p, maxback) + ln;
+          d = min(wabs + p, maxback) + ln;
         } else if (words && is_dict(md)) {   // a dictionary word (the only entry): its distance at p, its exact length
-          d = min(abs0 + p, maxback) + 1 + cdl + (md & 0x7FF);   // (a custom dictionary comes first, engine.ts:907)
+          d = min(wabs + p, maxback) + 1 + cdl + (md & 0x7FF);   // (a custom dictionary comes first, engine.ts:907)
           md = d | kDictFlag;
           word = ln == match_length(cur.m[q]) ? 1u : 0u;   // cut by the segment end: unusable
           ln = word ? ln : 0u;
@@ -407,7 +408,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
         nd = match_dist(x);
-        if (KD && nd == kCDictMark) nd = min(abs0 + i, maxback) + l;   // (d of the copy at i: see kCDictMark)
+        if (KD && nd == kCDictMark) nd = min(wabs + i, maxback) + l;   // (d of the copy at i: see kCDictMark)
         const float alt = __builtin_fmaf((float)(x >> 24), 0.25f, pn);   // (exact: code / 4 needs no rounding)
         // a match at the path's last distance is priced with short code 0
         const uint32_t use_last = 0u - (uint32_t)(nd == ld);   // a select, not a branch
@@ -562,7 +563,13 @@ __global__ __launch_bounds__(64) void merge_pieces_kernel(const Job *jobs, Seg *
     uint32_t m = pc.ncmd;
     if (m && n && carry == 0) {   // the previous piece ended in a copy: does this one continue it?
       const RawCmd f = src[0], p = dst[n - 1];
-      if (f.ins == 0 && f.dist == p.dist && !is_word(jb, f.dist)) {
+      // Never a dictionary copy: a word, or a custom-dictionary tail copy (its distance lies
+      // beyond the window at its start, pc.start - p.len: see kCDictMark) -- the copy at the
+      // next piece's start with that same distance reads the window (for a tail copy, from
+      // stream byte 0), and one joined copy would read past the dictionary's end.
+      const uint32_t maxback = (1u << jb.lgwin) - 16;
+      const bool p_dict = is_word(jb, p.dist) || (jb.cdict && p.dist > min(jb.win_abs + (pc.start - p.len), maxback));
+      if (f.ins == 0 && f.dist == p.dist && !p_dict && !is_word(jb, f.dist)) {
         wave_sync();
         if (lane == 0) dst[n - 1].len = p.len + f.len;
         src++;

@@ -128,6 +128,7 @@ struct StreamDesc {
   uint32_t prev_bytes;   // p1 | p2 << 8 before data[0] (streaming)
   uint32_t hist;         // streaming: history bytes before data[0] (device-resident, contiguous)
   uint32_t abs_base;     // streaming: stream position of data[0]
+  uint32_t win_abs;      // min(stream position of data[0], 2^24) (dictionary distances)
   uint32_t *hist_tab;    // streaming: the encoder's bucket table (null: none)
   uint64_t out_base;     // streaming: stream bytes emitted before this chunk
   bool streaming;        // a BrotliEncoder chunk (part index whenever it has segments to split)
@@ -318,6 +319,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     jb.prev_bytes = sd[j].prev_bytes;
     jb.hist = sd[j].hist;
     jb.abs_base = sd[j].abs_base;
+    jb.win_abs = sd[j].win_abs;
     jb.hist_tab = sd[j].hist_tab;
     if (jb.hist_tab) any_hist = true;
     jb.out_base = sd[j].out_base;
@@ -636,6 +638,7 @@ void fill_desc(StreamDesc &d, const uint8_t *p, uint64_t n, const Params &prm, b
   d.prev_bytes = 0;
   d.hist = 0;
   d.abs_base = 0;
+  d.win_abs = 0;
   d.hist_tab = nullptr;
   d.out_base = 0;
   d.streaming = !one_shot;
@@ -692,6 +695,7 @@ constexpr uint64_t kMaxChunk = 256ull << 20;   // BrotliEncoder: the largest dev
 constexpr uint64_t kStage = 8ull << 20;
 constexpr uint64_t kStageBudget = 256ull << 20;
 std::atomic<uint64_t> g_stage_bytes{0};
+std::atomic<int> g_live_encoders{0};   // BrotliEncoder objects alive (the default context keeps their workspace)
 uint64_t out_bound(uint64_t n) { return n + n / 8 + 4096 + 16 + sizeof(PartHead) + ((n + kSeg - 1) / kSeg) * sizeof(PartEntry); }
 
 }  // namespace
@@ -732,6 +736,15 @@ void mib_encode_ws_free(void *p) {
   if (!ws) return;
   if (ws->buf) hipFree(ws->buf);
   delete ws;
+}
+int mib_live_encoders(void) { return g_live_encoders.load(); }
+// the default context after a host call: a workspace above `keep` bytes is released
+void mib_encode_ws_trim(void **p, uint64_t keep) {
+  Workspace *ws = reinterpret_cast<Workspace *>(*p);
+  if (ws && ws->cap > keep) {
+    mib_encode_ws_free(ws);
+    *p = nullptr;
+  }
 }
 
 int mib_ctx_encode(mib_ctx *c, const mib_enc_opts *o, const uint8_t *d_in, const uint64_t *in_offsets, size_t k,
@@ -887,6 +900,7 @@ static int encoder_run(mib_ctx *c, mib_encoder *const *es, const uint64_t *ns, c
     sd[i].prev_bytes = e->prev_bytes;
     sd[i].hist = (uint32_t)e->hist;
     sd[i].abs_base = (uint32_t)e->abs;
+    sd[i].win_abs = (uint32_t)std::min<uint64_t>(e->abs, 1u << 24);
     sd[i].hist_tab = e->tab;
     sd[i].out_base = e->obytes;
     e->ddict.attach(sd[i]);
@@ -960,6 +974,7 @@ int mib_encode_batch(const mib_span *in, size_t k, const mib_enc_opts *o, mib_bu
 mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
   if (o && o->dict && o->dict_len >= (1ull << 31)) return nullptr;
   mib_encoder *e = new mib_encoder();
+  g_live_encoders++;
   if (o) e->opts = *o;
   else mib_enc_opts_default(&e->opts);
   if (o && o->dict && o->dict_len) e->dict.assign(o->dict, o->dict + o->dict_len);
@@ -1102,6 +1117,7 @@ void mib_encoder_free(mib_encoder *e) {
     g_stage_bytes.fetch_sub(kStage);
   }
   delete e;
+  g_live_encoders--;
 }
 
 }  // extern "C"

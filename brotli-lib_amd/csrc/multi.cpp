@@ -3,9 +3,16 @@
 // heaviest buffer to the least-loaded shard, like brotli_amd/shard.py), one host thread and
 // one mib_ctx per shard; shard s runs on visible device s % device_count, so a one-GPU host
 // can run two shards on one device (how the tests exercise the sharding).  Outputs come back
-// in input order.  Only the public C ABI is used: each shard is an ordinary device-resident
-// batch (mib_ctx_encode / mib_ctx_decode).  Nothing crosses between GPUs: the buffers are
-// independent, so there is no collective; the results meet in host memory.
+// in input order.  Nothing crosses between GPUs: the buffers are independent, so there is no
+// collective; the results meet in host memory.
+//
+// A shard is a context plus its host-side staging, kept across calls in a pool (the same
+// hygiene as the single-GPU host path, runtime.cpp): device input / output buffers are the
+// context's staging slots (no hipMalloc / hipFree per call), the inputs are packed into a
+// pinned host buffer and cross PCIe in ONE asynchronous copy per shard, and the results come
+// back the same way (one copy per shard, then host copies into the result buffers) instead of
+// one pageable hipMemcpy per buffer.  Concurrent sharded calls take different shards from the
+// pool (created on demand), so they run side by side instead of queueing on one lock.
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 #include <string.h>
@@ -17,19 +24,76 @@
 
 #include "../../include/brotli_amd.h"
 
-// runtime.cpp: result buffers from device memory (mib_set_allocator's allocator)
-extern "C" int mib_buf_from_device(mib_buf *out, const void *d_src, uint64_t len);
-extern "C" int mib_bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len);
+// runtime.cpp: result buffers (mib_set_allocator's allocator), the context's stream and staging
+extern "C" uint8_t *mib_buf_alloc(size_t n);
+extern "C" void *mib_ctx_stream_of(mib_ctx *c);
+extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need);
+extern "C" void mib_ctx_trim(mib_ctx *c, uint64_t keep_stage, uint64_t keep_scratch);
 
 namespace {
 
 constexpr int kMaxShards = 64;
-std::mutex g_multi_mu;                 // one sharded call at a time: the shard contexts are reused
-mib_ctx *g_shard_ctx[kMaxShards];      // shard s -> its context (device s % n), created on first use
+// a shard's buffers above these sizes are released after the call (a batch of the usual size
+// keeps its buffers; one huge batch does not pin GiBs of host and device memory forever)
+constexpr uint64_t kKeepPinned = 1ull << 30;
+constexpr uint64_t kKeepDevice = 4ull << 30;
 
 int device_count() {
   int n = 0;
   return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
+struct Shard {
+  int device = -1;
+  mib_ctx *ctx = nullptr;
+  uint8_t *pin = nullptr;   // pinned host staging (inputs in, results out)
+  uint64_t pin_cap = 0;
+  uint8_t *pinned(uint64_t need) {
+    if (pin_cap >= need) return pin;
+    if (pin) hipHostFree(pin);
+    pin = nullptr;
+    pin_cap = 0;
+    const uint64_t n = std::max<uint64_t>(need, 1 << 20);
+    if (hipHostMalloc((void **)&pin, n, hipHostMallocDefault) != hipSuccess) {
+      pin = nullptr;
+      return nullptr;
+    }
+    pin_cap = n;
+    return pin;
+  }
+  void trim() {
+    if (pin && pin_cap > kKeepPinned) {
+      hipHostFree(pin);
+      pin = nullptr;
+      pin_cap = 0;
+    }
+    mib_ctx_trim(ctx, kKeepDevice, kKeepDevice);
+  }
+};
+
+std::mutex g_pool_mu;                        // guards the free lists only
+std::vector<Shard *> g_pool[kMaxShards];     // idle shards for shard index s (device s % n)
+
+Shard *acquire(int s, int dev) {
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool[s].empty()) {
+      Shard *sh = g_pool[s].back();
+      g_pool[s].pop_back();
+      return sh;
+    }
+  }
+  mib_ctx *c = mib_ctx_new(dev);
+  if (!c) return nullptr;
+  Shard *sh = new Shard();
+  sh->device = dev;
+  sh->ctx = c;
+  return sh;
+}
+void release(int s, Shard *sh) {
+  sh->trim();
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_pool[s].push_back(sh);
 }
 
 // size-balanced assignment: buffers by size, largest first, each to the least-loaded shard
@@ -48,80 +112,114 @@ std::vector<std::vector<size_t>> assign(const mib_span *in, size_t k, int shards
   return out;
 }
 
-struct DevBuf {
-  void *p = nullptr;
-  ~DevBuf() {
-    if (p) hipFree(p);
-  }
-  int alloc(uint64_t n) {
-    return hipMalloc(&p, n ? n : 1) == hipSuccess ? 0 : MIB_E_OUT_OF_MEMORY;
-  }
-  uint8_t *u8() const { return (uint8_t *)p; }
-};
+uint64_t align256(uint64_t n) { return (n + 255) & ~255ull; }
 
-int encode_shard(mib_ctx *c, const mib_span *in, const std::vector<size_t> &idx, const mib_enc_opts *o, mib_buf *out,
-                 int *status) {
+// The shard's inputs packed back to back (the device-resident ABI reads stream i from
+// [in_offsets[i], in_offsets[i + 1])) into the pinned buffer, 64 zero bytes after the last,
+// then one copy to device staging slot 0.
+int upload(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, std::vector<uint64_t> &ioff, uint8_t **d_in,
+           hipStream_t st) {
   const size_t k = idx.size();
-  if (!k) return 0;
-  std::vector<uint64_t> ioff(k + 1, 0), ooff(k + 1, 0);   // the shard's streams packed back to back
-  uint64_t cap = 0;
-  for (size_t q = 0; q < k; q++) {
-    const uint64_t n = in[idx[q]].size;
-    ioff[q + 1] = ioff[q] + n;
-    cap += n + n / 8 + 8192 + ((n >> 16) + 1) * 72;   // (the encoder's bound: stored blocks + a part index)
-  }
-  DevBuf din, dout;
-  int rc;
-  if ((rc = din.alloc(ioff[k] + 64)) || (rc = dout.alloc(cap + 64))) return rc;
+  ioff.assign(k + 1, 0);
+  for (size_t q = 0; q < k; q++) ioff[q + 1] = ioff[q] + in[idx[q]].size;
+  uint8_t *pin = sh.pinned(ioff[k] + 64);
+  *d_in = mib_ctx_stage(sh.ctx, 0, ioff[k] + 64);
+  if (!pin || !*d_in) return MIB_E_OUT_OF_MEMORY;
   for (size_t q = 0; q < k; q++)
-    if (in[idx[q]].size && hipMemcpy(din.u8() + ioff[q], in[idx[q]].data, in[idx[q]].size, hipMemcpyHostToDevice) != hipSuccess)
-      return MIB_E_NO_DEVICE;
-  if ((rc = mib_ctx_encode(c, o, din.u8(), ioff.data(), k, dout.u8(), cap, ooff.data(), nullptr))) return rc;
-  std::vector<mib_buf *> outs(k);
-  std::vector<const uint8_t *> src(k);
-  std::vector<uint64_t> lens(k);
-  for (size_t q = 0; q < k; q++) {
-    outs[q] = &out[idx[q]];
-    src[q] = dout.u8() + ooff[q];
-    lens[q] = ooff[q + 1] - ooff[q];
-    status[idx[q]] = 0;
-  }
-  if ((rc = mib_bufs_from_device(k, outs.data(), src.data(), lens.data()))) return rc;
+    if (in[idx[q]].size) memcpy(pin + ioff[q], in[idx[q]].data, in[idx[q]].size);
+  memset(pin + ioff[k], 0, 64);
+  if (hipMemcpyAsync(*d_in, pin, ioff[k] + 64, hipMemcpyHostToDevice, st) != hipSuccess) return MIB_E_NO_DEVICE;
   return 0;
 }
 
-int decode_shard(mib_ctx *c, const mib_span *in, const std::vector<size_t> &idx, mib_buf *out, int *status) {
+// Results [d_src[q], + len[q]) on the device -> out[idx[q]]: packed into the pinned buffer by
+// one asynchronous copy per result (no pageable copies, one wait), then host copies.
+int download(Shard &sh, const std::vector<size_t> &idx, const std::vector<const uint8_t *> &d_src,
+             const std::vector<uint64_t> &len, const std::vector<bool> &want, mib_buf *out, hipStream_t st) {
+  const size_t k = idx.size();
+  std::vector<uint64_t> poff(k + 1, 0);
+  for (size_t q = 0; q < k; q++) poff[q + 1] = poff[q] + (want[q] ? align256(len[q]) : 0);
+  uint8_t *pin = sh.pinned(poff[k] + 64);
+  if (!pin) return MIB_E_OUT_OF_MEMORY;
+  for (size_t q = 0; q < k; q++)
+    if (want[q] && len[q] && hipMemcpyAsync(pin + poff[q], d_src[q], len[q], hipMemcpyDeviceToHost, st) != hipSuccess)
+      return MIB_E_NO_DEVICE;
+  if (hipStreamSynchronize(st) != hipSuccess) return MIB_E_NO_DEVICE;
+  for (size_t q = 0; q < k; q++) {
+    if (!want[q]) continue;
+    mib_buf &o = out[idx[q]];
+    o.data = mib_buf_alloc(len[q]);
+    o.size = 0;
+    if (!o.data) return MIB_E_OUT_OF_MEMORY;
+    o.size = len[q];
+    if (len[q]) memcpy(o.data, pin + poff[q], len[q]);
+  }
+  return 0;
+}
+
+int encode_shard(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, const mib_enc_opts *o, mib_buf *out,
+                 int *status) {
   const size_t k = idx.size();
   if (!k) return 0;
-  std::vector<uint64_t> ioff(k + 1, 0), ooff(k + 1, 0);
+  hipStream_t st = (hipStream_t)mib_ctx_stream_of(sh.ctx);
+  std::vector<uint64_t> ioff, ooff(k + 1, 0);
+  uint8_t *d_in = nullptr;
+  int rc;
+  if ((rc = upload(sh, in, idx, ioff, &d_in, st))) return rc;
+  uint64_t cap = 0;
+  for (size_t q = 0; q < k; q++) {
+    const uint64_t n = in[idx[q]].size;
+    cap += n + n / 8 + 8192 + ((n >> 16) + 1) * 72;   // (the encoder's bound: stored blocks + a part index)
+  }
+  uint8_t *d_out = mib_ctx_stage(sh.ctx, 1, cap + 64);
+  if (!d_out) return MIB_E_OUT_OF_MEMORY;
+  if ((rc = mib_ctx_encode(sh.ctx, o, d_in, ioff.data(), k, d_out, cap, ooff.data(), st))) return rc;
+  std::vector<const uint8_t *> src(k);
+  std::vector<uint64_t> lens(k);
+  std::vector<bool> want(k, true);
+  for (size_t q = 0; q < k; q++) {
+    src[q] = d_out + ooff[q];
+    lens[q] = ooff[q + 1] - ooff[q];
+    status[idx[q]] = 0;
+  }
+  return download(sh, idx, src, lens, want, out, st);
+}
+
+int decode_shard(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, mib_buf *out, int *status) {
+  const size_t k = idx.size();
+  if (!k) return 0;
+  hipStream_t st = (hipStream_t)mib_ctx_stream_of(sh.ctx);
+  std::vector<uint64_t> ioff, ooff(k + 1, 0);
   for (size_t q = 0; q < k; q++) {
     const mib_span &s = in[idx[q]];
-    ioff[q + 1] = ioff[q] + s.size;
     const int64_t est = mib_decoded_size(s.data, s.size);
     // a header size, else room for a part-indexed stream's total (known only from its index),
     // else 8x the input; a stream that outgrows it is decoded again alone
     const uint64_t capq = est > 0 ? (uint64_t)est : std::max<uint64_t>(1 << 16, 8 * (uint64_t)s.size);
-    ooff[q + 1] = ooff[q] + ((capq + 4096 + 255) & ~255ull);
+    ooff[q + 1] = ooff[q] + align256(capq + 4096);
   }
-  DevBuf din, dout;
+  uint8_t *d_in = nullptr;
   int rc;
-  if ((rc = din.alloc(ioff[k] + 64)) || (rc = dout.alloc(ooff[k] + 64))) return rc;
-  for (size_t q = 0; q < k; q++)
-    if (in[idx[q]].size && hipMemcpy(din.u8() + ioff[q], in[idx[q]].data, in[idx[q]].size, hipMemcpyHostToDevice) != hipSuccess)
-      return MIB_E_NO_DEVICE;
+  if ((rc = upload(sh, in, idx, ioff, &d_in, st))) return rc;
+  uint8_t *d_out = mib_ctx_stage(sh.ctx, 1, ooff[k] + 64);
+  if (!d_out) return MIB_E_OUT_OF_MEMORY;
   std::vector<int64_t> sizes(k);
-  std::vector<int> st(k);
-  rc = mib_ctx_decode(c, din.u8(), ioff.data(), k, dout.u8(), ooff.data(), sizes.data(), st.data(), nullptr);
+  std::vector<int> stv(k);
+  rc = mib_ctx_decode(sh.ctx, d_in, ioff.data(), k, d_out, ooff.data(), sizes.data(), stv.data(), st);
   if (rc && rc != MIB_E_NEED_SPACE) return rc;
+  std::vector<const uint8_t *> src(k);
+  std::vector<uint64_t> lens(k);
+  std::vector<bool> want(k);
   for (size_t q = 0; q < k; q++) {
-    const size_t i = idx[q];
-    status[i] = st[q];
-    if (st[q] == 0) {
-      if ((rc = mib_buf_from_device(&out[i], dout.u8() + ooff[q], (uint64_t)sizes[q]))) return rc;
-    } else if (st[q] == MIB_E_NEED_SPACE) {
-      status[i] = mib_decode(in[i].data, in[i].size, nullptr, 0, -1, -1, &out[i]);   // the growing single-stream path
-    }
+    status[idx[q]] = stv[q];
+    want[q] = stv[q] == 0;
+    src[q] = d_out + ooff[q];
+    lens[q] = want[q] ? (uint64_t)sizes[q] : 0;
   }
+  if ((rc = download(sh, idx, src, lens, want, out, st))) return rc;
+  for (size_t q = 0; q < k; q++)
+    if (stv[q] == MIB_E_NEED_SPACE)   // the growing single-stream path
+      status[idx[q]] = mib_decode(in[idx[q]].data, in[idx[q]].size, nullptr, 0, -1, -1, &out[idx[q]]);
   return 0;
 }
 
@@ -132,21 +230,26 @@ int run_shards(const mib_span *in, size_t k, int n_gpus, F fn) {
   if (ndev <= 0) return MIB_E_NO_DEVICE;
   int shards = n_gpus <= 0 ? ndev : n_gpus;
   shards = std::max(1, std::min<int>({shards, kMaxShards, (int)std::max<size_t>(k, 1)}));
-  std::lock_guard<std::mutex> lk(g_multi_mu);
+  std::vector<Shard *> sh(shards, nullptr);
+  int rc = 0;
+  for (int s = 0; s < shards && !rc; s++)
+    if (!(sh[s] = acquire(s, s % ndev))) rc = MIB_E_NO_DEVICE;
+  if (!rc) {
+    const std::vector<std::vector<size_t>> parts = assign(in, k, shards);
+    std::vector<int> rcs(shards, 0);
+    std::vector<std::thread> th;
+    for (int s = 0; s < shards; s++)
+      th.emplace_back([&, s] {
+        hipSetDevice(sh[s]->device);
+        rcs[s] = fn(*sh[s], parts[s]);
+      });
+    for (auto &t : th) t.join();
+    for (int r : rcs)
+      if (r && !rc) rc = r;
+  }
   for (int s = 0; s < shards; s++)
-    if (!g_shard_ctx[s] && !(g_shard_ctx[s] = mib_ctx_new(s % ndev))) return MIB_E_NO_DEVICE;
-  const std::vector<std::vector<size_t>> parts = assign(in, k, shards);
-  std::vector<int> rcs(shards, 0);
-  std::vector<std::thread> th;
-  for (int s = 0; s < shards; s++)
-    th.emplace_back([&, s] {
-      hipSetDevice(s % ndev);
-      rcs[s] = fn(g_shard_ctx[s], parts[s]);
-    });
-  for (auto &t : th) t.join();
-  for (int r : rcs)
-    if (r) return r;
-  return 0;
+    if (sh[s]) release(s, sh[s]);
+  return rc;
 }
 
 }  // namespace
@@ -162,8 +265,8 @@ int mib_encode_batch_n(const mib_span *in, size_t k, const mib_enc_opts *o, int 
     if ((!in[i].data && in[i].size) || in[i].size >= (1ull << 31)) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
-  const int rc = run_shards(in, k, n_gpus, [&](mib_ctx *c, const std::vector<size_t> &idx) {
-    return encode_shard(c, in, idx, o, out, status);
+  const int rc = run_shards(in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) {
+    return encode_shard(sh, in, idx, o, out, status);
   });
   if (rc)
     for (size_t i = 0; i < k; i++) mib_buf_free(&out[i]);
@@ -179,8 +282,8 @@ int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, i
     if (!in[i].data && in[i].size) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
-  const int rc = run_shards(in, k, n_gpus, [&](mib_ctx *c, const std::vector<size_t> &idx) {
-    return decode_shard(c, in, idx, out, status);
+  const int rc = run_shards(in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) {
+    return decode_shard(sh, in, idx, out, status);
   });
   if (rc)
     for (size_t i = 0; i < k; i++) mib_buf_free(&out[i]);

@@ -423,11 +423,24 @@ int mib_buf_from_device(mib_buf *out, const void *d_src, uint64_t len) {
   out->size = 0;
   if (!out->data) return MIB_E_OUT_OF_MEMORY;
   out->size = len;
-  if (len && hipMemcpy(out->data, d_src, len, hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
+  if (len && hipMemcpy(out->data, d_src, len, hipMemcpyDeviceToHost) != hipSuccess) {
+    mib_buf_free(out);
+    return MIB_E_NO_DEVICE;
+  }
   return 0;
 }
 
+static int bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len);
+// On failure no result stays allocated: a caller that reports the error keeps no buffer
+// (the Python mirror's allocator would otherwise hold those bytes for the process' life)
 int mib_bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len) {
+  for (size_t i = 0; i < k; i++) outs[i]->data = nullptr, outs[i]->size = 0;
+  const int rc = bufs_from_device(k, outs, d_src, len);
+  if (rc)
+    for (size_t i = 0; i < k; i++) mib_buf_free(outs[i]);
+  return rc;
+}
+static int bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const *d_src, const uint64_t *len) {
   if (!k) return 0;
   const uint8_t *lo = d_src[0], *hi = d_src[0];
   uint64_t sum = 0;
@@ -533,10 +546,58 @@ void mib_part_stats(mib_ctx *c, uint64_t *parallel, uint64_t *fallback) {
 
 // internal (encode.hip)
 mib_ctx *mib_default_ctx(void) { return default_ctx(); }
-void mib_default_lock(int on) {
-  if (on) g_default_mu.lock();
-  else g_default_mu.unlock();
+// The host-memory entry points (here, encode.hip, woff2.hip) hold the default context for one
+// call at a time; when the outermost of them returns, buffers a large call grew are released:
+// a long-lived server keeps what its usual calls need (the latency path stays free of
+// hipMalloc), not GiBs reserved since its largest call (a 1 GiB brotliDecode: a 1 GiB input
+// stage and a 2 GiB output stage).
+constexpr uint64_t kKeepStage = 64ull << 20;      // staging buffers (input, output, dictionary, encoder output)
+constexpr uint64_t kKeepScratch = 1ull << 30;     // decoder scratch, part tables, encoder workspace
+int g_default_depth = 0;                          // (guarded by g_default_mu)
+extern "C" void mib_encode_ws_trim(void **ws, uint64_t keep);
+extern "C" int mib_live_encoders(void);
+static void release_large(uint8_t **p, uint64_t *cap, uint64_t keep) {
+  if (*p && *cap > keep) {
+    hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+  }
 }
+static void trim_default_ctx(mib_ctx *c) {
+  hipSetDevice(c->device);
+  // (while a BrotliEncoder lives, its chunk after chunk reuses the workspace and the encoder
+  // output stage: kept)
+  const bool streaming = mib_live_encoders() > 0;
+  for (int i = 0; i < 4; i++)
+    if (!(streaming && i == 3)) release_large(&c->stage[i], &c->stage_cap[i], kKeepStage);
+  release_large(&c->d_scratch, &c->scratch_bytes, kKeepScratch);
+  release_large(&c->d_parts, &c->parts_bytes, kKeepScratch);
+  if (!streaming) mib_encode_ws_trim(&c->enc_ws, kKeepScratch);
+}
+// a context's buffers above these sizes (staging slots; decoder scratch, part tables and
+// encoder workspace), released (multi.cpp's shard contexts after each sharded call)
+void mib_ctx_trim(mib_ctx *c, uint64_t keep_stage, uint64_t keep_scratch) {
+  hipSetDevice(c->device);
+  for (int i = 0; i < 4; i++) release_large(&c->stage[i], &c->stage_cap[i], keep_stage);
+  release_large(&c->d_scratch, &c->scratch_bytes, keep_scratch);
+  release_large(&c->d_parts, &c->parts_bytes, keep_scratch);
+  mib_encode_ws_trim(&c->enc_ws, keep_scratch);
+}
+void mib_default_lock(int on) {
+  if (on) {
+    g_default_mu.lock();
+    g_default_depth++;
+  } else {
+    if (--g_default_depth == 0 && g_default_ctx) trim_default_ctx(g_default_ctx);
+    g_default_mu.unlock();
+  }
+}
+namespace {
+struct DefaultUse {   // mib_default_lock for this file's entry points
+  DefaultUse() { mib_default_lock(1); }
+  ~DefaultUse() { mib_default_lock(0); }
+};
+}  // namespace
 int mib_ctx_ready(mib_ctx *c) { return c ? ensure_device(c->device) : MIB_E_INVALID_ARG; }
 void *mib_ctx_stream_of(mib_ctx *c) { return (void *)c->stream; }
 int mib_ctx_device_of(mib_ctx *c) { return c->device; }
@@ -781,7 +842,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
   if (!out || (!in && n)) return MIB_E_INVALID_ARG;
   out->data = nullptr;
   out->size = 0;
-  std::lock_guard<std::recursive_mutex> use(g_default_mu);
+  DefaultUse use;
   mib_ctx *c = default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
   hipSetDevice(c->device);
@@ -866,7 +927,7 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
 }
 
 int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
-  std::lock_guard<std::recursive_mutex> use(g_default_mu);
+  DefaultUse use;
   mib_ctx *c = default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
   hipSetDevice(c->device);

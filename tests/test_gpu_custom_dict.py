@@ -53,6 +53,27 @@ def test_one_shot_tail_copies(q, lgwin):
     assert alone != data
 
 
+@pytest.mark.parametrize('q', [11, 9])
+def test_tail_copy_ending_on_a_parse_piece_boundary(q):
+    """a dictionary tail copy that ends exactly on an 8 KiB parse-piece
+    boundary B has distance min(B - L, max) + L = B; a window copy starting at B that repeats
+    the stream's first bytes has distance B too.  Joining the two (as two window copies of one
+    distance are joined across pieces) would make one dictionary copy longer than the tail:
+    the reference decoder reads past the dictionary and fails.  Each piece boundary of the
+    first segment is tried, with unique bytes around it."""
+    import random
+    d = c5_dictionary(8192, 21)
+    rnd = random.Random(99)
+    for B in (8192, 16384, 40960):
+        L = 37
+        head = bytes(rnd.getrandbits(8) for _ in range(B - L))
+        data = head + d[-L:] + head[:300] + bytes(rnd.getrandbits(8) for _ in range(5000))
+        r0 = _oracle.compound_refs()
+        enc = brotli_amd.brotliEncode(data, {'quality': q, 'customDictionary': d})
+        _both(data, enc, d)
+        assert _oracle.compound_refs() > r0, 'the tail copy before the boundary was not emitted'
+
+
 def test_int8_dictionary_and_small_inputs():
     import array
     d = c5_dictionary(4096, 7)
