@@ -75,6 +75,7 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=10.0, help='target wall time of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true')
+    ap.add_argument('--stream-chunk', type=int, default=32, help='c5: BrotliEncoder streamChunk in MiB (0: the reference\'s cadence)')
     return ap.parse_args()
 
 
@@ -215,7 +216,10 @@ def run_stream(args, rank, world, local):
     lg = 24 if args.lgwin == 22 else args.lgwin
     data = datagen.c5_stream(size, 5000 + rank, dev)
     cdict = datagen.c5_dictionary()
-    opts = {'quality': q, 'lgwin': lg, 'mode': 1, 'customDictionary': cdict}
+    # throughput mode (streamChunk, brotli_amd.h): device encodes of >= 32 MiB growing with the
+    # stream; --stream-chunk 0 measures the reference's cadence (every update() encodes its
+    # complete blocks)
+    opts = {'quality': q, 'lgwin': lg, 'mode': 1, 'customDictionary': cdict, 'streamChunk': args.stream_chunk * MIB}
     step = MIB
 
     view = memoryview(data)   # update() gets views of the stream, as Uint8Array.subarray gives
@@ -281,6 +285,7 @@ def run_stream(args, rank, world, local):
                                    'chunks, q%d lgwin%d TEXT, %d B custom dictionary, then brotliDecode of the stream '
                                    'with it (host buffers: PCIe included)' % (size, q, lg, len(cdict)),
                        'name': 'c5', 'bytes_per_stream': size, 'quality': q, 'lgwin': lg,
+                       'stream_chunk_MiB': args.stream_chunk,
                        'custom_dictionary_bytes': len(cdict), 'parallelism': 'replicas%d' % world},
             'encode_MBps': round(mb / te, 3), 'decode_MBps': round(mb / td, 3),
             'compressed_ratio': round(len(stream) / size, 5),

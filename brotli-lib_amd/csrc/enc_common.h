@@ -26,13 +26,12 @@ constexpr int kLongCopy = 200;                // copies longer than this are tak
 constexpr uint32_t kMaxMetablock = 1u << 24;  // encode.ts:206
 constexpr uint32_t kHashBits = 17;            // bucket hash bits (hashBytes4, match.ts:162-172)
 constexpr int kHashBytes = 6;                  // bytes a bucket key covers (see hashn)
-constexpr uint32_t kInvalidKey = 1u << kHashBits;   // (within a stream group) positions without kHashBytes bytes
-constexpr int kGroupKeyBits = 6;
+constexpr uint32_t kInvalidKey = 1u << kHashBits;   // the sort key of positions without kHashBytes bytes
 // Streaming history (BrotliEncoder across update() calls): per encoder, for every hash bucket
 // the stream positions of its kHistWays most recent earlier occurrences, newest first
 // (the reference keeps a hash chain over its ring, hash-chains.ts / encode.ts:354-374).
 constexpr int kHistWays = 16;
-constexpr uint32_t kNoPos = 0xFFFFFFFFu;              // sort key = stream group (<= 64 groups) << 18 | hash or invalid
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;              // (a history slot with no position)
 constexpr int kHdrBytes = 2048;               // metablock header: block-switch codes, context maps (not the trees)
 constexpr int kTreeBytes = 1024;              // one serialised prefix code
 constexpr int kLitCtx = 64;                   // literal contexts (RFC 7932 section 7.1)
@@ -461,8 +460,9 @@ void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs
 void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces);
 void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw);
 void launch_rep(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const CostModel *model, RawCmd *raw, uint32_t *cnts);
-void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
-                      uint32_t *vals);
+size_t sort_ws_bytes(uint32_t total);
+void launch_sort(hipStream_t st, const Job *jobs, const uint32_t *pos_job, int njobs, uint32_t total, int hb, void *ws,
+                 uint32_t *tmp_k, uint32_t *tmp_v, uint32_t *skeys, uint32_t *svals);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h);
 void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes);

@@ -1,5 +1,5 @@
-// Match finding: hash keys, the device radix sort that turns
-// every hash bucket into a flat chain, and the LDS-tiled candidate walk.
+// Match finding: the LDS-tiled candidate walk over each stream's
+// hash buckets (laid out as flat chains by the bucket sort, enc_sort.hip).
 #include <algorithm>
 #include <cstdlib>
 
@@ -8,47 +8,6 @@
 namespace mib {
 namespace enc {
 
-// ---------------------------------------------------------------- 1. keys
-// Every global position (including the padding after each stream) gets the key
-// (stream group << 18 | hash of kHashBytes bytes), the invalid hash 2^17 for padding and a stream's last
-// bytes.  A stream group is 2^gshift consecutive streams (at most 64 groups a call, so keys
-// have at most 24 bits: three radix passes).  The sort is stable and global positions
-// ascend stream by stream, so within a bucket the entries of one stream are contiguous and
-// in position order -- a candidate walk stops where the stream changes -- and the entries a
-// wave of find_matches tiles touches stay within one group's streams (cache locality).
-__global__ void hash_keys_kernel(const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
-                                 uint32_t *vals) {
-  // four consecutive positions per thread (total is a multiple of the 64 KiB segment): one
-  // 16-byte load covers their (<= 6)-byte keys, and keys / values are stored as uint4
-  for (uint32_t g = (blockIdx.x * blockDim.x + threadIdx.x) * 4; g < total; g += gridDim.x * blockDim.x * 4) {
-    const uint32_t j = pos_job[g >> kSegBits];
-    const Job &jb = jobs[j];
-    const uint32_t p = g - jb.pos_base, grp = (j >> gshift) << (kHashBits + 1);
-    uint32_t k4[4];
-    if (!jb.uncompressed && p + 16 <= jb.n) {
-      const uintptr_t a = (uintptr_t)(jb.data + p);
-      const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-      const uint32_t sh = (uint32_t)(a & 3);
-      const uint32_t v0 = w[0], v1 = w[1], v2 = w[2], v3 = w[3];
-      const uint64_t lo = (uint64_t)__builtin_amdgcn_alignbyte(v1, v0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(v2, v1, sh) << 32);
-      const uint64_t hi = __builtin_amdgcn_alignbyte(v3, v2, sh);   // bytes 8..11
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint64_t x = k ? (lo >> (8 * k)) | (hi << (64 - 8 * k)) : lo;
-        const uint64_t v = (x & ((1ull << (8 * hb)) - 1)) << (64 - 8 * hb);   // (= hashn)
-        k4[k] = grp | (uint32_t)((v * 0x1E35A7BD1E35A7BDull) >> (64 - kHashBits));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint32_t q = p + k;
-        k4[k] = grp | ((q + (uint32_t)hb <= jb.n && !jb.uncompressed) ? hashn(jb.data + q, hb) : kInvalidKey);
-      }
-    }
-    *reinterpret_cast<uint4 *>(keys + g) = make_uint4(k4[0], k4[1], k4[2], k4[3]);
-    *reinterpret_cast<uint4 *>(vals + g) = make_uint4(g, g + 1, g + 2, g + 3);
-  }
-}
 // ---------------------------------------------------------------- 2. matches
 // One thread per SORTED entry: a bucket is a run of equal keys with positions ascending, so
 // the candidates of entry r are entries r-1, r-2, ... (most recent first) -- the
@@ -90,11 +49,19 @@ __device__ __forceinline__ void load_prefix32(const uint8_t *p, uint32_t avail, 
 template <int kTile, bool kHist, bool kParts>
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                                                              const uint32_t *sorted_keys, const uint32_t *sorted_vals,
-                                                             uint32_t total, int depth, uint32_t max_dist, uint32_t *matches) {
+                                                             uint32_t total, int depth, uint32_t max_dist, uint32_t *matches,
+                                                             int xcd_order) {
   __shared__ uint32_t skey[kTile + kBack];
   __shared__ uint32_t spos[kTile + kBack];
   __shared__ uint64_t spre[kPreW][kTile + kBack];
-  const uint32_t r0 = blockIdx.x * kTile;
+  // xcd_order (an experiment, off): blocks are dealt round-robin over the 8 XCDs (b and b + 8
+  // share one, MI355X_MICROARCH.md), so block b takes tile (b % 8) * per + b / 8 -- each XCD
+  // sweeps one contiguous eighth of the sorted entries, a few streams at a time, meant to keep
+  // the prefixes its tiles gather in its 4 MiB L2 (measured: no faster)
+  const uint32_t ntiles = (total + kTile - 1) / kTile, per = (ntiles + 7) / 8;
+  const uint32_t tix = xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
+  if (tix >= ntiles) return;
+  const uint32_t r0 = tix * kTile;
   for (int t = threadIdx.x; t < kTile + kBack; t += kTile) {
     int64_t r = (int64_t)r0 - kBack + t;
     uint32_t key = 0xFFFFFFFEu, g = 0;
@@ -379,20 +346,17 @@ void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_j
   hipLaunchKernelGGL(cdict_matches_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, matches);
 }
 
-void launch_hash_keys(hipStream_t st, const Job *jobs, const uint32_t *pos_job, uint32_t total, int gshift, int hb, uint32_t *keys,
-                      uint32_t *vals) {
-  const unsigned grid = (unsigned)std::min<uint64_t>(8192, (total / 4 + 255) / 256);
-  hipLaunchKernelGGL(hash_keys_kernel, dim3(grid), dim3(256), 0, st, jobs, pos_job, total, gshift, hb, keys, vals);
-}
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                          const uint32_t *skeys, const uint32_t *svals, uint32_t total, int depth, uint32_t max_dist,
                          bool hist, bool parts, uint32_t *matches) {
   // tile of sorted entries per block: each tile also stages the kBack entries before it
   // (MIB_FM_TILE: experiment knob, 256 / 512 / 1024)
   static const int tile = getenv("MIB_FM_TILE") ? atoi(getenv("MIB_FM_TILE")) : 256;
-#define MIB_FM(T, H, P)                                                                                                 \
-  hipLaunchKernelGGL((find_matches_kernel<T, H, P>), dim3((total + T - 1) / T), dim3(T), 0, st, jobs, pos_job, seg_ref, \
-                     skeys, svals, total, depth, max_dist, matches)
+  // XCD-aware tile order (MIB_FM_XCD=1): measured no faster on C4 (64.9 vs 65.4 ms), off
+  static const int xcd = getenv("MIB_FM_XCD") ? atoi(getenv("MIB_FM_XCD")) : 0;
+#define MIB_FM(T, H, P)                                                                                                   \
+  hipLaunchKernelGGL((find_matches_kernel<T, H, P>), dim3(8 * (((total + T - 1) / T + 7) / 8)), dim3(T), 0, st, jobs, pos_job, \
+                     seg_ref, skeys, svals, total, depth, max_dist, matches, xcd)
 #define MIB_FM_T(T)                            \
   do {                                         \
     if (hist && parts) MIB_FM(T, true, true);  \

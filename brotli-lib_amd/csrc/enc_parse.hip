@@ -889,7 +889,7 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 // else dp_kernel<1>
 static int dp_ks(int nsegs) {
   static const int v = getenv("MIB_DP_KS") ? atoi(getenv("MIB_DP_KS")) : 0;   // experiments
-  if (v == 1 || v == 2) return v;
+  if (v == 1 || v == 2 || v == 4) return v;   // (4: measured slower on C4, 106.6 -> 119.5 ms: 180 VGPRs, half the waves)
   return nsegs < 2048 ? 1 : 2;
 }
 static int dp_workgroups(int nsegs) {
@@ -905,6 +905,11 @@ static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int ns
       hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
     else
       hipLaunchKernelGGL((dp_kernel<1, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+  } else if (dp_ks(nsegs) == 4) {
+    if (model)
+      hipLaunchKernelGGL((dp_kernel<4, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+    else
+      hipLaunchKernelGGL((dp_kernel<4, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
   } else {
     if (model)
       hipLaunchKernelGGL((dp_kernel<2, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);

@@ -9,9 +9,9 @@
 // symbols -- restructured for the GPU (kernels in enc_match / enc_parse / enc_entropy /
 // enc_emit.hip):
 //
-//   hash_keys + radix sort   every position of every stream gets key (stream group | hash of 6 bytes, 4 for fonts),
-//                            <= 24 bits; a stable device radix sort lays each bucket out as
-//                            flat chains, one per stream, positions ascending
+//   bucket sort              every position of every stream gets a key (the hash of 6 bytes, 4 for
+//                            fonts); each stream's positions are sorted by it, stably, so each
+//                            bucket is a flat chain, positions ascending (enc_sort.hip)
 //   find_matches             thread per sorted entry, LDS tile of the chain: the staircase of
 //                            (distance, length) matches, findAllMatches-style
 //   dp                       wave per 64 KiB segment: shortest path, 64 lanes relax the
@@ -23,7 +23,6 @@
 // slot is known at every segment start, so all entropy-coding work is segment-parallel.
 // The output is one valid RFC 7932 stream per input, decodable by any decoder.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -393,15 +392,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   const int nsegs = (int)segs.size(), nmbs = (int)mbs.size();
   const size_t nm1 = std::max<size_t>(1, mbs.size()), ns1 = std::max<size_t>(1, segs.size());
 
-  const uint64_t last_job = k ? k - 1 : 0;
-  static const int gbits = (int)env_u32("MIB_GROUP_BITS", kGroupKeyBits, 0, 12);
-  int gshift = 0;   // stream groups of the sort key: at most 2^gbits of them
-  while ((last_job >> gshift) >= (1u << gbits)) gshift++;
-  int key_bits = kHashBits + 1;
-  while (key_bits < (int)kHashBits + 1 + gbits && ((last_job >> gshift) >> (key_bits - kHashBits - 1)) != 0) key_bits++;
-  size_t sort_tmp = 0;
-  CK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                        (uint32_t *)nullptr, (int)total, 0, key_bits, st));
+  const size_t sort_tmp = sort_ws_bytes(total);
   size_t need = 64 * 256;
   need += 4 * (size_t)total * 4 + sort_tmp;
   need += (size_t)total * kMatchRec * 4;
@@ -486,11 +477,8 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     CK(hipMemsetAsync(hd, 0, nm1 * kMaxBT * kDistCtx * 128 * 4, st));
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
     const int depth = (int)env_u32("MIB_DEPTH", (uint32_t)depth_for_quality(prm.quality), 1, 64);   // override: experiments
-    tm.start("hash_keys");
-    launch_hash_keys(st, d_jobs, d_seg_job, total, gshift, hash_bytes(prm), keys, vals);
-    tm.stop();
-    tm.start("radix_sort");
-    CK(hipcub::DeviceRadixSort::SortPairs(sort_ws, sort_tmp, keys, skeys, vals, svals, (int)total, 0, key_bits, st));
+    tm.start("bucket_sort");
+    launch_sort(st, d_jobs, d_seg_job, (int)k, total, hash_bytes(prm), sort_ws, keys, vals, skeys, svals);
     tm.stop();
     tm.start("find_matches");
     const DictDev *dd = any_dict ? dict_device(mib_ctx_device_of(ctx)) : nullptr;
@@ -709,10 +697,11 @@ struct mib_encoder {
   uint32_t prev_bytes = 0;        // the last two bytes handed to the engine (literal contexts)
   uint64_t window = 1 << 22;      // 2^lgwin: the history kept for the next chunk
   uint64_t block = 1 << 16;       // the reference's 2^lgblock (enc-constants.ts:129-147)
-  uint64_t chunk = 32ull << 20;   // input per device encode: whole blocks, at least this much
-                                  // (512 parse segments: 8 MiB left 7/8 of the chip idle in the DP);
-                                  // it grows with the stream (kMaxChunk)
-  bool chunk_fixed = false;       // MIB_STREAM_CHUNK set: no growth
+  uint64_t chunk = 0;             // input per device encode: whole blocks, at least this much --
+                                  // 2^lgblock (the reference's cadence, encode.ts:366-374), or in
+                                  // throughput mode (mib_enc_opts.stream_chunk) that many bytes,
+                                  // growing with the stream (kMaxChunk)
+  bool chunk_fixed = true;        // no growth (the reference's cadence; MIB_STREAM_CHUNK)
   // device state (the default context's device): the window of history, then the pending
   // input (update() copies each piece straight here), ping-ponged so the next chunk's history
   // is one device copy; the bucket table of earlier positions
@@ -990,9 +979,23 @@ mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
   }
   e->block = 1ull << lgblock;
   e->window = 1ull << prm.lgwin;
-  e->chunk_fixed = getenv("MIB_STREAM_CHUNK") != nullptr;
-  e->chunk = (uint64_t)env_u32("MIB_STREAM_CHUNK", (uint32_t)(e->chunk >> 20), 1, 4096) << 20;   // MiB (tests, experiments)
-  e->chunk = std::max<uint64_t>(e->block, e->chunk);
+  // Output cadence.  Default: the reference's -- each update() encodes every complete block
+  // it has, so a streaming caller gets bytes as soon as a block is complete.  stream_chunk:
+  // throughput mode -- a device encode waits for that much input, and grows with what the
+  // stream has already encoded (a 32 MiB encode is 512 parse segments, a quarter of the DP's
+  // waves: small encodes leave the chip idle).  MIB_STREAM_CHUNK (MiB, tests and experiments):
+  // a fixed size.
+  if (getenv("MIB_STREAM_CHUNK")) {
+    e->chunk = (uint64_t)env_u32("MIB_STREAM_CHUNK", 32, 1, 4096) << 20;
+    e->chunk_fixed = true;
+  } else if (o && o->stream_chunk) {
+    e->chunk = std::min<uint64_t>(o->stream_chunk, kMaxChunk);
+    e->chunk_fixed = false;
+  } else {
+    e->chunk = e->block;
+    e->chunk_fixed = true;
+  }
+  e->chunk = std::max<uint64_t>(e->block, e->chunk / e->block * e->block);
   return e;
 }
 

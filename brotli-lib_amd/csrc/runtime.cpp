@@ -371,6 +371,7 @@ void mib_enc_opts_default(mib_enc_opts *o) {
   o->size_hint = 0;
   o->dict = nullptr;
   o->dict_len = 0;
+  o->stream_chunk = 0;
 }
 
 int mib_init(int device) {

@@ -159,11 +159,11 @@ static void encoder_finalize(napi_env env, void *data, void *hint) {
   mib_encoder_free((mib_encoder *)data);
 }
 
-/* encoderNew(quality, lgwin, mode, dictionary|null) -> external handle (the encoder copies
- * the dictionary) */
+/* encoderNew(quality, lgwin, mode, dictionary|null, streamChunk) -> external handle (the
+ * encoder copies the dictionary) */
 static napi_value js_encoder_new(napi_env env, napi_callback_info info) {
-  size_t argc = 4;
-  napi_value argv[4], out;
+  size_t argc = 5;
+  napi_value argv[5], out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   mib_enc_opts o;
   mib_enc_opts_default(&o);
@@ -173,6 +173,8 @@ static napi_value js_encoder_new(napi_env env, napi_callback_info info) {
   size_t dn = 0;
   if (argc > 3 && get_bytes(env, argv[3], &o.dict, &dn) == 0) o.dict_len = dn;
   else o.dict = NULL;
+  const int64_t sc = argc > 4 ? get_i64(env, argv[4], 0) : 0;
+  o.stream_chunk = sc > 0 ? (uint64_t)sc : 0;
   mib_encoder *e = mib_encoder_new(&o);
   if (!e) return throw_code(env, MIB_E_OUT_OF_MEMORY);
   CHECK(env, napi_create_external(env, e, encoder_finalize, NULL, &out));
@@ -211,11 +213,12 @@ static napi_value js_encoder_finish(napi_env env, napi_callback_info info) {
   return take(env, &b);
 }
 
-/* encodeBatch([bytes...], quality, lgwin, mode, gpus) -> [Buffer...]: one GPU launch sequence
- * (gpus >= 0: sharded over that many GPUs, 0 = all; -1 / absent: the default device) */
+/* encodeBatch([bytes...], quality, lgwin, mode, gpus, dictionary|null) -> [Buffer...]: one GPU
+ * launch sequence (gpus >= 0: sharded over that many GPUs, 0 = all; -1 / absent: the default
+ * device) */
 static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
-  size_t argc = 5;
-  napi_value argv[5], out;
+  size_t argc = 6;
+  napi_value argv[6], out;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   uint32_t k = 0;
   bool is_arr = false;
@@ -229,6 +232,9 @@ static napi_value js_encode_batch(napi_env env, napi_callback_info info) {
   o.quality = get_int(env, argc > 1 ? argv[1] : NULL, o.quality);
   o.lgwin = get_int(env, argc > 2 ? argv[2] : NULL, o.lgwin);
   o.mode = get_int(env, argc > 3 ? argv[3] : NULL, o.mode);
+  size_t dn = 0;
+  if (argc > 5 && get_bytes(env, argv[5], &o.dict, &dn) == 0) o.dict_len = dn;
+  else o.dict = NULL;
   mib_span *in = (mib_span *)calloc(k ? k : 1, sizeof(mib_span));
   mib_buf *res = (mib_buf *)calloc(k ? k : 1, sizeof(mib_buf));
   int *st = (int *)calloc(k ? k : 1, sizeof(int));
@@ -271,6 +277,7 @@ typedef struct {
   int gpus;         /* >= 0: sharded over that many GPUs (0 = all), else the default device */
   mib_enc_opts o;
   uint8_t *blob;    /* the inputs, back to back (owned) */
+  uint8_t *dict;    /* encode: the customDictionary (owned copy), or NULL */
   mib_span *in;
   mib_buf *res;
   int *st;
@@ -278,7 +285,7 @@ typedef struct {
 } AsyncBatch;
 
 static void async_free(AsyncBatch *a) {
-  free(a->blob), free(a->in), free(a->res), free(a->st), free(a);
+  free(a->blob), free(a->dict), free(a->in), free(a->res), free(a->st), free(a);
 }
 
 static void async_execute(napi_env env, void *data) {
@@ -321,10 +328,11 @@ static void async_complete(napi_env env, napi_status status, void *data) {
   async_free(a);
 }
 
-/* encodeBatchAsync(inputs, quality, lgwin, mode, gpus) / decodeBatchAsync(inputs, gpus) -> Promise */
+/* encodeBatchAsync(inputs, quality, lgwin, mode, gpus, dictionary|null) /
+ * decodeBatchAsync(inputs, gpus) -> Promise */
 static napi_value start_async(napi_env env, napi_callback_info info, int decode) {
-  size_t argc = 5;
-  napi_value argv[5], promise, name;
+  size_t argc = 6;
+  napi_value argv[6], promise, name;
   CHECK(env, napi_get_cb_info(env, info, &argc, argv, NULL, NULL));
   bool is_arr = false;
   uint32_t k = 0;
@@ -342,6 +350,18 @@ static napi_value start_async(napi_env env, napi_callback_info info, int decode)
     a->o.quality = get_int(env, argc > 1 ? argv[1] : NULL, a->o.quality);
     a->o.lgwin = get_int(env, argc > 2 ? argv[2] : NULL, a->o.lgwin);
     a->o.mode = get_int(env, argc > 3 ? argv[3] : NULL, a->o.mode);
+    const uint8_t *d;
+    size_t dn;
+    if (argc > 5 && get_bytes(env, argv[5], &d, &dn) == 0 && dn) {   /* (copied: JS may detach it) */
+      a->dict = (uint8_t *)malloc(dn);
+      if (!a->dict) {
+        free(a);
+        return throw_code(env, MIB_E_OUT_OF_MEMORY);
+      }
+      memcpy(a->dict, d, dn);
+      a->o.dict = a->dict;
+      a->o.dict_len = dn;
+    }
   }
   a->in = (mib_span *)calloc(k ? k : 1, sizeof(mib_span));
   a->res = (mib_buf *)calloc(k ? k : 1, sizeof(mib_buf));

@@ -44,7 +44,9 @@ function brotliEncode(input, options) {
 class BrotliEncoder {
   constructor(options) {
     const [q, lg, m] = clampOptions(options)
-    this._h = native.encoderNew(q, lg, m, dictOf(options))
+    // options.streamChunk (extension): throughput mode, see brotli_amd.h mib_enc_opts.stream_chunk
+    const sc = options && options.streamChunk ? Math.max(0, options.streamChunk) : 0
+    this._h = native.encoderNew(q, lg, m, dictOf(options), sc)
   }
   update(input) {
     return toU8(native.encoderUpdate(this._h, input))
@@ -86,14 +88,14 @@ function gpusOf(options) {
 // batch entry point of this engine: independent buffers in one GPU launch sequence
 function brotliEncodeBatch(inputs, options) {
   const [q, lg, m] = clampOptions(options)
-  return native.encodeBatch(inputs, q, lg, m, gpusOf(options)).map(toU8)
+  return native.encodeBatch(inputs, q, lg, m, gpusOf(options), dictOf(options)).map(toU8)
 }
 
 // the same, off the JS thread: the GPU work runs on a worker (napi_async_work), a Promise
 // resolves to the outputs (decode: a stream that fails gives its Error in its slot)
 function brotliEncodeBatchAsync(inputs, options) {
   const [q, lg, m] = clampOptions(options)
-  return native.encodeBatchAsync(inputs, q, lg, m, gpusOf(options)).then((outs) => outs.map(toU8))
+  return native.encodeBatchAsync(inputs, q, lg, m, gpusOf(options), dictOf(options)).then((outs) => outs.map(toU8))
 }
 function brotliDecodeBatchAsync(inputs, options) {
   return native.decodeBatchAsync(inputs, gpusOf(options)).then((outs) => outs.map((o) => (o instanceof Error ? o : toU8(o))))

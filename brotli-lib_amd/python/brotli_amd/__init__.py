@@ -41,7 +41,8 @@ class BrotliError(Exception):
 
 class _Opts(ctypes.Structure):
     _fields_ = [('quality', ctypes.c_int), ('lgwin', ctypes.c_int), ('mode', ctypes.c_int),
-                ('size_hint', ctypes.c_uint64), ('dict', ctypes.c_char_p), ('dict_len', ctypes.c_uint64)]
+                ('size_hint', ctypes.c_uint64), ('dict', ctypes.c_char_p), ('dict_len', ctypes.c_uint64),
+                ('stream_chunk', ctypes.c_uint64)]
 
 
 class _Buf(ctypes.Structure):
@@ -175,7 +176,7 @@ def _opts(options):
     the stream then decodes with, and only with, the same dictionary).  The dictionary's
     bytes object is kept on the returned structure for the duration of the call."""
     options = options or {}
-    o = _Opts(11, 22, EncoderMode.GENERIC, 0, None, 0)
+    o = _Opts(11, 22, EncoderMode.GENERIC, 0, None, 0, 0)
     if options.get('quality') is not None:
         o.quality = max(0, min(11, int(options['quality'])))
     if options.get('lgwin') is not None:
@@ -184,6 +185,8 @@ def _opts(options):
         o.mode = int(options['mode'])
     if options.get('sizeHint') is not None:
         o.size_hint = int(options['sizeHint'])
+    if options.get('streamChunk') is not None:   # BrotliEncoder throughput mode (brotli_amd.h)
+        o.stream_chunk = max(0, int(options['streamChunk']))
     if options.get('customDictionary') is not None:
         d = _bytes(options['customDictionary'])
         o._keep = d

@@ -56,6 +56,12 @@ typedef struct {
    * Host memory, borrowed for the call (BrotliEncoder keeps its own copy). NULL: none. */
   const uint8_t *dict;
   uint64_t dict_len;
+  /* BrotliEncoder only (extension): 0 = the reference's cadence (encode.ts:366-374: every
+   * update() encodes each complete 2^lgblock block it has and returns its bytes); N > 0 =
+   * throughput mode: input gathers until at least N bytes (whole blocks) are pending, and the
+   * device encode then grows with the stream (up to 256 MiB) -- update() may return nothing
+   * for a while and finish() returns the rest. */
+  uint64_t stream_chunk;
 } mib_enc_opts;
 
 typedef struct { uint8_t *data; size_t size; } mib_buf;          /* library-allocated result */
@@ -85,8 +91,9 @@ int64_t mib_decoded_size(const uint8_t *in, size_t n);
 
 /* BrotliEncoder (encode.ts:290-490): update() returns the newly completed bytes.  The
  * encoder keeps its 2^lgwin window of history in HBM, so matches reach across update()
- * calls; input is encoded in whole 2^lgblock blocks, several MiB per device pass, so
- * update() may return nothing until enough input has arrived (finish() returns the rest). */
+ * calls; input is encoded in whole 2^lgblock blocks: by default each update() encodes the
+ * complete blocks it has (the reference's cadence), with mib_enc_opts.stream_chunk several
+ * MiB per device pass (throughput mode). */
 typedef struct mib_encoder mib_encoder;
 mib_encoder *mib_encoder_new(const mib_enc_opts *o);
 int mib_encoder_update(mib_encoder *e, const uint8_t *in, size_t n, mib_buf *out);
