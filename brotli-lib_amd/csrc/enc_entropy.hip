@@ -1855,10 +1855,11 @@ void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
 // that every symbol lookup is an HBM load.  With up to 64 codes some C3 fonts overflowed it,
 // and the batch kernel waits for its slowest stream: C3 decode 76 -> 46 ms at 32 codes, and
 // the stream is smaller too (0.4585 -> 0.4582: fewer codes to send); 24: 0.45816 / 45.6 ms;
-// C4 never needs more than 24.  MIB_LIT_TREES overrides (4..64).
+// C4 never needs more than 24.  MIB_LIT_TREES overrides (1..64; 1: one code per block type,
+// context-free literals).
 constexpr int kLitTreeCap = 24;
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
-  static const int cap = getenv("MIB_LIT_TREES") ? std::min(kMaxLitTrees, std::max(4, atoi(getenv("MIB_LIT_TREES")))) : kLitTreeCap;
+  static const int cap = getenv("MIB_LIT_TREES") ? std::min(kMaxLitTrees, std::max(1, atoi(getenv("MIB_LIT_TREES")))) : kLitTreeCap;
   hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, cap);
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,

@@ -62,6 +62,11 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
   const uint32_t tix = xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
   if (tix >= ntiles) return;
   const uint32_t r0 = tix * kTile;
+  // Each stream's positions are sorted within the stream's own range of global positions
+  // (enc_sort.hip), so the tile's entries -- 256 within one 64 KiB range -- are all of one
+  // stream: one SegRef for the block instead of a dependent lookup per entry.  Lookback
+  // entries of the stream before are never candidates (the walk stops at them): no prefix.
+  const SegRef sr = seg_ref[r0 >> kSegBits];
   for (int t = threadIdx.x; t < kTile + kBack; t += kTile) {
     int64_t r = (int64_t)r0 - kBack + t;
     uint32_t key = 0xFFFFFFFEu, g = 0;
@@ -69,10 +74,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     if (r >= 0 && r < (int64_t)total) {
       key = sorted_keys[r];
       g = sorted_vals[r];
-      if ((key & kInvalidKey) == 0) {
-        const SegRef sr = seg_ref[g >> kSegBits];
-        load_prefix32(sr.base + g, sr.end - g, pre);
-      }
+      if ((key & kInvalidKey) == 0 && g >= sr.pos_base) load_prefix32(sr.base + g, sr.end - g, pre);
     }
     skey[t] = key;
     spos[t] = g;
@@ -86,12 +88,11 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
   const uint32_t key = skey[me], g = spos[me];
   int cnt = 0;
   if ((key & kInvalidKey) == 0) {
-    const SegRef sr = seg_ref[g >> kSegBits];
     const uint32_t p = g - sr.pos_base;
     // (pos_base is a multiple of the segment: the segment's end in global positions)
     const uint32_t limit = min(((g >> kSegBits) + 1) << kSegBits, sr.end) - g;   // copies never cross a parse segment
     const uint8_t *cur = sr.base + g;
-    const Job &jb = jobs[(kHist || kParts) ? pos_job[g >> kSegBits] : 0];   // (the streaming / part-index fields)
+    const Job &jb = jobs[(kHist || kParts) ? pos_job[r0 >> kSegBits] : 0];   // (the streaming / part-index fields)
     const bool parts = kParts && jb.parts;
     const uint32_t pA = (kHist || kParts) ? jb.abs_base + p : 0u, pbits = kParts ? jb.part_bits : 16u,
                    plag = kParts ? jb.part_lag : 0u;

@@ -12,18 +12,42 @@
 //   tile_scan  block per stream, thread per digit: each (tile, digit)'s first output slot
 //              (the digit's count in the stream's earlier tiles + the stream's earlier digits)
 //   scatter    block per tile, wave per quarter: a stable counting sort of the tile in LDS
-//              (each wave ranks its 2048 items round by round, 64 at a time, equal digits
-//              found by nine ballots), then coalesced runs to the output
+//              (each wave ranks its 2048 items round by round, 64 at a time, by returning LDS
+//              atomics, which serve the lanes of a wave in lane order), then coalesced runs
+//              to the output
 // Traffic per position: pass 1 reads the bytes twice and writes key + position (8 B), pass 2
 // reads the keys (4 B), then key + position, and writes 8 B: ~30 B.  (It replaced a
 // library radix sort of (stream group | hash) keys: three 8-bit passes over key + value
 // arrays written by a separate key kernel, 24 + 3 ms on C4.)
+
 #include <algorithm>
+#include <vector>
 
 #include "enc_common.h"
 
 namespace mib {
 namespace enc {
+
+// (the hardware property the ranking relies on, checked by the GPU tests)
+__global__ void lds_atomic_order_kernel(const uint32_t *addr, int trials, uint32_t *bad) {
+  __shared__ uint32_t cnt[4][64];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t nbad = 0;
+  for (int t = blockIdx.x * 4 + (int)w; t < trials; t += gridDim.x * 4) {
+    cnt[w][lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t a = addr[t * 64 + lane] & 63;
+    const uint32_t r = atomicAdd(&cnt[w][a], 1u);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t below = 0;
+    for (int l = 0; l < 64; l++) {
+      const uint32_t al = (uint32_t)__shfl((int)a, l);   // (every lane: a shuffle reads active lanes only)
+      below += ((uint32_t)l < lane && al == a) ? 1u : 0u;
+    }
+    nbad += r != below ? 1u : 0u;
+  }
+  atomicAdd(bad, nbad);
+}
 
 constexpr int kTileBits = 13;
 constexpr uint32_t kTile = 1u << kTileBits;   // positions per tile (a stream's span is a multiple)
@@ -154,9 +178,8 @@ __global__ __launch_bounds__(kDigits) void tile_scan_kernel(const Job *jobs, int
 // Block per tile.  Wave w owns items [2048 w, 2048 (w + 1)) of the tile in position order;
 // stable order = wave order, then round order, then lane order.  Sweep 1: each wave's digit
 // counts; their prefix over the waves and the tile's digit offsets give each wave its first
-// slot per digit.  Sweep 2, round by round: a lane's rank among the earlier lanes of its round
-// with the same digit (nine ballots), the digit's next slot (cur), and the group's lowest lane
-// advances cur by the group's size.  Items go to LDS in sorted order, then out in runs.
+// slot per digit.  Sweep 2, round by round: each item takes its digit's next slot (cur) by a
+// returning atomic.  Items go to LDS in sorted order, then out in runs.
 template <bool kFirst>
 __global__ __launch_bounds__(kSortT) void tile_scatter_kernel(const Job *jobs, const uint32_t *pos_job, int hb,
                                                               const uint32_t *in_k, const uint32_t *in_v, const uint16_t *hist,
@@ -198,8 +221,10 @@ __global__ __launch_bounds__(kSortT) void tile_scatter_kernel(const Job *jobs, c
       key[r] = in_k[base + i];
       val[r] = in_v[base + i];
     }
-    atomicAdd(&cur[w][digit_of<kFirst>(key[r])], 1u);
   }
+  // (a loop of its own: with the count in the load loop every load was waited for at once)
+#pragma unroll
+  for (int r = 0; r < kRounds; r++) atomicAdd(&cur[w][digit_of<kFirst>(key[r])], 1u);
   __syncthreads();
   // lbase: exclusive scan of the tile's digit counts; cur[w][d]: lbase[d] + the counts of the
   // waves before w
@@ -235,25 +260,17 @@ __global__ __launch_bounds__(kSortT) void tile_scatter_kernel(const Job *jobs, c
     }
   }
   __syncthreads();
-  const uint64_t lt = (1ull << lane) - 1;
+  // Ranking: one returning LDS atomic per item.  The lanes of one ds_add_rtn_u32 that hit the
+  // same address get their values in lane order (probed on the MI355X over 65,536 random
+  // collision patterns: scripts/probe/lds_atomic_order.hip, and mib_selftest_lds_atomic_order
+  // in the GPU tests), and a wave's LDS operations complete in issue order: so round r's items
+  // take their digit's slots in (round, lane) order -- the sort is stable.  (Nine ballots per
+  // round to the same effect cost ~90 VALU per round: the whole pass was VALU-bound.)
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
-    const uint32_t d = digit_of<kFirst>(key[r]);
-    uint64_t eq = ~0ull;
-#pragma unroll
-    for (int b = 0; b < kDigitBits; b++) {
-      const uint64_t m = __ballot((d >> b) & 1);
-      eq &= ((d >> b) & 1) ? m : ~m;
-    }
-    const uint32_t below = (uint32_t)__popcll(eq & lt);
-    const uint32_t slot = cur[w][d] + below;
+    const uint32_t slot = atomicAdd(&cur[w][digit_of<kFirst>(key[r])], 1u);
     sk[slot] = key[r];
     sv[slot] = val[r];
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (below == 0) cur[w][d] = slot + (uint32_t)__popcll(eq);   // the group's lowest lane
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
   }
   __syncthreads();
   // out: item i (sorted) of digit d goes to off[tile][d] + (i - lbase[d]); consecutive threads,
@@ -265,6 +282,42 @@ __global__ __launch_bounds__(kSortT) void tile_scatter_kernel(const Job *jobs, c
     out_v[dst] = sv[i];
   }
 }
+
+}  // namespace enc
+}  // namespace mib
+
+// Self-test: lanes of one wave colliding on LDS addresses through returning atomics (random
+// patterns of 1..64 addresses, `trials` of them): how many lanes got a value other than their
+// rank in lane order (0 on the MI355X).  Returns that count, or < 0 on a HIP error.
+extern "C" int64_t mib_selftest_lds_atomic_order(int trials) {
+  if (trials <= 0) return 0;
+  std::vector<uint32_t> h((size_t)trials * 64);
+  uint32_t x = 12345;
+  for (int t = 0; t < trials; t++) {
+    const uint32_t range = 1 + (uint32_t)(t % 64);
+    for (int l = 0; l < 64; l++) {
+      x ^= x << 13; x ^= x >> 17; x ^= x << 5;
+      h[(size_t)t * 64 + l] = x % range;
+    }
+  }
+  uint32_t *d = nullptr, *bad = nullptr, nb = 0;
+  if (hipMalloc(&d, h.size() * 4) != hipSuccess) return -1;
+  if (hipMalloc(&bad, 4) != hipSuccess) {
+    hipFree(d);
+    return -1;
+  }
+  int64_t rc = -1;
+  if (hipMemcpy(d, h.data(), h.size() * 4, hipMemcpyHostToDevice) == hipSuccess && hipMemset(bad, 0, 4) == hipSuccess) {
+    hipLaunchKernelGGL(mib::enc::lds_atomic_order_kernel, dim3(256), dim3(256), 0, 0, d, trials, bad);
+    if (hipMemcpy(&nb, bad, 4, hipMemcpyDeviceToHost) == hipSuccess) rc = nb;
+  }
+  hipFree(d);
+  hipFree(bad);
+  return rc;
+}
+
+namespace mib {
+namespace enc {
 
 size_t sort_ws_bytes(uint32_t total) {
   const size_t ntiles = total >> kTileBits;

@@ -113,6 +113,11 @@ int mib_encode_batch_n(const mib_span *in, size_t k, const mib_enc_opts *o, int 
 int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, int *status);
 /* Visible HIP devices (0 without a GPU). */
 int mib_device_count(void);
+/* Diagnostics: the hardware property the match finder's bucket sort relies on for its
+ * stability (the lanes of one wave's returning LDS atomic on one address are served in lane
+ * order): lanes that broke it over `trials` random collision patterns (0 expected), < 0 on a
+ * HIP error. */
+int64_t mib_selftest_lds_atomic_order(int trials);
 
 void mib_buf_free(mib_buf *b);
 /* The allocator behind every mib_buf the library returns (default malloc / free), in the
