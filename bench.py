@@ -76,6 +76,8 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true')
     ap.add_argument('--stream-chunk', type=int, default=32, help='c5: BrotliEncoder streamChunk in MiB (0: the reference\'s cadence)')
+    ap.add_argument('--gpus-in-lib', type=int, default=0,
+                    help='host-API leg: the batch through mib_*_batch_n with N shards against the one-context batch')
     return ap.parse_args()
 
 
@@ -449,6 +451,67 @@ def run_ref(args):
           flush=True)
 
 
+def run_in_lib(args):
+    """in-library sharding leg: the workload's batch as host buffers through
+    the C ABI's sharded batch calls (mib_encode_batch_n / mib_decode_batch_n: a context per
+    shard, pinned one-copy staging, shard s on device s % ndev) against the one-context batch
+    (mib_encode_batch / mib_decode_batch) on the same buffers.  On one GPU all N shards share
+    device 0, so this times the sharding machinery's overhead, not multi-GPU scaling."""
+    import brotli_amd
+    import torch
+    wl = args.workload
+    k0, size0, mode, _, gen = WORKLOADS[wl]
+    k = args.streams if args.streams > 0 else k0
+    size = args.size if args.size > 0 else size0
+    dev = torch.device('cuda', 0)
+    data = make_inputs(wl, k, size, 0, dev).cpu().numpy().tobytes()
+    bufs = [data[i * size:(i + 1) * size] for i in range(k)]
+    del data
+    opts = {'quality': args.quality, 'lgwin': args.lgwin, 'mode': mode}
+    n = args.gpus_in_lib
+
+    def leg(gpus):
+        comp = brotli_amd.encode_batch(bufs, opts, gpus=gpus)
+        out = brotli_amd.decode_batch(comp, gpus=gpus)
+        return comp, out
+
+    ref_comp = None
+    for g in (None, n):
+        for _ in range(max(1, args.warmup)):
+            comp, out = leg(g)
+            if out != bufs:
+                raise SystemExit('in-library leg: round trip FAILED (gpus=%s)' % g)
+            if ref_comp is None:
+                ref_comp = comp
+            elif comp != ref_comp:
+                raise SystemExit('in-library leg: sharded streams differ from the one-context batch')
+    res = {}
+    for g in (None, n):
+        te = td = 0.0
+        for _ in range(args.steps):
+            t0 = time.perf_counter()
+            comp = brotli_amd.encode_batch(bufs, opts, gpus=g)
+            t1 = time.perf_counter()
+            brotli_amd.decode_batch(comp, gpus=g)
+            t2 = time.perf_counter()
+            te += t1 - t0
+            td += t2 - t1
+        res['one_context' if g is None else 'shards'] = {'encode_ms': round(te * 1e3 / args.steps, 3),
+                                                         'decode_ms': round(td * 1e3 / args.steps, 3)}
+    one = res['one_context']['encode_ms'] + res['one_context']['decode_ms']
+    sh = res['shards']['encode_ms'] + res['shards']['decode_ms']
+    total = k * size
+    print(json.dumps({
+        'metric': 'encode+decode MB/s at q11 lgwin=22, host buffers through the sharded C-ABI batch calls',
+        'value': round(total / 1e6 / (sh * 1e-3), 3), 'unit': 'MB/s', 'n_gpus': 1, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(sh, 3), 'higher_is_better': True, 'scaling': 'weak',
+        'vs_baseline': None, 'dtype': 'u8', 'data': 'synthetic',
+        'config': {'workload': '%s batch (%d x %d B) as host buffers: mib_encode_batch_n + mib_decode_batch_n with %d '
+                               'shards on device 0 vs mib_encode_batch + mib_decode_batch (PCIe included)'
+                               % (wl, k, size, n), 'name': 'in_lib', 'shards': n, 'parallelism': 'shards%d_on_1gpu' % n},
+        'legs': res, 'shard_overhead': round(sh / one - 1.0, 4), 'roofline': None, 'cpu_baseline': None}), flush=True)
+
+
 def datagen_device(total, seed, dev):
     from brotli_amd import datagen
     return datagen.enwik_device(total, seed, dev)
@@ -461,6 +524,8 @@ def main():
         return run_ref(args)
     if wl == 'latency':
         return run_latency(args)
+    if args.gpus_in_lib > 0:
+        return run_in_lib(args)
     if wl == 'c5':
         return run_stream(args, int(os.environ.get('RANK', '0')), int(os.environ.get('WORLD_SIZE', '1')),
                           int(os.environ.get('LOCAL_RANK', '0')))

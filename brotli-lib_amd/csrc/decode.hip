@@ -152,6 +152,19 @@ __shared__ Dec g_dec;   // the decoder state: LDS, so that it is wave-uniform an
 // scripts/probe/glds_probe.hip), so a slot is 64 dwords; kCopyQ slots, used round robin.
 constexpr int kCopyQ = 4;
 __shared__ uint32_t g_cp[kCopyQ][64];
+__device__ __forceinline__ uint32_t lds_addr(const __attribute__((address_space(3))) void *p) {
+  return (uint32_t)(uintptr_t)p;
+}
+__device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b) {   // a * 2 + b, one VALU op
+  uint32_t r;
+  asm("v_lshl_add_u32 %0, %1, 1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+// fast_loop's context-modelled literals: the chain in VGPRs (1) or through SGPRs (0, A/B builds)
+#ifndef MIB_VLIT
+#define MIB_VLIT 1
+#endif
+constexpr bool kVlit = MIB_VLIT;
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
@@ -1878,7 +1891,53 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       // literals are gathered one per lane (lane pos & 63) and stored a
       // 64-byte line at a time; the inner loops run to the next line end, so the line check
       // is not paid per literal
-      if (kTrivial) {
+      if (kTrivial && kVlit) {
+        // one code: entry (LDS) -> its length -> the next entry, the chain in VGPRs (as below)
+        ensure();
+        uint32_t vlo = (uint32_t)W, vhi = (uint32_t)(W >> 32), vn = N, vnv = Nv;
+        int vP = P, vPw = Pw, vF = F;
+        int vc1 = c1, vc2 = c2b;
+        while (pos < end) {
+          const int seg_end = U(min(end, (pos | 63) + 1));
+          while (pos < seg_end) {
+            const uint32_t bits = __builtin_amdgcn_alignbit(vhi, vlo, (uint32_t)(vP - vPw));
+            int off = lit_root + (int)(bits & 0xFF);
+            int e = t16[off];
+            int sym = e & 0xFFF, len = e >> 12;
+            if (__builtin_expect(U(e) >= 0x9000, 0)) {
+              off += sym + (int)((bits & ((1u << len) - 1u)) >> 8);
+              e = t16[off];
+              sym = e & 0xFFF;
+              len = 8 + (e >> 12);
+            }
+            vF = vP;
+            vP += len;
+            ob = lane == (pos & 63) ? (uint32_t)sym : ob;
+            vc2 = vc1;
+            vc1 = sym;
+            const bool adv = vP - vPw >= 32;
+            vlo = adv ? vhi : vlo;
+            vhi = adv ? vn : vhi;
+            vn = adv ? vnv : vn;
+            vPw = adv ? vPw + 32 : vPw;
+            vnv = win32[(vPw >> 5) + 3];
+            pos++;
+          }
+          if ((pos & 63) == 0) {
+            const int p = (fl0 & ~63) + lane;
+            if (p >= fl0) ring[p] = (uint8_t)ob;
+            fl0 = pos;
+          }
+        }
+        P = U(vP);
+        F = U(vF);
+        Pw = U(vPw);
+        W = (uint64_t)(uint32_t)U((int)vlo) | ((uint64_t)(uint32_t)U((int)vhi) << 32);
+        N = (uint32_t)U((int)vn);
+        Nv = vnv;
+        c1 = U(vc1);
+        c2b = U(vc2);
+      } else if (kTrivial) {
         while (pos < end) {
           const int seg_end = U(min(end, (pos | 63) + 1));
           while (pos < seg_end) {
@@ -1895,6 +1954,78 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
             fl0 = pos;
           }
         }
+      } else if (kVlit) {
+        // The chain in VGPRs (every lane holds the same values): table entry (LDS) -> symbol ->
+        // the next literal's root, ctx_root[lut1[p2] << 8 | p1] (LDS) -> the next entry.  Two
+        // LDS round trips and a few VALU ops per literal; the bits at P come from the 64-bit
+        // window W while the root read is in flight.  (The scalar form -- readfirstlane of the
+        // entry, the root from a gathered row by v_readlane -- took ~450 cycles a literal: an LDS
+        // read crossing to SGPRs costs ~120 cycles and a dependent v_readlane ~80, against ~70
+        // for an LDS read feeding VALU ops, scripts/probe/chain_probe.hip on the MI355X.)
+        ensure();   // P - Pw < 32
+        LU8 *lut1b = (LU8 *)g_lds.ctx_lut + 256;
+        LU16 *croot = (LU16 *)g_lds.ctx_root;
+        uint32_t vlo = (uint32_t)W, vhi = (uint32_t)(W >> 32), vn = N, vnv = Nv;
+        int vP = P, vPw = Pw, vF = F;
+        int vc1 = c1, vc2 = c2b;
+        int vroot = croot[(lut1b[c2b] << 8) | c1];
+        uint32_t vcls = lut1b[c1];   // lut1[p2] of the next literal
+        while (pos < end) {
+          const int seg_end = U(min(end, (pos | 63) + 1));
+          while (pos < seg_end) {
+            const uint32_t bits = __builtin_amdgcn_alignbit(vhi, vlo, (uint32_t)(vP - vPw));   // 32 bits at P
+            // (LDS byte addresses as index * 2 + a base ready early: one v_lshl_add on the chain)
+            const uint32_t tb = lds_addr(t16) + ((bits & 0xFF) << 1);
+            const uint32_t ea = lshl1_add((uint32_t)vroot, tb);
+            int e = *(LU16 *)(uintptr_t)ea;
+            int sym = e & 0xFFF, len = e >> 12;
+            const uint32_t cb = lds_addr(croot) + (vcls << 9);
+            // the next root and context class, issued before the second-level test resolves
+            int nroot = *(LU16 *)(uintptr_t)lshl1_add((uint32_t)sym, cb);
+            uint32_t ncls = lut1b[sym];
+            if (__builtin_expect(U(e) >= 0x9000, 0)) {   // a second-level table (uniform branch)
+              // (the first reads are used on this path too, so they are not sunk below the
+              // branch; the results replace them in place, so the common path copies nothing)
+              asm volatile("; %0 %1" ::"v"(nroot), "v"(ncls));
+              const int e2 = *(LU16 *)(uintptr_t)(ea + 2u * (sym + ((bits & ((1u << len) - 1u)) >> 8)));
+              const int sym2 = e2 & 0xFFF, len2 = 8 + (e2 >> 12);
+              const int nroot2 = *(LU16 *)(uintptr_t)lshl1_add((uint32_t)sym2, cb);
+              const uint32_t ncls2 = lut1b[sym2];
+              asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
+                           : "+v"(nroot), "+v"(ncls), "+v"(sym), "+v"(len)
+                           : "v"(nroot2), "v"(ncls2), "v"(sym2), "v"(len2));
+            }
+            vF = vP;
+            vP += len;
+            ob = lane == (pos & 63) ? (uint32_t)sym : ob;
+            vc2 = vc1;
+            vc1 = sym;
+            vroot = nroot;
+            vcls = ncls;
+            // the window keeps >= 32 bits at P (a literal takes <= 15)
+            const bool adv = vP - vPw >= 32;
+            vlo = adv ? vhi : vlo;
+            vhi = adv ? vn : vhi;
+            vn = adv ? vnv : vn;
+            vPw = adv ? vPw + 32 : vPw;
+            vnv = win32[(vPw >> 5) + 3];
+            pos++;
+          }
+          if ((pos & 63) == 0) {
+            const int p = (fl0 & ~63) + lane;
+            if (p >= fl0) ring[p] = (uint8_t)ob;
+            fl0 = pos;
+          }
+        }
+        // back to the scalar state
+        P = U(vP);
+        F = U(vF);
+        Pw = U(vPw);
+        W = (uint64_t)(uint32_t)U((int)vlo) | ((uint64_t)(uint32_t)U((int)vhi) << 32);
+        N = (uint32_t)U((int)vn);
+        Nv = vnv;
+        c1 = U(vc1);
+        c2b = U(vc2);
       } else {
         int root = U((int)g_lds.ctx_root[(lut1_of(c2b) << 8) | c1]);
         while (pos < end) {

@@ -50,7 +50,7 @@ template <int kTile, bool kHist, bool kParts>
 __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                                                              const uint32_t *sorted_keys, const uint32_t *sorted_vals,
                                                              uint32_t total, int depth, uint32_t max_dist, uint32_t *matches,
-                                                             int xcd_order) {
+                                                             int flags) {
   __shared__ uint32_t skey[kTile + kBack];
   __shared__ uint32_t spos[kTile + kBack];
   __shared__ uint64_t spre[kPreW][kTile + kBack];
@@ -58,6 +58,10 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
   // share one, MI355X_MICROARCH.md), so block b takes tile (b % 8) * per + b / 8 -- each XCD
   // sweeps one contiguous eighth of the sorted entries, a few streams at a time, meant to keep
   // the prefixes its tiles gather in its 4 MiB L2 (measured: no faster)
+  // flags (experiments): 1 the XCD order; 8 records stored in SORTED order (wrong streams:
+  // for timing the kernel without its scattered stores only)
+  const int xcd_order = flags & 1;
+  const bool sorted_store = flags & 8;
   const uint32_t ntiles = (total + kTile - 1) / kTile, per = (ntiles + 7) / 8;
   const uint32_t tix = xcd_order ? (blockIdx.x & 7) * per + (blockIdx.x >> 3) : blockIdx.x;
   if (tix >= ntiles) return;
@@ -228,10 +232,10 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
 #undef TAKE
     }
     // a match word is never 0 (length >= 4): the unused tail entries mark the count
-    *reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec) = make_uint4(local[0], local[1], local[2], local[3]);
+    *reinterpret_cast<uint4 *>(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec) = make_uint4(local[0], local[1], local[2], local[3]);
     return;
   }
-  *reinterpret_cast<uint4 *>(matches + (uint64_t)g * kMatchRec) = make_uint4(0u, 0u, 0u, 0u);   // no candidates
+  *reinterpret_cast<uint4 *>(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec) = make_uint4(0u, 0u, 0u, 0u);   // no candidates
 }
 
 // ---------------------------------------------------------------- streaming history update
@@ -355,9 +359,10 @@ void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_jo
   static const int tile = getenv("MIB_FM_TILE") ? atoi(getenv("MIB_FM_TILE")) : 256;
   // XCD-aware tile order (MIB_FM_XCD=1): measured no faster on C4 (64.9 vs 65.4 ms), off
   static const int xcd = getenv("MIB_FM_XCD") ? atoi(getenv("MIB_FM_XCD")) : 0;
+  static const int flags = (xcd ? 1 : 0) | (getenv("MIB_FM_SORTED_STORE") ? 8 : 0);
 #define MIB_FM(T, H, P)                                                                                                   \
   hipLaunchKernelGGL((find_matches_kernel<T, H, P>), dim3(8 * (((total + T - 1) / T + 7) / 8)), dim3(T), 0, st, jobs, pos_job, \
-                     seg_ref, skeys, svals, total, depth, max_dist, matches, xcd)
+                     seg_ref, skeys, svals, total, depth, max_dist, matches, flags)
 #define MIB_FM_T(T)                            \
   do {                                         \
     if (hist && parts) MIB_FM(T, true, true);  \
