@@ -58,6 +58,18 @@ constexpr int kLenTab = kLongCopy + 1;
 constexpr int kInsTab = 256;            // insert lengths with a table entry
 constexpr float kInf = 3.0e38f;
 constexpr uint32_t kCostLast = 255;   // cost code of a match at the path's last distance
+// LDS per workgroup sized for five workgroups per CU (the price table keeps kPtabW of its 24
+// columns: copy codes of relaxed lengths <= kLongCopy stay below it; literal costs as 16-bit
+// fixed point, which they are), VGPRs for MIB_DP_OCC waves per SIMD: the step is a dependent
+// chain (node fetch by ds_bpermute, two table reads, the relaxation's compares), so more waves
+// hide more of it -- five alone (C4 dp 106.5 -> 100.7 ms), but four beside the other encode
+// lanes' kernels (r04o: C4 2,937 vs 2,861 MB/s).
+#ifndef MIB_DP_OCC
+#define MIB_DP_OCC 4   // (A/B builds: 5; with two encode lanes 4 is faster, r04o)
+#endif
+constexpr int kDpWavesPerSimd = MIB_DP_OCC;
+constexpr int kPtabW = 20;
+static_assert(kLongCopy <= 325, "copy codes of lengths <= 325 are < 20 (command.ts getCopyLengthCode)");
 
 typedef const __attribute__((address_space(1))) uint8_t GCU8;
 
@@ -96,6 +108,17 @@ __device__ __forceinline__ uint32_t ins_extra_sel(int ic) {
   return u < 6u ? 0u : u < 16u ? (u - 4u) >> 1 : u < 21u ? u - 10u : u == 21u ? 12u : u == 22u ? 14u : 24u;
 }
 
+// copy_code (command.ts getCopyLengthCode) for 4 <= n <= 325 without branches or tables
+#ifndef MIB_DP_CC
+#define MIB_DP_CC 0   // (A/B builds: 1)
+#endif
+__device__ __forceinline__ uint32_t copy_code_sel(uint32_t n) {
+  const uint32_t a = n - 6u, nb = 30u - (uint32_t)__clz((int)(a | 1u));   // n in [10, 134): log2(n - 6) - 1
+  const uint32_t mid = (nb << 1) + (a >> nb) + 4u;
+  const uint32_t hi = 43u - (uint32_t)__clz((int)((n - 70u) | 1u));     // n in [134, 2118): log2(n - 70) + 12
+  return n < 10u ? n - 2u : n < 134u ? mid : hi;
+}
+
 struct Staged {   // one position's parse inputs as loaded
   uint32_t m[kMaxMatches];
   uint32_t nm;
@@ -126,7 +149,7 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
 // profiles tell the two passes apart).  KD: some stream has a custom dictionary (records with
 // kCDictMark; a separate build, so the common case pays nothing for it)
 template <int KS, bool KM, bool KD>
-__global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
+__global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
                                                            uint64_t *choice /* per position+1 */) {
@@ -135,10 +158,10 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
   static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
   constexpr uint64_t kLaneMask = kL == 64 ? ~0ull : ((1ull << kL) - 1);
-  __shared__ uint32_t ptab_all[kDpWaves * kS][24 * 24];   // per segment: (insert code, copy code) -> fp16 (explicit distance) | fp16 (short code 0) << 16
+  __shared__ uint32_t ptab_all[kDpWaves * kS][24 * kPtabW];   // per segment: (insert code, copy code) -> fp16 (explicit distance) | fp16 (short code 0) << 16
   __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
   __shared__ uint16_t itab[kInsTab];                       // insert length -> insert code | its extra bits << 8
-  __shared__ float litc_all[kDpWaves * kS][256];
+  __shared__ uint16_t litc_all[kDpWaves * kS][256];   // literal costs in 1/256 bits (exact: they are quantised so)
   __shared__ StageEnt stg_all[kDpWaves][64];
   for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 4 ? copy_code((uint32_t)t) : 0);
   for (int t = threadIdx.x; t < kInsTab; t += 64 * kDpWaves) {
@@ -150,7 +173,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   const uint32_t h = lane / kL, hl = lane % kL, hbase = h * kL;
   const int sgi = (blockIdx.x * kDpWaves + (int)w) * kS + (int)h;
   StageEnt *stg = stg_all[w];
-  float *litc = litc_all[w * kS + h];
+  uint16_t *litc = litc_all[w * kS + h];
   uint32_t *ptab = ptab_all[w * kS + h];
   // this lane group's segment (a = b: nothing to parse)
   uint32_t a = 0, b = 0, gbase = 0, job = 0;
@@ -183,8 +206,8 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   const CostModel *cm = (KM && a < b) ? model + job : nullptr;
   const float dist0 = dist_price(0, cm);
   if (a < b)
-    for (uint32_t t = hl; t < 24 * 24; t += kL) {
-      const int ic = (int)(t / 24), cc = (int)(t % 24);
+    for (uint32_t t = hl; t < 24 * kPtabW; t += kL) {
+      const int ic = (int)(t / kPtabW), cc = (int)(t % kPtabW);
       const _Float16 x = (_Float16)copy_price(ic, cc, false, dist0, cm), y = (_Float16)copy_price(ic, cc, true, dist0, cm);
       ptab[t] = (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
     }
@@ -193,7 +216,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
   if (cm) {
     if (a < b)
       for (uint32_t k = hl; k < 256; k += kL)
-        litc[k] = (float)(uint32_t)(fminf(fmaxf(cm->lit[k], 1.f), 255.f) * 256.f) * (1.f / 256.f);
+        litc[k] = (uint16_t)(uint32_t)(fminf(fmaxf(cm->lit[k], 1.f), 255.f) * 256.f);
   } else {
     uint32_t part = 0;
     if (a < b)
@@ -204,7 +227,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
       for (uint32_t k = hl; k < 256; k += kL) {
         const uint32_t c = lit_histo[job * 256 + k];
         const float v = c ? lt - log2f((float)c) : lt + 2.f;
-        litc[k] = (float)(uint32_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f) * (1.f / 256.f);
+        litc[k] = (uint16_t)(uint32_t)(fminf(fmaxf(v, 1.f), 255.f) * 256.f);
       }
   }
   wave_sync();
@@ -244,7 +267,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
     const uint32_t p = i0 + hl;
     const uint32_t nm = p < b ? cur.nm : 0u;
     StageEnt e;
-    e.lc = p < b ? litc[cur.lit] : 0.f;
+    e.lc = p < b ? (float)litc[cur.lit] * (1.f / 256.f) : 0.f;
     uint32_t maxlen = 0, word = 0;
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++) {
@@ -389,7 +412,7 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
                                       match_length(em.w) & actm};   // 0 past nm
     const uint32_t vpk[kMaxMatches] = {emc.x, emc.y, emc.z, emc.w};
     const uint32_t maxrel = max(1u, maxlen);
-    const uint32_t *trow = ptab + ic * 24;
+    const uint32_t *trow = ptab + ic * kPtabW;
     // relax every edge out of i: lane j of chunk k takes length kL k + j - off
 #pragma unroll
     for (int c = 0; c < kC; c++) {
@@ -404,7 +427,11 @@ __global__ __launch_bounds__(64 * kDpWaves) void dp_kernel(const Job *jobs, cons
 #pragma unroll
         for (int q = kMaxMatches - 1; q >= 0; q--)
           x = l <= mL[q] ? vpk[q] : x;   // mL = 0 past nm
+#if MIB_DP_CC
+        const uint32_t tv = trow[copy_code_sel(l)];   // (arithmetic: no dependent LDS read)
+#else
         const uint32_t tv = trow[cctab[l]];
+#endif
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
         nd = match_dist(x);

@@ -31,6 +31,7 @@
 #include <atomic>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "enc_common.h"
@@ -38,6 +39,8 @@
 extern "C" void mib_ctx_add_time(mib_ctx *c, const char *name, double ms);
 extern "C" int mib_ctx_profiling(mib_ctx *c);
 extern "C" void **mib_ctx_enc_ws(mib_ctx *c);
+extern "C" void **mib_ctx_lane_ws(mib_ctx *c, int l);
+extern "C" void *mib_ctx_lane_stream(mib_ctx *c, int l);
 extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need);
 
 // ====================================================================== host orchestration
@@ -292,7 +295,7 @@ const DictDev *dict_device(int dev) {
 
 // Encode a group of streams into d_out (packed from out_pos; returns the per-stream sizes).
 int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k, uint8_t *d_out, uint64_t out_cap,
-                 uint64_t out_pos, uint64_t *sizes, int32_t (*dc_out)[4], hipStream_t st) {
+                 uint64_t out_pos, uint64_t *sizes, int32_t (*dc_out)[4], hipStream_t st, void **ws_slot) {
   std::vector<Job> jobs(k);
   std::vector<Seg> segs;
   std::vector<Mb> mbs;
@@ -407,10 +410,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
   need += ns1 * sizeof(Seg) << kMaxPieceShift;   // parse pieces
   need += 40 * 256;   // alignment
-  Workspace *ws = reinterpret_cast<Workspace *>(*mib_ctx_enc_ws(ctx));
+  Workspace *ws = reinterpret_cast<Workspace *>(*ws_slot);
   if (!ws) {
     ws = new Workspace();
-    *mib_ctx_enc_ws(ctx) = ws;
+    *ws_slot = ws;
   }
   if (ws->cap < need) {
     if (ws->buf) hipFree(ws->buf);
@@ -577,16 +580,36 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
 constexpr uint64_t kWsBytesPerPosition = 80;
 constexpr size_t kGroupStreams = 65536;   // bounds the per-call descriptor arrays
 
+constexpr int kMaxLanes = 4;   // encode lanes at most (runtime.cpp kEncLanes; encode_streams)
 uint64_t group_position_limit(mib_ctx *ctx) {
   size_t free_b = 0, total_b = 0;
   uint64_t lim = (1ull << 31) - 4 * (uint64_t)kSeg;
   if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
     const Workspace *ws = reinterpret_cast<const Workspace *>(*mib_ctx_enc_ws(ctx));
-    const uint64_t usable = ((uint64_t)free_b + (ws ? ws->cap : 0)) / 10 * 8;   // leave 20% to the caller
+    uint64_t held = ws ? ws->cap : 0;
+    for (int l = 1; l < kMaxLanes; l++) {
+      const Workspace *wl = reinterpret_cast<const Workspace *>(*mib_ctx_lane_ws(ctx, l));
+      held += wl ? wl->cap : 0;
+    }
+    const uint64_t usable = ((uint64_t)free_b + held) / 10 * 8;   // leave 20% to the caller
     lim = std::min<uint64_t>(lim, std::max<uint64_t>(usable / kWsBytesPerPosition, 1ull << 24));
   }
   return lim;
 }
+
+// Encode lanes: a batch that fits one group runs as N parts (by positions) on N HIP streams at
+// once, each with its own workspace, lanes 1.. driven from host threads of their own.  The
+// parse and the match walk fill the chip on their own, but the ~20 small kernels after them
+// (codes, split, clustering, Huffman, sizes, emit: ~50 ms of a C4 step) are latency-bound,
+// block per segment or metablock: the other parts' kernels fill them.  Lanes 1.. pack their
+// streams into staging buffers that are then copied behind lane 0's.  MIB_ENC_LANES (1-4).
+uint64_t out_bound(uint64_t n);
+constexpr uint64_t kLaneMinPositions = 32ull << 20;   // positions per lane at least
+int enc_lanes() {
+  static const int n = (int)env_u32("MIB_ENC_LANES", 2, 1, kMaxLanes);
+  return n;
+}
+constexpr int kLaneStage = 4;   // mib_ctx_stage slots of lanes 1.. packed output: 4, 5, 6
 
 // Split k streams into groups and encode them back to back into d_out.
 int encode_streams(mib_ctx *ctx, const mib_enc_opts *o, const StreamDesc *sd, size_t k, uint8_t *d_out,
@@ -594,6 +617,69 @@ int encode_streams(mib_ctx *ctx, const mib_enc_opts *o, const StreamDesc *sd, si
   const uint64_t kGroupPositions = group_position_limit(ctx);
   Params prm = make_params(o);
   out_offsets[0] = 0;
+  // lanes when the whole call is one group
+  uint64_t all = 0;
+  for (size_t j = 0; j < k; j++) all += ((sd[j].n + kSeg - 1) / kSeg + 1) * kSeg;
+  const int nl = (int)std::min<uint64_t>(std::min<uint64_t>((uint64_t)enc_lanes(), k), all / kLaneMinPositions);
+  if (nl >= 2 && k <= kGroupStreams && all <= kGroupPositions) {
+    // lane l takes streams [cut[l], cut[l + 1]): near equal positions
+    std::vector<size_t> cut(nl + 1, k);
+    cut[0] = 0;
+    {
+      uint64_t pos = 0;
+      size_t j = 0;
+      for (int l = 1; l < nl; l++) {   // (every lane gets a stream at least)
+        while (j < k - (size_t)(nl - l) && (j <= cut[l - 1] || pos * nl < all * (uint64_t)l))
+          pos += ((sd[j++].n + kSeg - 1) / kSeg + 1) * kSeg;
+        cut[l] = j;
+      }
+    }
+    std::vector<hipStream_t> lst(nl, st);
+    std::vector<uint8_t *> lout(nl, d_out);
+    std::vector<uint64_t> lcap(nl, out_cap);
+    bool ok = true;
+    for (int l = 1; l < nl && ok; l++) {
+      uint64_t b = 64;
+      for (size_t j = cut[l]; j < cut[l + 1]; j++) b += out_bound(sd[j].n);
+      lst[l] = (hipStream_t)mib_ctx_lane_stream(ctx, l);
+      lout[l] = mib_ctx_stage(ctx, kLaneStage + l - 1, b);
+      lcap[l] = b;
+      ok = lst[l] && lout[l];
+    }
+    if (ok) {
+      // lanes 1.. start after everything already queued on st (inputs, the dictionary)
+      hipEvent_t ev;
+      CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      CK(hipEventRecord(ev, st));
+      for (int l = 1; l < nl; l++) CK(hipStreamWaitEvent(lst[l], ev, 0));
+      std::vector<uint64_t> sz(k, 0);
+      std::vector<int> rc(nl, 0);
+      const int dev = mib_ctx_device_of(ctx);
+      auto run = [&](int l) {
+        if (l && hipSetDevice(dev) != hipSuccess) {
+          rc[l] = MIB_E_NO_DEVICE;
+          return;
+        }
+        rc[l] = encode_group(ctx, prm, sd + cut[l], cut[l + 1] - cut[l], lout[l], lcap[l], 0, sz.data() + cut[l],
+                             dc_out ? dc_out + cut[l] : nullptr, lst[l], l ? mib_ctx_lane_ws(ctx, l) : mib_ctx_enc_ws(ctx));
+      };
+      std::vector<std::thread> th;
+      for (int l = 1; l < nl; l++) th.emplace_back(run, l);
+      run(0);
+      for (auto &t : th) t.join();
+      hipEventDestroy(ev);
+      for (int l = 0; l < nl; l++)
+        if (rc[l]) return rc[l];
+      for (size_t q = 0; q < k; q++) out_offsets[q + 1] = out_offsets[q] + sz[q];
+      if (out_offsets[k] > out_cap) return MIB_E_NEED_SPACE;
+      for (int l = 1; l < nl; l++) {
+        const uint64_t n1 = out_offsets[cut[l + 1]] - out_offsets[cut[l]];
+        if (n1) CK(hipMemcpyAsync(d_out + out_offsets[cut[l]], lout[l], n1, hipMemcpyDeviceToDevice, st));
+      }
+      CK(hipStreamSynchronize(st));
+      return 0;
+    }
+  }
   size_t i = 0;
   std::vector<uint64_t> sizes;
   while (i < k) {
@@ -607,7 +693,7 @@ int encode_streams(mib_ctx *ctx, const mib_enc_opts *o, const StreamDesc *sd, si
     }
     sizes.assign(j - i, 0);
     int rc = encode_group(ctx, prm, sd + i, j - i, d_out, out_cap, out_offsets[i], sizes.data(), dc_out ? dc_out + i : nullptr,
-                          st);
+                          st, mib_ctx_enc_ws(ctx));
     if (rc) return rc;
     for (size_t q = i; q < j; q++) out_offsets[q + 1] = out_offsets[q] + sizes[q - i];
     i = j;

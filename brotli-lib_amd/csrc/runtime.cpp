@@ -275,6 +275,8 @@ int waves_per_cu(int device, size_t waves) {
 
 }  // namespace
 
+constexpr int kEncLanes = 4;                  // encode lanes at most (encode.hip)
+constexpr int kStageSlots = 4 + kEncLanes - 1;   // + lanes 1.. packed output
 struct mib_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -288,18 +290,24 @@ struct mib_ctx {
   // part decoding: entries, positions, progress words, ticket (one allocation)
   uint8_t *d_parts = nullptr;
   uint64_t parts_bytes = 0;
-  // encode workspace (encode.hip)
+  // encode workspaces (encode.hip): lane 0 on `stream`, lane l > 0 on lane_stream[l] (a batch
+  // encode runs as concurrent parts, encode_streams)
   void *enc_ws = nullptr;
+  void *lane_ws[kEncLanes] = {};
+  hipStream_t lane_stream[kEncLanes] = {};
   // staging buffers of the host-memory entry points (input, output, dictionary, encoder
-  // output), kept across calls so a small call does not pay hipMalloc / hipFree
-  uint8_t *stage[4] = {nullptr, nullptr, nullptr, nullptr};
-  uint64_t stage_cap[4] = {0, 0, 0, 0};
+  // output) and lane 1's packed output, kept across calls so a small call does not pay
+  // hipMalloc / hipFree
+  uint8_t *stage[kStageSlots] = {};
+  uint64_t stage_cap[kStageSlots] = {};
   // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
   uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
   bool profiling = false;
   std::vector<mib_kernel_time> times;
+  std::mutex times_mu;   // (two encode lanes collect at once)
   void add_time(const char *name, double ms) {
+    std::lock_guard<std::mutex> lk(times_mu);
     for (auto &t : times)
       if (strncmp(t.name, name, sizeof(t.name)) == 0) {
         t.ms += ms;
@@ -318,10 +326,20 @@ struct mib_ctx {
 extern "C" void mib_ctx_add_time(mib_ctx *c, const char *name, double ms) { c->add_time(name, ms); }
 extern "C" int mib_ctx_profiling(mib_ctx *c) { return c->profiling ? 1 : 0; }
 extern "C" void **mib_ctx_enc_ws(mib_ctx *c) { return &c->enc_ws; }
+// encode lane l (1 .. kEncLanes - 1): its workspace slot, its stream (created on first use, on
+// the context's device)
+extern "C" void **mib_ctx_lane_ws(mib_ctx *c, int l) { return &c->lane_ws[l]; }
+extern "C" void *mib_ctx_lane_stream(mib_ctx *c, int l) {
+  if (!c->lane_stream[l]) {
+    hipSetDevice(c->device);
+    if (hipStreamCreateWithFlags(&c->lane_stream[l], hipStreamNonBlocking) != hipSuccess) c->lane_stream[l] = nullptr;
+  }
+  return (void *)c->lane_stream[l];
+}
 int grow(void **p, uint64_t *cap, uint64_t need);
 // a staging buffer of at least `need` bytes (its content is not kept when it grows)
 extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need) {
-  if (slot < 0 || slot > 3) return nullptr;
+  if (slot < 0 || slot >= kStageSlots) return nullptr;
   return grow((void **)&c->stage[slot], &c->stage_cap[slot], need) == 0 ? c->stage[slot] : nullptr;
 }
 extern "C" void mib_encode_ws_free(void *ws);
@@ -530,10 +548,14 @@ void mib_ctx_free(mib_ctx *c) {
   if (c->d_jobs) hipFree(c->d_jobs);
   if (c->d_aux) hipFree(c->d_aux);
   if (c->d_parts) hipFree(c->d_parts);
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < kStageSlots; i++)
     if (c->stage[i]) hipFree(c->stage[i]);
   if (c->enc_ws) mib_encode_ws_free(c->enc_ws);
   if (c->stream) hipStreamDestroy(c->stream);
+  for (int l = 0; l < kEncLanes; l++) {
+    if (c->lane_ws[l]) mib_encode_ws_free(c->lane_ws[l]);
+    if (c->lane_stream[l]) hipStreamDestroy(c->lane_stream[l]);
+  }
   delete c;
 }
 
@@ -569,20 +591,24 @@ static void trim_default_ctx(mib_ctx *c) {
   // (while a BrotliEncoder lives, its chunk after chunk reuses the workspace and the encoder
   // output stage: kept)
   const bool streaming = mib_live_encoders() > 0;
-  for (int i = 0; i < 4; i++)
+  for (int i = 0; i < kStageSlots; i++)
     if (!(streaming && i == 3)) release_large(&c->stage[i], &c->stage_cap[i], kKeepStage);
   release_large(&c->d_scratch, &c->scratch_bytes, kKeepScratch);
   release_large(&c->d_parts, &c->parts_bytes, kKeepScratch);
-  if (!streaming) mib_encode_ws_trim(&c->enc_ws, kKeepScratch);
+  if (!streaming) {
+    mib_encode_ws_trim(&c->enc_ws, kKeepScratch);
+    for (int l = 0; l < kEncLanes; l++) mib_encode_ws_trim(&c->lane_ws[l], kKeepScratch);
+  }
 }
 // a context's buffers above these sizes (staging slots; decoder scratch, part tables and
 // encoder workspace), released (multi.cpp's shard contexts after each sharded call)
 void mib_ctx_trim(mib_ctx *c, uint64_t keep_stage, uint64_t keep_scratch) {
   hipSetDevice(c->device);
-  for (int i = 0; i < 4; i++) release_large(&c->stage[i], &c->stage_cap[i], keep_stage);
+  for (int i = 0; i < kStageSlots; i++) release_large(&c->stage[i], &c->stage_cap[i], keep_stage);
   release_large(&c->d_scratch, &c->scratch_bytes, keep_scratch);
   release_large(&c->d_parts, &c->parts_bytes, keep_scratch);
   mib_encode_ws_trim(&c->enc_ws, keep_scratch);
+  for (int l = 0; l < kEncLanes; l++) mib_encode_ws_trim(&c->lane_ws[l], keep_scratch);
 }
 void mib_default_lock(int on) {
   if (on) {
