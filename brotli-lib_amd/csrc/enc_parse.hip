@@ -152,7 +152,7 @@ template <int KS, bool KM, bool KD>
 __global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
-                                                           uint64_t *choice /* per position+1 */) {
+                                                           uint64_t *choice /* per position+1 */, float cmd_pen) {
   constexpr int kS = KS;                // segments per wave
   constexpr int kL = 64 / kS;           // lanes per segment
   constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
@@ -162,7 +162,9 @@ __global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(cons
   __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
   __shared__ uint16_t itab[kInsTab];                       // insert length -> insert code | its extra bits << 8
   __shared__ uint16_t litc_all[kDpWaves * kS][256];   // literal costs in 1/256 bits (exact: they are quantised so)
-  __shared__ StageEnt stg_all[kDpWaves][64];
+  // (one spare entry per 32 lanes: the groups' entries i and 32 + i fall 12 banks apart, not on
+  // the same banks -- two segments at the same offset read them in one instruction)
+  __shared__ StageEnt stg_all[kDpWaves][64 + 2];
   for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 4 ? copy_code((uint32_t)t) : 0);
   for (int t = threadIdx.x; t < kInsTab; t += 64 * kDpWaves) {
     const int ic = ins_code((uint32_t)t);
@@ -208,7 +210,8 @@ __global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(cons
   if (a < b)
     for (uint32_t t = hl; t < 24 * kPtabW; t += kL) {
       const int ic = (int)(t / kPtabW), cc = (int)(t % kPtabW);
-      const _Float16 x = (_Float16)copy_price(ic, cc, false, dist0, cm), y = (_Float16)copy_price(ic, cc, true, dist0, cm);
+      const _Float16 x = (_Float16)(copy_price(ic, cc, false, dist0, cm) + cmd_pen),
+                     y = (_Float16)(copy_price(ic, cc, true, dist0, cm) + cmd_pen);
       ptab[t] = (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
     }
   // literal costs: iteration 0 from the stream's order-0 histogram (zopfli-cost-model.ts:
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(cons
     }
     e.info = (maxlen ? nm : 0u) | (maxlen << 8) | ((word ? maxlen : 4u) << 16);   // | the shortest usable length
     e.pad[0] = e.pad[1] = 0;
-    stg[lane] = e;
+    stg[lane + (lane >> 5)] = e;
     DPCOUNT(6, 1);
   };
   if (!done) stage();
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(cons
       }
     }
     const bool act = !done;
-    const StageEnt &e = stg[src];
+    const StageEnt &e = stg[src + (src >> 5)];
     const uint32_t info = e.info;
     const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? ((info >> 8) & 0xFF) : 0u;
     const uint32_t minlen = info >> 16;   // 4, or a dictionary word's length: that length only
@@ -927,21 +930,23 @@ template <bool KD>
 static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
                         const CostModel *model, const uint32_t *matches, uint64_t *choice) {
   const dim3 g(dp_workgroups(nsegs)), b(64 * kDpWaves);
+  // MIB_CMD_PENALTY (bits, experiment): added to every copy's price, fewer and longer commands
+  static const float cmd_pen = getenv("MIB_CMD_PENALTY") ? (float)atof(getenv("MIB_CMD_PENALTY")) : 0.f;
   if (dp_ks(nsegs) == 1) {
     if (model)
-      hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
     else
-      hipLaunchKernelGGL((dp_kernel<1, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<1, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
   } else if (dp_ks(nsegs) == 4) {
     if (model)
-      hipLaunchKernelGGL((dp_kernel<4, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<4, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
     else
-      hipLaunchKernelGGL((dp_kernel<4, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<4, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
   } else {
     if (model)
-      hipLaunchKernelGGL((dp_kernel<2, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<2, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
     else
-      hipLaunchKernelGGL((dp_kernel<2, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice);
+      hipLaunchKernelGGL((dp_kernel<2, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
   }
 }
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
