@@ -107,17 +107,20 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       const int dmax = min(depth, kBack);
       for (int t = 1; t <= dmax; t++) {
         const int e = me - t;
-        if (skey[e] != key || spos[e] < sr.pos_base) break;   // bucket or stream changes
-        const uint32_t d = g - spos[e];
-        if (d > max_dist || best >= limit) break;
+        // one exit test and one reject test per candidate, computed without branches (the
+        // nested ifs were four exec-mask branches per candidate: 65.8 -> 62.6 ms on C4, r04t2)
+        const uint32_t ke = skey[e], pe = spos[e];
+        const uint64_t x0 = mine0 ^ spre[0][e];
+        const uint32_t d = g - pe;
+        if ((ke != key) | (pe < sr.pos_base) | (d > max_dist) | (best >= limit)) break;
+        const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
+        if ((x0 != 0) & (qlen <= best)) continue;   // known exactly and not longer
         const uint32_t pc = parts ? part_cap(pA, d, pbits, plag) : ~0u;   // part index: lagging source
         if (pc <= best) continue;
-        const uint64_t x0 = mine0 ^ spre[0][e];
         uint32_t len;
         if (x0) {
-          len = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;
-          if (len <= best) continue;
-      } else {
+          len = qlen;
+        } else {
           // a candidate can only beat `best` if it matches byte `best` too
           if (best < 8 * kPreW) {
             const uint32_t sh = 8 * (best & 7);
@@ -174,17 +177,20 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       bool stop = false;
       for (; t <= dmax; t++) {
         const int e = me - t;
-        if (skey[e] != key || spos[e] < sr.pos_base) break;   // bucket or stream changes
-        const uint32_t d = g - spos[e];
-        if (d > max_dist || best >= limit) {
-          stop = true;
+        // (the tests flattened as in the window-only walk above)
+        const uint32_t ke = skey[e], pe = spos[e];
+        const uint64_t x0 = mine0 ^ spre[0][e];
+        const uint32_t d = g - pe;
+        const bool endb = (ke != key) | (pe < sr.pos_base);   // bucket or stream changes
+        if (endb | (d > max_dist) | (best >= limit)) {
+          stop = !endb;
           break;
         }
-        const uint64_t x0 = mine0 ^ spre[0][e];
+        const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
+        if ((x0 != 0) & (qlen <= best)) continue;
         uint32_t len;
         if (x0) {
-          len = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;
-          if (len <= best) continue;
+          len = qlen;
         } else {
           // a candidate can only beat `best` if it matches byte `best` too
           if (best < 8 * kPreW) {
