@@ -108,17 +108,6 @@ __device__ __forceinline__ uint32_t ins_extra_sel(int ic) {
   return u < 6u ? 0u : u < 16u ? (u - 4u) >> 1 : u < 21u ? u - 10u : u == 21u ? 12u : u == 22u ? 14u : 24u;
 }
 
-// copy_code (command.ts getCopyLengthCode) for 4 <= n <= 325 without branches or tables
-#ifndef MIB_DP_CC
-#define MIB_DP_CC 0   // (A/B builds: 1)
-#endif
-__device__ __forceinline__ uint32_t copy_code_sel(uint32_t n) {
-  const uint32_t a = n - 6u, nb = 30u - (uint32_t)__clz((int)(a | 1u));   // n in [10, 134): log2(n - 6) - 1
-  const uint32_t mid = (nb << 1) + (a >> nb) + 4u;
-  const uint32_t hi = 43u - (uint32_t)__clz((int)((n - 70u) | 1u));     // n in [134, 2118): log2(n - 70) + 12
-  return n < 10u ? n - 2u : n < 134u ? mid : hi;
-}
-
 struct Staged {   // one position's parse inputs as loaded
   uint32_t m[kMaxMatches];
   uint32_t nm;
@@ -430,11 +419,7 @@ __global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(cons
 #pragma unroll
         for (int q = kMaxMatches - 1; q >= 0; q--)
           x = l <= mL[q] ? vpk[q] : x;   // mL = 0 past nm
-#if MIB_DP_CC
-        const uint32_t tv = trow[copy_code_sel(l)];   // (arithmetic: no dependent LDS read)
-#else
         const uint32_t tv = trow[cctab[l]];
-#endif
         const float pn = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv & 0xFFFF));
         const float pl = (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
         nd = match_dist(x);
