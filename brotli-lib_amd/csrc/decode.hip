@@ -165,6 +165,11 @@ __device__ __forceinline__ uint32_t lshl1_add(uint32_t a, uint32_t b) {   // a *
 #define MIB_VLIT 1
 #endif
 constexpr bool kVlit = MIB_VLIT;
+// fast_loop's one-code literals: 64 entries decoded at once and walked (1), or the chain (0)
+#ifndef MIB_SPECLIT
+#define MIB_SPECLIT 1
+#endif
+constexpr bool kSpecLit = MIB_SPECLIT;
 
 #define ERR(s, c) ((s).running = (s).running >= 0 ? (c) : (s).running, (c))
 
@@ -1891,7 +1896,55 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       // literals are gathered one per lane (lane pos & 63) and stored a
       // 64-byte line at a time; the inner loops run to the next line end, so the line check
       // is not paid per literal
-      if (kTrivial && kVlit) {
+      if (kTrivial && kSpecLit) {
+        // One code for every literal: the entries of 64 literals-to-be are read at once, lane l
+        // decoding as if a literal started at bit Pb + l (one LDS read; the second-level tables
+        // per lane), and the run walks them: literal k starts at offset o, its entry is lane
+        // o's (a v_readlane), the next starts at o + its length.  ~12 scalar instructions a
+        // literal instead of an LDS round trip each; a new set of entries when o passes 63.
+        // (kTrivial never reads the context bytes c1 / c2b: not tracked here.)
+        int Pb = P, o = 0, last = P;
+        bool fresh = true;
+        int ent = 0;
+        while (pos < end) {
+          const int seg_end = U(min(end, (pos | 63) + 1));
+          while (pos < seg_end) {
+            if (fresh || o >= 64) {
+              Pb += o;
+              o = 0;
+              fresh = false;
+              // the 128 bits from Pw = Pb & ~31 (the handover test keeps them inside win)
+              const int pw = Pb & ~31;
+              const uint32_t w0 = win32[pw >> 5], w1 = win32[(pw >> 5) + 1], w2 = win32[(pw >> 5) + 2],
+                             w3 = win32[(pw >> 5) + 3];
+              const uint32_t ol = (uint32_t)(Pb - pw) + (uint32_t)lane;   // < 95
+              const uint32_t lo = ol < 32 ? w0 : ol < 64 ? w1 : w2, hi = ol < 32 ? w1 : ol < 64 ? w2 : w3;
+              const uint32_t bits = __builtin_amdgcn_alignbit(hi, lo, ol);   // 32 bits at Pb + lane
+              const int i1 = lit_root + (int)(bits & 0xFF);
+              ent = t16[i1];
+              if (ent >= 0x9000)   // a second-level table (per lane); its length + the 8 root bits
+                ent = t16[i1 + (ent & 0xFFF) + (int)((bits & ((1u << (ent >> 12)) - 1u)) >> 8)] + (8 << 12);
+            }
+            const int ek = __builtin_amdgcn_readlane(ent, o);
+            last = Pb + o;
+            ob = write_lane(ob, (uint32_t)(ek & 0xFFF), (uint32_t)(pos & 63));
+            o += ek >> 12;
+            pos++;
+          }
+          if ((pos & 63) == 0) {
+            const int p = (fl0 & ~63) + lane;
+            if (p >= fl0) ring[p] = (uint8_t)ob;
+            fl0 = pos;
+          }
+        }
+        // the reader after the run: position, fill point (the last literal's start), window
+        P = Pb + o;
+        F = last;
+        Pw = P & ~31;
+        W = (uint64_t)(uint32_t)U((int)win32[Pw >> 5]) | ((uint64_t)(uint32_t)U((int)win32[(Pw >> 5) + 1]) << 32);
+        N = (uint32_t)U((int)win32[(Pw >> 5) + 2]);
+        Nv = win32[(Pw >> 5) + 3];
+      } else if (kTrivial && kVlit) {
         // one code: entry (LDS) -> its length -> the next entry, the chain in VGPRs (as below)
         ensure();
         uint32_t vlo = (uint32_t)W, vhi = (uint32_t)(W >> 32), vn = N, vnv = Nv;
