@@ -2015,18 +2015,24 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
         // entry, the root from a gathered row by v_readlane -- took ~450 cycles a literal: an LDS
         // read crossing to SGPRs costs ~120 cycles and a dependent v_readlane ~80, against ~70
         // for an LDS read feeding VALU ops, scripts/probe/chain_probe.hip on the MI355X.)
+        // The bits come from a 128-bit window w0..w3 at pw (a multiple of 32) with the offset
+        // of P in it below 64, in a VGPR for the extraction and in an SGPR for the refill test
+        // (taken every ~10 literals: the window moves by 64 bits).
         ensure();   // P - Pw < 32
         LU8 *lut1b = (LU8 *)g_lds.ctx_lut + 256;
         LU16 *croot = (LU16 *)g_lds.ctx_root;
-        uint32_t vlo = (uint32_t)W, vhi = (uint32_t)(W >> 32), vn = N, vnv = Nv;
-        int vP = P, vPw = Pw, vF = F;
+        uint32_t w0 = (uint32_t)W, w1 = (uint32_t)(W >> 32), w2 = N, w3 = Nv;
+        int pw = Pw, so = P - Pw;
+        uint32_t vo = (uint32_t)so;
+        int vF = F;
         int vc1 = c1, vc2 = c2b;
         int vroot = croot[(lut1b[c2b] << 8) | c1];
         uint32_t vcls = lut1b[c1];   // lut1[p2] of the next literal
         while (pos < end) {
           const int seg_end = U(min(end, (pos | 63) + 1));
           while (pos < seg_end) {
-            const uint32_t bits = __builtin_amdgcn_alignbit(vhi, vlo, (uint32_t)(vP - vPw));   // 32 bits at P
+            const bool up = vo >= 32u;
+            const uint32_t bits = __builtin_amdgcn_alignbit(up ? w2 : w1, up ? w1 : w0, vo);   // 32 bits at P
             // (LDS byte addresses as index * 2 + a base ready early: one v_lshl_add on the chain)
             const uint32_t tb = lds_addr(t16) + ((bits & 0xFF) << 1);
             const uint32_t ea = lshl1_add((uint32_t)vroot, tb);
@@ -2036,7 +2042,9 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
             // the next root and context class, issued before the second-level test resolves
             int nroot = *(LU16 *)(uintptr_t)lshl1_add((uint32_t)sym, cb);
             uint32_t ncls = lut1b[sym];
-            if (__builtin_expect(U(e) >= 0x9000, 0)) {   // a second-level table (uniform branch)
+            const int se = U(e);
+            int slen = se >> 12;
+            if (__builtin_expect(se >= 0x9000, 0)) {   // a second-level table (uniform branch)
               // (the first reads are used on this path too, so they are not sunk below the
               // branch; the results replace them in place, so the common path copies nothing)
               asm volatile("; %0 %1" ::"v"(nroot), "v"(ncls));
@@ -2047,21 +2055,25 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
               asm volatile("v_mov_b32 %0, %4\n\tv_mov_b32 %1, %5\n\tv_mov_b32 %2, %6\n\tv_mov_b32 %3, %7"
                            : "+v"(nroot), "+v"(ncls), "+v"(sym), "+v"(len)
                            : "v"(nroot2), "v"(ncls2), "v"(sym2), "v"(len2));
+              slen = U(len2);
             }
-            vF = vP;
-            vP += len;
+            vF = pw + (int)vo;
+            vo += (uint32_t)len;
+            so += slen;
             ob = lane == (pos & 63) ? (uint32_t)sym : ob;
             vc2 = vc1;
             vc1 = sym;
             vroot = nroot;
             vcls = ncls;
-            // the window keeps >= 32 bits at P (a literal takes <= 15)
-            const bool adv = vP - vPw >= 32;
-            vlo = adv ? vhi : vlo;
-            vhi = adv ? vn : vhi;
-            vn = adv ? vnv : vn;
-            vPw = adv ? vPw + 32 : vPw;
-            vnv = win32[(vPw >> 5) + 3];
+            if (so >= 64) {   // the window moves by 64 bits (a literal takes <= 15)
+              pw += 64;
+              so -= 64;
+              vo -= 64u;
+              w0 = w2;
+              w1 = w3;
+              w2 = win32[(pw >> 5) + 2];
+              w3 = win32[(pw >> 5) + 3];
+            }
             pos++;
           }
           if ((pos & 63) == 0) {
@@ -2070,13 +2082,13 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
             fl0 = pos;
           }
         }
-        // back to the scalar state
-        P = U(vP);
+        // back to the scalar state (the reader's window reloaded at P)
+        P = pw + so;
         F = U(vF);
-        Pw = U(vPw);
-        W = (uint64_t)(uint32_t)U((int)vlo) | ((uint64_t)(uint32_t)U((int)vhi) << 32);
-        N = (uint32_t)U((int)vn);
-        Nv = vnv;
+        Pw = P & ~31;
+        W = (uint64_t)(uint32_t)U((int)win32[Pw >> 5]) | ((uint64_t)(uint32_t)U((int)win32[(Pw >> 5) + 1]) << 32);
+        N = (uint32_t)U((int)win32[(Pw >> 5) + 2]);
+        Nv = win32[(Pw >> 5) + 3];
         c1 = U(vc1);
         c2b = U(vc2);
       } else {
