@@ -86,9 +86,40 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     for (int i = 0; i < kPreW; i++) spre[i][t] = pre[i];
   }
   __syncthreads();
+  // Each entry's candidates are the entries before it in its bucket run (same key, same
+  // stream): the run's first index by a segmented max-scan -- a flag where the key or the
+  // stream changes, the wave's prefix maximum of the flagged indices, the chunks before it
+  // carried through LDS -- so the walk's trip count is known and its loop reads no keys.
+  // (Wave w scans entries kBack + 64 w .. + 63; wave 0 also the kBack lookback entries.)
+  __shared__ int chunk_last[kTile / 64 + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  auto run_flag = [&](int e) -> int {   // e > 0
+    return (skey[e] != skey[e - 1] || spos[e - 1] < sr.pos_base) ? e : -1;
+  };
+  auto wave_max_scan = [&](int v) -> int {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(v, o);
+      v = lane >= o ? max(v, u) : v;
+    }
+    return v;
+  };
+  const int me = kBack + threadIdx.x;
+  int st_local = wave_max_scan(run_flag(me));
+  if (lane == 63) chunk_last[wv + 1] = st_local;
+  if (wv == 0) {
+    const int lb = wave_max_scan(lane == 0 ? 0 : run_flag(lane));
+    if (lane == 63) chunk_last[0] = lb;   // (>= 0: entry 0 starts a run)
+  }
+  __syncthreads();
+  if (st_local < 0) {
+    int c = chunk_last[0];
+    for (int q = 1; q <= wv; q++) c = max(c, chunk_last[q]);
+    st_local = c;
+  }
+  const int nrun = me - st_local;   // the entries before me in my run
   const uint32_t r = r0 + threadIdx.x;
   if (r >= total) return;
-  const int me = kBack + threadIdx.x;
   const uint32_t key = skey[me], g = spos[me];
   int cnt = 0;
   if ((key & kInvalidKey) == 0) {
@@ -104,15 +135,16 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
     if constexpr (!kHist) {
       const uint64_t mine0 = spre[0][me];
-      const int dmax = min(depth, kBack);
-      for (int t = 1; t <= dmax; t++) {
+      const int dmax = min(depth, kBack), nwalk = min(dmax, nrun);
+      for (int t = 1; t <= nwalk; t++) {
         const int e = me - t;
         // one exit test and one reject test per candidate, computed without branches (the
-        // nested ifs were four exec-mask branches per candidate: 65.8 -> 62.6 ms on C4, r04t2)
-        const uint32_t ke = skey[e], pe = spos[e];
+        // nested ifs were four exec-mask branches per candidate: 65.8 -> 62.6 ms on C4, r04t2);
+        // the bucket run's end is the trip count
+        const uint32_t pe = spos[e];
         const uint64_t x0 = mine0 ^ spre[0][e];
         const uint32_t d = g - pe;
-        if ((ke != key) | (pe < sr.pos_base) | (d > max_dist) | (best >= limit)) break;
+        if ((d > max_dist) | (best >= limit)) break;
         const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
         if ((x0 != 0) & (qlen <= best)) continue;   // known exactly and not longer
         const uint32_t pc = parts ? part_cap(pA, d, pbits, plag) : ~0u;   // part index: lagging source
@@ -175,15 +207,15 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       const int dmax = min(depth, kBack);
       int t = 1;
       bool stop = false;
-      for (; t <= dmax; t++) {
+      const int nwalk = min(dmax, nrun);
+      for (; t <= nwalk; t++) {
         const int e = me - t;
-        // (the tests flattened as in the window-only walk above)
-        const uint32_t ke = skey[e], pe = spos[e];
+        // (the tests flattened as in the window-only walk above; the run's end is the trip count)
+        const uint32_t pe = spos[e];
         const uint64_t x0 = mine0 ^ spre[0][e];
         const uint32_t d = g - pe;
-        const bool endb = (ke != key) | (pe < sr.pos_base);   // bucket or stream changes
-        if (endb | (d > max_dist) | (best >= limit)) {
-          stop = !endb;
+        if ((d > max_dist) | (best >= limit)) {
+          stop = true;
           break;
         }
         const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
