@@ -38,9 +38,11 @@ constexpr int kLitCtx = 64;                   // literal contexts (RFC 7932 sect
 constexpr int kDistCtx = 4;                   // distance contexts (copy length 2, 3, 4, >4)
 // Block splitting (block-splitter.ts): up to kMaxBT block types per category, decided per
 // metablock over 8 KiB units of commands (kSubBits), kSubPerSeg units per parse segment.
-constexpr int kMaxBT = 4;
+constexpr int kMaxBT = 8;
 constexpr uint32_t kSubBits = 13;
 constexpr int kSubPerSeg = 1 << (kSegBits - kSubBits);
+constexpr int kSplitWideUnits = 256;          // literal metablocks of up to 2 MiB (units) may take 8
+                                              // types, longer ones 4 (enc_entropy.hip split_k)
 constexpr int kSubHist = 256 + 704 + 128;      // a unit's literal | command | distance-code histograms
 constexpr int kMaxLitTrees = 64;              // literal prefix codes per metablock (decoder tables stay in LDS)
 // code slots: literal (type, cluster) | command (type) | distance (type, cluster)
@@ -150,7 +152,7 @@ struct Mb {                   // one metablock: block types per category, litera
   uint32_t nbt[3];            // block types: literal, command, distance
   uint32_t first_count[3];    // symbols in the first block of each category
   uint32_t nlit_t[kMaxBT], ndist_t[kMaxBT];   // prefix codes (clusters) per literal / distance block type
-  uint8_t lit_cmap[kLitSlots];             // (type, context) -> literal code slot (type * 64 + cluster)
+  uint16_t lit_cmap[kLitSlots];            // (type, context) -> literal code slot (type * 64 + cluster)
   uint8_t dist_cmap[kMaxBT * kDistCtx];    // (type, context) -> distance code slot (type * 4 + cluster)
   uint32_t tree_bits[kTreeSlots];
   uint64_t bit_off;           // of the header, stream-relative
@@ -402,7 +404,7 @@ __device__ __forceinline__ uint32_t header_bits(const Codes &cd, const Cmd &c, c
 }
 // (lut, cmap: the context-mode table and the metablock's literal context map, LDS copies in
 // the sizes / emit kernels)
-__device__ __forceinline__ int literal_tree(const uint8_t *cmap, const uint8_t *lut, const Unit &u, uint32_t p12) {
+__device__ __forceinline__ int literal_tree(const uint16_t *cmap, const uint8_t *lut, const Unit &u, uint32_t p12) {
   return cmap[u.type[0] * kLitCtx + (lut[p12 & 0xFF] | lut[256 + (p12 >> 8)])];
 }
 __device__ __forceinline__ uint32_t dist_bits(const Codes &cd, const Mb &mb, const Cmd &c, const Unit &u, uint32_t q) {
@@ -413,7 +415,7 @@ __device__ __forceinline__ uint32_t dist_bits(const Codes &cd, const Mb &mb, con
 }
 // bits of item k of command c (insert at stream position p); su: the segment's units (the
 // command's header and distance go by the unit of p, each literal by its own position's)
-__device__ __forceinline__ uint32_t item_bits(const Codes &cd, const Mb &mb, const uint8_t *cmap, const uint8_t *lut, const Job &jb,
+__device__ __forceinline__ uint32_t item_bits(const Codes &cd, const Mb &mb, const uint16_t *cmap, const uint8_t *lut, const Job &jb,
                                               const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q,
                                               uint32_t k) {
   if (k == 0) return header_bits(cd, c, su[unit_of(sg, p)], q);
@@ -465,7 +467,8 @@ void launch_sort(hipStream_t st, const Job *jobs, const uint32_t *pos_job, int n
                  uint32_t *tmp_k, uint32_t *tmp_v, uint32_t *skeys, uint32_t *svals);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h);
-void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes);
+void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes,
+                  int max_units, int max_short_units);
 void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd);
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds);

@@ -108,7 +108,7 @@ __device__ __forceinline__ void put_switch(W &wr, const Codes &cd, int cat, cons
 
 // item k of command q (see item_bits in enc_common.h: same bits, in stream order)
 template <class W>
-__device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb, const uint8_t *cmap, const uint8_t *lut, const Job &jb,
+__device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb, const uint16_t *cmap, const uint8_t *lut, const Job &jb,
                                            const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q, uint32_t k) {
   const Unit &u = su[unit_of(sg, p)];
   if (k == 0) {
@@ -139,7 +139,7 @@ __device__ __forceinline__ void write_item(W &wr, const Codes &cd, const Mb &mb,
 // Item k of command q when it carries no block switch (the common case): its bits and its
 // whole bit string (<= 15 + 24 + 24 bits), so the write pass ORs it without looking the codes up
 // again; an item with a switch returns false and is written by write_item.
-__device__ __forceinline__ bool item_packed(const Codes &cd, const Mb &mb, const uint8_t *cmap, const uint8_t *lut, const Job &jb,
+__device__ __forceinline__ bool item_packed(const Codes &cd, const Mb &mb, const uint16_t *cmap, const uint8_t *lut, const Job &jb,
                                             const Cmd &c, uint32_t p, const Seg &sg, const Unit *su, uint32_t q, uint32_t k,
                                             uint32_t &bits, uint64_t &val) {
   const Unit &u = su[unit_of(sg, p)];
@@ -202,7 +202,8 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   const int t = threadIdx.x;
   const Codes &cd = codes[sg.mb];
   const Mb &mb = mbs[sg.mb];
-  __shared__ uint8_t sh_lut[512], sh_cmap[kLitSlots];   // per-literal lookups from LDS
+  __shared__ uint8_t sh_lut[512];   // per-literal lookups from LDS
+  __shared__ uint16_t sh_cmap[kLitSlots];
   for (int i = t; i < 512; i += kBlock) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   for (int i = t; i < kLitSlots; i += kBlock) sh_cmap[i] = mb.lit_cmap[i];
   __syncthreads();

@@ -285,8 +285,8 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
   for (int i = t; i < 512; i += NT) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
-  for (int i = t; i < kMaxBT * 704; i += NT) sh_c[i] = 0;
-  for (int i = t; i < kMaxBT * kDistCtx * 128; i += NT) sh_d[i] = 0;
+  for (int i = t; i < (int)mb.nbt[1] * 704; i += NT) sh_c[i] = 0;
+  for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT) sh_d[i] = 0;
   __syncthreads();
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
@@ -299,9 +299,9 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
   }
   const uint32_t m = sg.mb;
   __syncthreads();
-  for (int i = t; i < kMaxBT * 704; i += NT)
+  for (int i = t; i < (int)mb.nbt[1] * 704; i += NT)
     if (sh_c[i]) atomicAdd(&hc[(size_t)m * kMaxBT * 704 + i], sh_c[i]);
-  for (int i = t; i < kMaxBT * kDistCtx * 128; i += NT)
+  for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT)
     if (sh_d[i]) atomicAdd(&hd[(size_t)m * kMaxBT * kDistCtx * 128 + i], sh_d[i]);
   __syncthreads();
   uint32_t present = 0;   // literal block types used by this segment
@@ -385,7 +385,7 @@ __device__ __forceinline__ int tri(int a, int b) { return a * (2 * kLitCtx - a -
 __device__ unsigned long long g_clu_prof[8];
 #endif
 __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd,
-                                                         int lit_cap) {
+                                                         int lit_cap, int kl, int kd) {
   constexpr int kMaxH = kLitCtx;
   // rows padded by one word: lanes reading one symbol of 64 different histograms hit 64 banks
   __shared__ uint32_t h[kMaxH][257];
@@ -396,7 +396,8 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
   __shared__ float red_v[kCluT / 64];
   __shared__ int red_i[kCluT / 64];
   __shared__ int sh_best, sh_alive;
-  const int m = blockIdx.x / (2 * kMaxBT), kind = (blockIdx.x / kMaxBT) & 1, ty = blockIdx.x % kMaxBT;
+  // block per (metablock, literal type < kl | distance type < kd)
+  const int nr = kl + kd, m = blockIdx.x / nr, r = blockIdx.x % nr, kind = r < kl ? 0 : 1, ty = kind == 0 ? r : r - kl;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
@@ -593,7 +594,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
       if (alive[label[q]] && rep_id[label[q]] < 0) rep_id[label[q]] = k++;
     for (int q = 0; q < nh; q++) {
       const int c = alive[label[q]] ? rep_id[label[q]] : 0;
-      if (kind == 0) mb.lit_cmap[ty * kLitCtx + q] = (uint8_t)(ty * kLitCtx + c);
+      if (kind == 0) mb.lit_cmap[ty * kLitCtx + q] = (uint16_t)(ty * kLitCtx + c);
       else mb.dist_cmap[ty * kDistCtx + q] = (uint8_t)(ty * kDistCtx + c);
     }
     if (k == 0) k = 1;
@@ -961,7 +962,6 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
 // Block (one wave) per (metablock, code slot): literal (block type, cluster), command (block
 // type), distance (block type, cluster); slots beyond the metablock's counts are empty.
 // blocks per metablock: the used codes only (literal codes are at most kMaxLitTrees in all)
-constexpr int kHuffBlocks = kMaxLitTrees + kMaxBT + kMaxBT * kDistCtx;
 #ifdef MIB_PROF   // timing experiment: trees, count-limit attempts, cycles in rank sort / tree / store, per block
 __device__ unsigned long long g_huff_prof[8];
 #define HPT() __builtin_amdgcn_s_memtime()
@@ -975,7 +975,7 @@ __device__ unsigned long long g_huff_prof[8];
 template <int AMAX>
 __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                                                      const uint32_t *hc, const uint32_t *hd, Codes *codes,
-                                                     uint8_t *trees, int r0, int nr) {
+                                                     uint8_t *trees, int nl, int kc, int nr) {
   __shared__ uint32_t h[AMAX];
   __shared__ int16_t nzs[AMAX];
   __shared__ int16_t sorted[AMAX];
@@ -986,7 +986,7 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ uint8_t buf[kTreeBytes];
   __shared__ int sh_ok;
   __shared__ TreeScratch ts;
-  const int m = blockIdx.x / nr, r = r0 + (int)(blockIdx.x % nr);
+  const int m = blockIdx.x / nr, r = (int)(blockIdx.x % nr);
   const int lane = threadIdx.x;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
@@ -999,21 +999,21 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   };
   // the unused slots' sizes are zeroed by the blocks in turn (each slot by one block)
   if (lane == 0)
-    for (int q = r; q < kTreeSlots; q += kHuffBlocks)
+    for (int q = r; q < kTreeSlots; q += nr)
       if (!slot_used(q)) mb.tree_bits[q] = 0;
   // block r builds the r-th used code: literal codes first (at most kMaxLitTrees of them,
   // numbered per block type), then the command codes, then the distance codes
   int t = -1;
-  if (r < kMaxLitTrees) {
+  if (r < nl) {
     int acc = 0;
     for (int ty = 0; ty < (int)mb.nbt[0] && t < 0; ty++) {
       if (r < acc + (int)mb.nlit_t[ty]) t = ty * kLitCtx + (r - acc);
       acc += (int)mb.nlit_t[ty];
     }
-  } else if (r < kMaxLitTrees + kMaxBT) {
-    t = kCmdSlot + (r - kMaxLitTrees);
+  } else if (r < nl + kc) {
+    t = kCmdSlot + (r - nl);
   } else {
-    t = kDistSlot + (r - kMaxLitTrees - kMaxBT);
+    t = kDistSlot + (r - nl - kc);
   }
   if (t < 0 || !slot_used(t)) return;
   const bool lit = t < kCmdSlot, dist = t >= kDistSlot;
@@ -1174,23 +1174,223 @@ __device__ unsigned long long g_split_prof[8];
 #else
 #define SPMARK(k) do {} while (0)
 #endif
-template <int NT>
+// Exclusive scans of two per-unit series fa(i), fb(i) over i < n into ea / eb (eb may be null),
+// a thread per run of ceil(n / NT) units, the runs' sums scanned in LDS (wa, wb: NT each);
+// every thread gets the totals.  Ends with a barrier.
+template <int NT, class FA, class FB>
+__device__ void block_scan2(int t, int n, FA fa, FB fb, uint32_t *ea, uint32_t *eb, uint32_t *wa, uint32_t *wb, uint32_t &ta,
+                            uint32_t &tb) {
+  const int per = (n + NT - 1) / NT, lo = min(n, t * per), hi = min(n, lo + per);
+  uint32_t sa = 0, sb = 0;
+  for (int i = lo; i < hi; i++) {
+    sa += fa(i);
+    sb += fb(i);
+  }
+  wa[t] = sa;
+  wb[t] = sb;
+  __syncthreads();
+  for (int o = 1; o < NT; o <<= 1) {
+    const uint32_t va = t >= o ? wa[t - o] : 0u, vb = t >= o ? wb[t - o] : 0u;
+    __syncthreads();
+    wa[t] += va;
+    wb[t] += vb;
+    __syncthreads();
+  }
+  uint32_t xa = wa[t] - sa, xb = wb[t] - sb;
+  for (int i = lo; i < hi; i++) {
+    ea[i] = xa;
+    xa += fa(i);
+    if (eb) eb[i] = xb;
+    xb += fb(i);
+  }
+  ta = wa[NT - 1];
+  tb = wb[NT - 1];
+  __syncthreads();
+}
+
+// The split's shortest path with S states (S = 4 when the split seeds at most four types:
+// the same sums as ever; else kMaxBT).  Scratch (in th): the
+// chunks' S x S matrices, their start costs, exit maps (3 bits per state) and handed states.
+// ucost rows are S wide.
+template <int S>
+__device__ void split_path(int t, int nu, const uint32_t *ns, const float *ucost, uint8_t *asg, uint16_t *bp,
+                           uint32_t *scratch, float sw_cost) {
+  constexpr int kCh = S <= 4 ? kPathChunks : kPathChunks / 2;   // (the scratch fits th either way)
+  static_assert(kCh * (S * S + S) * 4 + kCh * 7 <= S * 704 * 4, "path scratch fits th");
+  const int CL = max(kPathCL, (nu + kCh - 1) / kCh);
+  const int nch = (nu + CL - 1) / CL;
+  float *Tm = reinterpret_cast<float *>(scratch);   // [nch][S * S]: (q, p) -> cost
+  float *Sd = Tm + kCh * S * S;                     // [nch][S]: costs at the chunk start
+  uint32_t *Xm = reinterpret_cast<uint32_t *>(Sd + kCh * S);   // exit maps
+  uint8_t *Pc = reinterpret_cast<uint8_t *>(Xm + kCh), *Qp = Pc + kCh, *Ln = Qp + kCh;
+  constexpr float kBig = 1e30f;
+  if (t < nch) {   // chunk transfer matrix
+    float T[S * S];
+#pragma unroll
+    for (int e = 0; e < S * S; e++) T[e] = (e / S) == (e % S) ? 0.f : kBig;
+    const int i1 = min(nu, (t + 1) * CL);
+    for (int i = t * CL; i < i1; i++) {
+      if (!ns[i]) continue;
+      float col[S];
+#pragma unroll
+      for (int p = 0; p < S; p++) {
+        float v = T[p];
+#pragma unroll
+        for (int q = 1; q < S; q++) v = fminf(v, T[S * q + p]);
+        col[p] = v + sw_cost;
+      }
+#pragma unroll
+      for (int q = 0; q < S; q++) {
+        const float u = ucost[i * S + q];
+#pragma unroll
+        for (int p = 0; p < S; p++) T[S * q + p] = fminf(T[S * q + p], col[p]) + u;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < S * S; e++) Tm[t * S * S + e] = T[e];
+  }
+  __syncthreads();
+  if (t == 0) {   // the costs at every chunk start
+    float dp[S];
+#pragma unroll
+    for (int q = 0; q < S; q++) dp[q] = 0.f;
+    for (int c = 0; c < nch; c++) {
+      float nd[S];
+#pragma unroll
+      for (int q = 0; q < S; q++) {
+        Sd[c * S + q] = dp[q];
+        float v = kBig;
+#pragma unroll
+        for (int p = 0; p < S; p++) v = fminf(v, Tm[c * S * S + S * q + p] + dp[p]);
+        nd[q] = v;
+      }
+#pragma unroll
+      for (int q = 0; q < S; q++) dp[q] = nd[q];
+    }
+    int cur = 0;
+    for (int q = 1; q < S; q++)
+      if (dp[q] < dp[cur]) cur = q;
+    Pc[kCh - 1] = (uint8_t)cur;   // (handed to the last chunk below)
+  }
+  __syncthreads();
+  if (t < nch) {   // replay: the serial walk's switch bits, then the chunk's exit map
+    float dp[S];
+#pragma unroll
+    for (int q = 0; q < S; q++) dp[q] = Sd[t * S + q];
+    const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
+    for (int i = i0; i < i1; i++) {
+      if (!ns[i]) continue;
+      float best = 1e30f;
+      int bq = 0;
+#pragma unroll
+      for (int q = 0; q < S; q++)
+        if (dp[q] < best) {
+          best = dp[q];
+          bq = q;
+        }
+      uint32_t bb = 0;
+      float nd[S];
+#pragma unroll
+      for (int q = 0; q < S; q++) {
+        const float stay = dp[q], sw = best + sw_cost;
+        const bool sv = sw < stay;   // (never at the first unit: every cost is 0 there)
+        nd[q] = (sv ? sw : stay) + ucost[i * S + q];
+        if (sv) bb |= 1u << q;
+      }
+      bp[i] = (uint16_t)(bb | (uint32_t)(bq << 8));
+#pragma unroll
+      for (int q = 0; q < S; q++) dp[q] = nd[q];
+    }
+    uint32_t xm = 0;
+    for (int cin = 0; cin < S; cin++) {
+      int cur = cin;
+      for (int i = i1 - 1; i >= i0; i--)
+        if (ns[i] && (bp[i] >> cur & 1)) cur = bp[i] >> 8;
+      xm |= (uint32_t)cur << (3 * cin);
+    }
+    Xm[t] = xm;
+  }
+  __syncthreads();
+  if (t == 0) {   // the state handed into every chunk from the right
+    int cur = Pc[kCh - 1];
+    for (int c = nch - 1; c >= 0; c--) {
+      Pc[c] = (uint8_t)cur;
+      cur = (int)((Xm[c] >> (3 * cur)) & 7);
+    }
+  }
+  __syncthreads();
+  if (t < nch) {   // the chunk's assignment; its last non-empty unit's type
+    int cur = Pc[t], ln = -1;
+    const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
+    for (int i = i1 - 1; i >= i0; i--) {
+      if (!ns[i]) continue;
+      asg[i] = (uint8_t)cur;
+      if (ln < 0) ln = cur;
+      if (bp[i] >> cur & 1) cur = bp[i] >> 8;
+    }
+    Ln[t] = (uint8_t)(ln < 0 ? 0xFF : ln);
+  }
+  __syncthreads();
+  if (t == 0) {   // empty units follow their predecessor: the type handed into each chunk
+    int prev = asg[0];
+    for (int c = 0; c < nch; c++) {
+      Qp[c] = (uint8_t)prev;
+      if (Ln[c] != 0xFF) prev = Ln[c];
+    }
+  }
+  __syncthreads();
+  if (t < nch) {
+    int prev = Qp[t];
+    const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
+    for (int i = i0; i < i1; i++) {
+      if (!ns[i]) asg[i] = (uint8_t)prev;
+      prev = asg[i];
+    }
+  }
+}
+
+// The block types a split may seed per category (literal, command, distance): the split is
+// tried with K types; types the shortest path leaves unused drop out.  Literals take up to 8
+// (C4 0.36469 -> 0.36365 compressed, C3 0.45579 -> 0.45569, decode unchanged; r04ad / r04ae).  Commands and distances keep 4:
+// with 8 their prefix codes overflow the decoder's LDS table area (§7) and C4 decode goes from
+// 140 to 299 ms for 0.05 % of bytes.  (A/B: MIB_SPLIT_BT = "l,c,d", each 1..kMaxBT.)
+constexpr int kSplitBtLit = 8;
+__device__ __forceinline__ int nu_of(const Mb &mb) { return (int)mb.nseg * kSubPerSeg; }
+struct SplitK { int k[3]; };
+SplitK split_k() {
+  static const SplitK sk = [] {
+    SplitK k{{kSplitBtLit, 4, 4}};
+    if (const char *e = getenv("MIB_SPLIT_BT")) sscanf(e, "%d,%d,%d", &k.k[0], &k.k[1], &k.k[2]);
+    for (int c = 0; c < 3; c++) k.k[c] = std::min(kMaxBT, std::max(1, k.k[c]));
+    return k;
+  }();
+  return sk;
+}
+// S: the refinement's states (4, or kMaxBT): a launch per S, each taking the (metablock,
+// category) blocks whose K it covers (K <= 4: S = 4, the loops and LDS of four types)
+template <int NT, int S>
 __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h,
-                                                    Codes *codes) {
-  __shared__ uint32_t th[kMaxBT][704];
-  __shared__ float bc[kMaxBT][704];
-  __shared__ float ucost[kMaxUnits][kMaxBT];
-  __shared__ uint8_t asg[kMaxUnits], bp[kMaxUnits];
+                                                    Codes *codes, SplitK sk) {
+  __shared__ uint32_t th[S][704];
+  __shared__ float bc[S][704];
+  extern __shared__ float ucost[];   // [units][S] (launch_split sizes it for the largest metablock)
+  __shared__ uint8_t asg[kMaxUnits];
+  __shared__ uint16_t bp[kMaxUnits];   // switch bits per state | best state << 8
   __shared__ uint32_t ns[kMaxUnits];   // the units' symbol counts (the serial steps read them from LDS)
-  __shared__ uint32_t tot[kMaxBT];
+  __shared__ uint32_t tot[S];
   constexpr int kSplitT = NT;
   __shared__ float red[kSplitT];
+  __shared__ uint32_t scan_b[kSplitT];   // (block scans: red and this hold the threads' partial sums)
   __shared__ int sh_ne, sh_keep;
   const int m = blockIdx.x / 3, cat = blockIdx.x % 3;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
+  // (literals: the metablock's 24 codes -- the decoder's LDS budget -- serve more block types
+  // in a short metablock, more contexts per type in a long one)
+  const int K = cat == 0 && nu_of(mbs[m]) > kSplitWideUnits ? min(sk.k[0], 4) : sk.k[cat];
+  if ((K <= 4) != (S == 4)) return;   // (the other launch's block)
 #ifdef MIB_PROF
   uint64_t sp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sp0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1204,51 +1404,62 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   for (int i = t; i < nu; i += kSplitT) ns[i] = U[i].nsym[cat];
   __syncthreads();
   SPMARK(0);
-  // seed: the non-empty units in kMaxBT contiguous runs
-  if (t == 0) {
-    int ne = 0;
-    for (int i = 0; i < nu; i++) ne += ns[i] ? 1 : 0;
-    int r = 0;
-    for (int i = 0; i < nu; i++) {
-      asg[i] = (uint8_t)(ne ? (r * kMaxBT) / ne : 0);
-      if (ns[i]) r++;
-    }
-    sh_ne = ne;
+  // seed: the non-empty units in K contiguous runs (unit i: rank r among them, type r K / ne)
+  {
+    uint32_t *rk = &th[0][0];
+    uint32_t nne, unused;
+    block_scan2<NT>(t, nu, [&](int i) -> uint32_t { return ns[i] ? 1u : 0u; }, [&](int) -> uint32_t { return 0u; }, rk,
+                    static_cast<uint32_t *>(nullptr), reinterpret_cast<uint32_t *>(red), scan_b, nne, unused);
+    for (int i = t; i < nu; i += kSplitT) asg[i] = (uint8_t)(nne ? (rk[i] * (uint32_t)K) / nne : 0u);
+    if (t == 0) sh_ne = (int)nne;
+    __syncthreads();
   }
-  __syncthreads();
   SPMARK(1);
   const int ne = sh_ne;
   int keep = 0;
-  if (ne >= 2 * kMaxBT) {
+  // the refinement: S-wide loops and unit-cost rows
+  auto refine = [&]() -> int {
     float base_cost = 0.f;
     for (int it = 0; it <= kSplitIters; it++) {
       // type histograms (it == kSplitIters: of the final assignment); one type = all units.
       // NT / 256 unit ranges in parallel (256 symbols each), summed with LDS atomics
       for (int x = t; x < A; x += kSplitT)
-        for (int q = 0; q < kMaxBT; q++) th[q][x] = 0;
+        for (int q = 0; q < S; q++) th[q][x] = 0;
       __syncthreads();
       {
         const int qd = t >> 8, i0 = (nu * qd) / (kSplitT / 256), i1 = (nu * (qd + 1)) / (kSplitT / 256);
         for (int x = t & 255; x < A; x += 256) {
-          uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-#pragma unroll 8
-          for (int i = i0; i < i1; i++) {   // (unrolled: eight unit rows in flight, not one)
+          uint32_t s[S];
+#pragma unroll
+          for (int q = 0; q < S; q++) s[q] = 0;
+          // eight unit rows a batch: the loads issued together, then summed (a load-use pair per
+          // row left one HBM/L2 round trip per row in flight)
+          int i = i0;
+          for (; i + 8 <= i1; i += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) v[j] = H[(size_t)(i + j) * kSubHist + x];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+              const int a = asg[i + j];
+#pragma unroll
+              for (int q = 0; q < S; q++) s[q] += a == q ? v[j] : 0u;
+            }
+          }
+          for (; i < i1; i++) {
             const uint32_t v = H[(size_t)i * kSubHist + x];
             const int a = asg[i];
-            s0 += a == 0 ? v : 0u;
-            s1 += a == 1 ? v : 0u;
-            s2 += a == 2 ? v : 0u;
-            s3 += a == 3 ? v : 0u;
+#pragma unroll
+            for (int q = 0; q < S; q++) s[q] += a == q ? v : 0u;
           }
-          if (s0) atomicAdd(&th[0][x], s0);
-          if (s1) atomicAdd(&th[1][x], s1);
-          if (s2) atomicAdd(&th[2][x], s2);
-          if (s3) atomicAdd(&th[3][x], s3);
+#pragma unroll
+          for (int q = 0; q < S; q++)
+            if (s[q]) atomicAdd(&th[q][x], s[q]);
         }
       }
       __syncthreads();
       SPMARK(2);
-      if (t < kMaxBT) {
+      if (t < S) {
         uint32_t s = 0;
         for (int x = 0; x < A; x++) s += th[t][x];
         tot[t] = s;
@@ -1256,11 +1467,13 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       __syncthreads();
       if (it == 0) {   // the one-type baseline: entropy of the merged histogram + one code's header
         float part = 0.f;
-        const uint32_t all = tot[0] + tot[1] + tot[2] + tot[3];
+        uint32_t all = 0;
+        for (int q = 0; q < S; q++) all += tot[q];
         const float la = __log2f((float)all);
         int nz = 0;
         for (int x = t; t < 256 && x < A; x += 256) {
-          const uint32_t c = th[0][x] + th[1][x] + th[2][x] + th[3][x];
+          uint32_t c = 0;
+          for (int q = 0; q < S; q++) c += th[q][x];
           if (c) {
             part += (float)c * (la - __log2f((float)c));
             nz++;
@@ -1276,36 +1489,29 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
         __syncthreads();
       }
       for (int x = t; x < A; x += kSplitT)
-        for (int q = 0; q < kMaxBT; q++) bc[q][x] = tot[q] ? sym_bits(th[q][x], __log2f((float)tot[q])) : 1e9f;
+        for (int q = 0; q < S; q++) bc[q][x] = tot[q] ? sym_bits(th[q][x], __log2f((float)tot[q])) : 1e9f;
       __syncthreads();
       SPMARK(3);
       if (it == kSplitIters) break;
       // every unit's bits under every type: a wave per unit, lanes over the symbols
       for (int i = t >> 6; i < nu; i += kSplitT / 64) {
-        float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+        float c[S];
+#pragma unroll
+        for (int q = 0; q < S; q++) c[q] = 0.f;
         if (ns[i]) {
           const uint32_t *h = H + (size_t)i * kSubHist;
 #pragma unroll 4
           for (int x = t & 63; x < A; x += 64) {
             const float v = (float)h[x];
-            c0 += v * bc[0][x];
-            c1 += v * bc[1][x];
-            c2 += v * bc[2][x];
-            c3 += v * bc[3][x];
+#pragma unroll
+            for (int q = 0; q < S; q++) c[q] += v * bc[q][x];
           }
-          for (int o = 32; o; o >>= 1) {
-            c0 += __shfl_xor(c0, o);
-            c1 += __shfl_xor(c1, o);
-            c2 += __shfl_xor(c2, o);
-            c3 += __shfl_xor(c3, o);
-          }
+#pragma unroll
+          for (int q = 0; q < S; q++)
+            for (int o = 32; o; o >>= 1) c[q] += __shfl_xor(c[q], o);
         }
-        if ((t & 63) == 0) {
-          ucost[i][0] = c0;
-          ucost[i][1] = c1;
-          ucost[i][2] = c2;
-          ucost[i][3] = c3;
-        }
+        if ((t & 63) == 0)
+          for (int q = 0; q < S; q++) ucost[i * S + q] = q < K ? c[q] : 1e30f;   // (types past K: empty)
       }
       __syncthreads();
       SPMARK(4);
@@ -1318,131 +1524,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       // (the switch bits), and the backtrack runs per chunk from the state handed in from
       // the right (one thread chains the chunks' exit maps).  Scratch: th, which the next
       // iteration recomputes.
-      {
-        const int CL = max(kPathCL, (nu + kPathChunks - 1) / kPathChunks);
-        const int nch = (nu + CL - 1) / CL;
-        float *Tm = reinterpret_cast<float *>(&th[0][0]);   // [nch][16]: (q, p) -> cost
-        float *Sd = Tm + kPathChunks * 16;                     // [nch][4]: costs at the chunk start
-        uint8_t *Xm = reinterpret_cast<uint8_t *>(Sd + kPathChunks * 4);   // exit maps
-        uint8_t *Pc = Xm + kPathChunks, *Qp = Pc + kPathChunks, *Ln = Qp + kPathChunks;
-        constexpr float kBig = 1e30f;
-        if (t < nch) {   // chunk transfer matrix
-          float T[16];
-#pragma unroll
-          for (int e = 0; e < 16; e++) T[e] = (e >> 2) == (e & 3) ? 0.f : kBig;
-          const int i1 = min(nu, (t + 1) * CL);
-          for (int i = t * CL; i < i1; i++) {
-            if (!ns[i]) continue;
-            float col[kMaxBT];
-#pragma unroll
-            for (int p = 0; p < kMaxBT; p++) col[p] = fminf(fminf(T[p], T[4 + p]), fminf(T[8 + p], T[12 + p])) + sw_cost;
-#pragma unroll
-            for (int q = 0; q < kMaxBT; q++) {
-              const float u = ucost[i][q];
-#pragma unroll
-              for (int p = 0; p < kMaxBT; p++) T[4 * q + p] = fminf(T[4 * q + p], col[p]) + u;
-            }
-          }
-#pragma unroll
-          for (int e = 0; e < 16; e++) Tm[t * 16 + e] = T[e];
-        }
-        __syncthreads();
-        if (t == 0) {   // the costs at every chunk start
-          float dp[kMaxBT] = {0.f, 0.f, 0.f, 0.f};
-          for (int c = 0; c < nch; c++) {
-            float nd[kMaxBT];
-#pragma unroll
-            for (int q = 0; q < kMaxBT; q++) {
-              Sd[c * 4 + q] = dp[q];
-              float v = kBig;
-#pragma unroll
-              for (int p = 0; p < kMaxBT; p++) v = fminf(v, Tm[c * 16 + 4 * q + p] + dp[p]);
-              nd[q] = v;
-            }
-#pragma unroll
-            for (int q = 0; q < kMaxBT; q++) dp[q] = nd[q];
-          }
-          int cur = 0;
-          for (int q = 1; q < kMaxBT; q++)
-            if (dp[q] < dp[cur]) cur = q;
-          Pc[kPathChunks - 1] = (uint8_t)cur;   // (handed to the last chunk below)
-        }
-        __syncthreads();
-        if (t < nch) {   // replay: the serial walk's switch bits, then the chunk's exit map
-          float dp[kMaxBT];
-#pragma unroll
-          for (int q = 0; q < kMaxBT; q++) dp[q] = Sd[t * 4 + q];
-          const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
-          for (int i = i0; i < i1; i++) {
-            if (!ns[i]) continue;
-            float best = 1e30f;
-            int bq = 0;
-#pragma unroll
-            for (int q = 0; q < kMaxBT; q++)
-              if (dp[q] < best) {
-                best = dp[q];
-                bq = q;
-              }
-            uint8_t bb = 0;
-            float nd[kMaxBT];
-#pragma unroll
-            for (int q = 0; q < kMaxBT; q++) {
-              const float stay = dp[q], sw = best + sw_cost;
-              const bool sv = sw < stay;   // (never at the first unit: every cost is 0 there)
-              nd[q] = (sv ? sw : stay) + ucost[i][q];
-              if (sv) bb |= (uint8_t)(1 << q);
-            }
-            bp[i] = (uint8_t)(bb | (bq << 4));
-#pragma unroll
-            for (int q = 0; q < kMaxBT; q++) dp[q] = nd[q];
-          }
-          uint32_t xm = 0;
-          for (int cin = 0; cin < kMaxBT; cin++) {
-            int cur = cin;
-            for (int i = i1 - 1; i >= i0; i--)
-              if (ns[i] && (bp[i] >> cur & 1)) cur = bp[i] >> 4;
-            xm |= (uint32_t)cur << (2 * cin);
-          }
-          Xm[t] = (uint8_t)xm;
-        }
-        __syncthreads();
-        if (t == 0) {   // the state handed into every chunk from the right
-          int cur = Pc[kPathChunks - 1];
-          for (int c = nch - 1; c >= 0; c--) {
-            Pc[c] = (uint8_t)cur;
-            cur = (Xm[c] >> (2 * cur)) & 3;
-          }
-        }
-        __syncthreads();
-        if (t < nch) {   // the chunk's assignment; its last non-empty unit's type
-          int cur = Pc[t], ln = -1;
-          const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
-          for (int i = i1 - 1; i >= i0; i--) {
-            if (!ns[i]) continue;
-            asg[i] = (uint8_t)cur;
-            if (ln < 0) ln = cur;
-            if (bp[i] >> cur & 1) cur = bp[i] >> 4;
-          }
-          Ln[t] = (uint8_t)(ln < 0 ? 0xFF : ln);
-        }
-        __syncthreads();
-        if (t == 0) {   // empty units follow their predecessor: the type handed into each chunk
-          int prev = asg[0];
-          for (int c = 0; c < nch; c++) {
-            Qp[c] = (uint8_t)prev;
-            if (Ln[c] != 0xFF) prev = Ln[c];
-          }
-        }
-        __syncthreads();
-        if (t < nch) {
-          int prev = Qp[t];
-          const int i0 = t * CL, i1 = min(nu, (t + 1) * CL);
-          for (int i = i0; i < i1; i++) {
-            if (!ns[i]) asg[i] = (uint8_t)prev;
-            prev = asg[i];
-          }
-        }
-      }
+      split_path<S>(t, nu, ns, ucost, asg, bp, &th[0][0], sw_cost);
       __syncthreads();
       SPMARK(5);
     }
@@ -1455,7 +1537,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       for (int x = t & 63; x < A; x += 64) part += (float)h[x] * bc[q][x];
     }
     for (int x = t; t < 256 && x < A; x += 256)
-      for (int q = 0; q < kMaxBT; q++) part += th[q][x] ? 3.5f : 0.f;
+      for (int q = 0; q < S; q++) part += th[q][x] ? 3.5f : 0.f;
     red[t] = part;
     __syncthreads();
     for (int o = kSplitT / 2; o; o >>= 1) {
@@ -1469,14 +1551,15 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
         if (prev >= 0 && asg[i] != prev) nsw++;
         prev = asg[i];
       }
-      for (int q = 0; q < kMaxBT; q++) used += tot[q] ? 1 : 0;
+      for (int q = 0; q < S; q++) used += tot[q] ? 1 : 0;
       const float split_cost = red[0] + 40.f * (float)used + sw_cost * (float)nsw + 60.f;
       sh_keep = (used > 1 && split_cost < base_cost) ? 1 : 0;
     }
     __syncthreads();
     SPMARK(6);
-    keep = sh_keep;
-  }
+    return sh_keep;
+  };
+  if (K > 1 && ne >= 2 * K) keep = refine();
 #ifdef MIB_PROF
   const uint64_t tail0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1491,67 +1574,89 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
     }
     return;
   }
-  // The serial layout works in LDS (the unit costs and switch bits are dead here): per unit
-  // its type, the count of the block a switch there opens, the switch's code; the units are
-  // then written by every thread.  (Writing each unit's fields to HBM inside the serial loop
-  // kept thread 0 waiting on its store queue, ~800 cycles a unit.)
-  uint32_t *lsw = reinterpret_cast<uint32_t *>(&ucost[0][0]);
-  uint8_t *lcode = reinterpret_cast<uint8_t *>(lsw + kMaxUnits);
-  uint8_t *lty = bp;
-  if (t == 0) {
-  // renumber by first use
-  // (packed 8 bits per type, 0xFF: unused -- an indexed private array lived in scratch memory,
-  // one round trip per unit of this serial loop)
-  uint32_t mapp = 0xFFFFFFFFu;
+  // The layout works in LDS (the unit costs, switch bits and histograms are dead here): per
+  // unit its type, the count of the block a switch there opens, the switch's code; the units
+  // are then written by every thread.  In parallel (a serial walk by one thread was ~800
+  // cycles a unit, 20 % of the kernel on 16 MiB metablocks): types renumbered by first use;
+  // a switch wherever a non-empty unit's type differs from the one before it (an empty unit
+  // carries its predecessor's type); scans give each switch its rank and each unit the
+  // symbols before it, so block b's count and its code (from the two blocks before it,
+  // RFC 7932 section 6) need no walk.
+  uint32_t *lsw = reinterpret_cast<uint32_t *>(ucost);                      // [nu]
+  uint8_t *lcode = reinterpret_cast<uint8_t *>(lsw + nu);                   // [nu]
+  uint32_t *swu = reinterpret_cast<uint32_t *>(lcode + ((nu + 3) & ~3));    // [nu]: unit of switch k
+  uint8_t *btype = reinterpret_cast<uint8_t *>(swu + nu);                   // [nu + 1]: type of block b
+  static_assert(kSubPerSeg >= 4, "10 bytes a unit + 4 fit the unit costs' 16");
+  uint32_t *cum = &th[0][0];                                                // [nu + 1]: symbols before unit i
+  uint32_t *swr = reinterpret_cast<uint32_t *>(&bc[0][0]);                  // [nu]: switches before unit i
+  static_assert(4 * 704 >= kMaxUnits + 1, "th / bc hold a value per unit");
+  uint8_t *lty = reinterpret_cast<uint8_t *>(bp);
+  __shared__ int sh_first[kMaxBT + 1];   // first non-empty unit of each type; [kMaxBT]: of any
+  __shared__ uint8_t sh_map[kMaxBT];
+  __shared__ uint32_t sh_hcode[kMaxBT + 2], sh_hcount[26], sh_nsw;
+  if (t <= kMaxBT) sh_first[t] = 0x7FFFFFFF;
+  if (t < kMaxBT + 2) sh_hcode[t] = 0;
+  if (t < 26) sh_hcount[t] = 0;
+  __syncthreads();
+  for (int i = t; i < nu; i += kSplitT)
+    if (ns[i]) {
+      atomicMin(&sh_first[asg[i]], i);
+      atomicMin(&sh_first[kMaxBT], i);
+    }
+  __syncthreads();
+  if (t == 0)
+    for (int q = 0; q < S; q++) {
+      int r = 0;
+      for (int p = 0; p < S; p++) r += sh_first[p] < sh_first[q] ? 1 : 0;
+      sh_map[q] = (uint8_t)r;
+    }
+  __syncthreads();
   int nt = 0;
-  for (int i = 0; i < nu; i++) {
-    if (!ns[i]) continue;
-    const uint32_t sh = 8u * asg[i];
-    if (((mapp >> sh) & 0xFF) == 0xFF) {
-      mapp = (mapp & ~(0xFFu << sh)) | ((uint32_t)nt << sh);
-      nt++;
-    }
-  }
-  // lay out the switches
-  uint32_t hcode[kMaxBT + 2] = {0, 0, 0, 0, 0, 0}, hcount[26];
-  for (int q = 0; q < 26; q++) hcount[q] = 0;
-  int cur = 0, last = 0, second = 1, open = -1;   // open: unit of the current block's switch (-1: the header's)
-  uint32_t count = 0;
-  bool started = false;
-  for (int i = 0; i < nu; i++) {
+  for (int q = 0; q < S; q++) nt += sh_first[q] != 0x7FFFFFFF ? 1 : 0;
+  const int fne = sh_first[kMaxBT];
+  auto is_sw = [&](int i) -> uint32_t { return (ns[i] && i > fne && asg[i] != asg[i - 1]) ? 1u : 0u; };
+  for (int i = t; i < nu; i += kSplitT) {
+    lty[i] = (uint8_t)(i < fne ? 0 : sh_map[asg[i]]);
     lsw[i] = 0;
-    const uint32_t nsy = ns[i];
-    if (!nsy) {
-      lty[i] = (uint8_t)cur;
-      continue;
-    }
-    const int ty = (int)((mapp >> (8u * asg[i])) & 0xFF);
-    if (started && ty != cur) {
-      if (open < 0) mb.first_count[cat] = count;
-      else lsw[open] = count;
-      hcount[block_count_code(count)]++;
-      const int code = ty == second ? 0 : ty == (last + 1) % nt ? 1 : ty + 2;
-      lcode[i] = (uint8_t)code;
-      hcode[code]++;
-      second = last;
-      last = ty;
-      cur = ty;
-      open = i;
-      count = 0;
-    }
-    started = true;
-    lty[i] = (uint8_t)ty;
-    count += nsy;
   }
-  if (open < 0) mb.first_count[cat] = count;
-  else lsw[open] = count;
-  hcount[block_count_code(count)]++;
-  mb.nbt[cat] = (uint32_t)nt;
-  Codes &cd = codes[m];
-  serial_depths(hcode, nt + 2, 15, cd.btd[cat]);
-  depths_to_codes(cd.btd[cat], nt + 2, cd.btc[cat]);
-  serial_depths(hcount, 26, 15, cd.bcd[cat]);
-  depths_to_codes(cd.bcd[cat], 26, cd.bcc[cat]);
+  uint32_t nsw, nsym;
+  block_scan2<NT>(t, nu, is_sw, [&](int i) -> uint32_t { return ns[i]; }, swr, cum, reinterpret_cast<uint32_t *>(red),
+                  scan_b, nsw, nsym);
+  if (t == 0) {
+    cum[nu] = nsym;
+    btype[0] = 0;
+  }
+  for (int i = t; i < nu; i += kSplitT)
+    if (is_sw(i)) {
+      swu[swr[i]] = (uint32_t)i;
+      btype[swr[i] + 1] = lty[i];
+    }
+  __syncthreads();
+  for (int bl = t; bl <= (int)nsw; bl += kSplitT) {   // block bl: from switch bl - 1 (unit 0 for bl = 0) to the next
+    const uint32_t st = bl == 0 ? 0u : swu[bl - 1], en = bl < (int)nsw ? swu[bl] : (uint32_t)nu;
+    const uint32_t count = cum[en] - cum[st];
+    atomicAdd(&sh_hcount[block_count_code(count)], 1u);
+    if (bl == 0) {
+      mb.first_count[cat] = count;
+    } else {
+      const int ty = btype[bl], last = btype[bl - 1], second = bl >= 2 ? btype[bl - 2] : 1;
+      const int code = ty == second ? 0 : ty == (last + 1) % nt ? 1 : ty + 2;
+      lsw[st] = count;
+      lcode[st] = (uint8_t)code;
+      atomicAdd(&sh_hcode[code], 1u);
+    }
+  }
+  __syncthreads();
+  if (t == 0) {
+    uint32_t hcode[kMaxBT + 2], hcount[26];
+    for (int q = 0; q < kMaxBT + 2; q++) hcode[q] = sh_hcode[q];
+    for (int q = 0; q < 26; q++) hcount[q] = sh_hcount[q];
+    mb.nbt[cat] = (uint32_t)nt;
+    Codes &cd = codes[m];
+    serial_depths(hcode, nt + 2, 15, cd.btd[cat]);
+    depths_to_codes(cd.btd[cat], nt + 2, cd.btc[cat]);
+    serial_depths(hcount, 26, 15, cd.bcd[cat]);
+    depths_to_codes(cd.bcd[cat], 26, cd.bcc[cat]);
   }
   __syncthreads();
   for (int i = t; i < nu; i += kSplitT) {
@@ -1731,7 +1836,8 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
   const int t = threadIdx.x;
   const Mb &mb = mbs[sg.mb];
   const Codes &cd = codes[sg.mb];
-  __shared__ uint8_t sh_lut[512], sh_cmap[kLitSlots];   // per-literal lookups from LDS
+  __shared__ uint8_t sh_lut[512];   // per-literal lookups from LDS
+  __shared__ uint16_t sh_cmap[kLitSlots];
   for (int i = t; i < 512; i += NT) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   for (int i = t; i < kLitSlots; i += NT) sh_cmap[i] = mb.lit_cmap[i];
   __syncthreads();
@@ -1825,11 +1931,33 @@ void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mb
   else
     hipLaunchKernelGGL(codes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
 }
-void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes) {
-  if (nmbs * 3 <= 256)
-    hipLaunchKernelGGL(split_kernel<1024>, dim3(nmbs * 3), dim3(1024), 0, st, jobs, mbs, nmbs, units, unit_h, codes);
-  else
-    hipLaunchKernelGGL(split_kernel<256>, dim3(nmbs * 3), dim3(256), 0, st, jobs, mbs, nmbs, units, unit_h, codes);
+void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes,
+                  int max_units, int max_short_units) {
+  const SplitK sk = split_k();
+  // a launch per state count: S = 4 for the blocks seeding at most four types, S = kMaxBT for
+  // the rest (if any: literals of the metablocks of up to kSplitWideUnits units)
+  const bool wide_short = std::max(sk.k[0], std::max(sk.k[1], sk.k[2])) > 4;
+  const bool wide_long = std::max(std::min(sk.k[0], 4), std::max(sk.k[1], sk.k[2])) > 4;
+  const bool narrow = std::min(sk.k[0], std::min(sk.k[1], sk.k[2])) <= 4 || max_units > kSplitWideUnits;
+  const size_t lds4 = (size_t)std::max(1, std::min(max_units, kMaxUnits)) * 4 * sizeof(float);
+  const size_t lds8 = (size_t)std::max(1, std::min(wide_long ? max_units : max_short_units, kMaxUnits)) * kMaxBT * sizeof(float);
+  static const bool attr = [] {   // (dynamic LDS past 64 KiB: 16 MiB metablocks)
+    hipFuncSetAttribute((const void *)split_kernel<1024, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxUnits * 4 * 4);
+    hipFuncSetAttribute((const void *)split_kernel<256, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxUnits * 4 * 4);
+    hipFuncSetAttribute((const void *)split_kernel<1024, kMaxBT>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxUnits * kMaxBT * 4);
+    hipFuncSetAttribute((const void *)split_kernel<256, kMaxBT>, hipFuncAttributeMaxDynamicSharedMemorySize, kMaxUnits * kMaxBT * 4);
+    return true;
+  }();
+  (void)attr;
+  const bool few = nmbs * 3 <= 256;
+  if (narrow) {
+    if (few) hipLaunchKernelGGL((split_kernel<1024, 4>), dim3(nmbs * 3), dim3(1024), lds4, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
+    else hipLaunchKernelGGL((split_kernel<256, 4>), dim3(nmbs * 3), dim3(256), lds4, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
+  }
+  if (wide_short || wide_long) {
+    if (few) hipLaunchKernelGGL((split_kernel<1024, kMaxBT>), dim3(nmbs * 3), dim3(1024), lds8, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
+    else hipLaunchKernelGGL((split_kernel<256, kMaxBT>), dim3(nmbs * 3), dim3(256), lds8, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
+  }
 }
 void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
@@ -1858,17 +1986,26 @@ void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
 // C4 never needs more than 24.  MIB_LIT_TREES overrides (1..64; 1: one code per block type,
 // context-free literals).
 constexpr int kLitTreeCap = 24;
-void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
+int lit_tree_cap() {
   static const int cap = getenv("MIB_LIT_TREES") ? std::min(kMaxLitTrees, std::max(1, atoi(getenv("MIB_LIT_TREES")))) : kLitTreeCap;
-  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * 2 * kMaxBT), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, cap);
+  return cap;
+}
+void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
+  const SplitK sk = split_k();
+  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * (sk.k[0] + sk.k[2])), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, lit_tree_cap(),
+                     sk.k[0], sk.k[2]);
 }
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
   // one launch for every slot (two launches by alphabet size, the literal one with half the LDS,
   // were measured: C4 6.0 -> 5.5 ms but C3 8.9 -> 10.2 -- the command / distance blocks, the
   // longest, then ran as a tail of their own)
-  hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * kHuffBlocks), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, 0,
-                     kHuffBlocks);
+  // blocks per metablock: the literal codes (at most the cap, or one per literal type), one per
+  // command type, the distance (type, cluster) slots
+  const SplitK sk = split_k();
+  const int nl = std::max(lit_tree_cap(), sk.k[0]), nr = nl + sk.k[1] + sk.k[2] * kDistCtx;
+  hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * nr), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, nl, sk.k[1],
+                     nr);
   hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,

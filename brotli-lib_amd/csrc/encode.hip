@@ -393,6 +393,12 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   if (pos_total >= (1ull << 31)) return MIB_E_INVALID_ARG;
   const uint32_t total = (uint32_t)pos_total;
   const int nsegs = (int)segs.size(), nmbs = (int)mbs.size();
+  int max_mb_units = 1, max_short_units = 1;   // (the split kernel's LDS: unit costs of the largest metablock)
+  for (const Mb &mb : mbs) {
+    const int nu = (int)mb.nseg * kSubPerSeg;
+    max_mb_units = std::max(max_mb_units, nu);
+    if (nu <= kSplitWideUnits) max_short_units = std::max(max_short_units, nu);
+  }
   const size_t nm1 = std::max<size_t>(1, mbs.size()), ns1 = std::max<size_t>(1, segs.size());
 
   const size_t sort_tmp = sort_ws_bytes(total);
@@ -524,7 +530,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_dist_ring(st, d_jobs, (int)k, d_segs, cmds);
     tm.stop();
     tm.start("block_split");
-    launch_split(st, d_jobs, d_mbs, nmbs, units, unit_h, codes);
+    launch_split(st, d_jobs, d_mbs, nmbs, units, unit_h, codes, max_mb_units, max_short_units);
     tm.stop();
     tm.start("type_histo");
     launch_histo(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, units, hl, hc, hd);
