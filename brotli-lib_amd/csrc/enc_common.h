@@ -456,7 +456,7 @@ size_t cost_model_hist_bytes(int njobs);
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,
                        uint32_t *hist, CostModel *model);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
-               const uint32_t *matches, uint64_t *choice, bool cdict);
+               const uint32_t *matches, uint64_t *choice, bool cdict, bool font);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
 void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces);

@@ -68,6 +68,9 @@ constexpr uint32_t kCostLast = 255;   // cost code of a match at the path's last
 #define MIB_DP_OCC 4   // (A/B builds: 5; with two encode lanes 4 is faster, r04o)
 #endif
 constexpr int kDpWavesPerSimd = MIB_DP_OCC;
+#ifndef MIB_DP_OCC_KS4
+#define MIB_DP_OCC_KS4 MIB_DP_OCC   // (A/B builds: the four-segment build's occupancy target)
+#endif
 constexpr int kPtabW = 20;
 static_assert(kLongCopy <= 325, "copy codes of lengths <= 325 are < 20 (command.ts getCopyLengthCode)");
 
@@ -138,7 +141,7 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
 // profiles tell the two passes apart).  KD: some stream has a custom dictionary (records with
 // kCDictMark; a separate build, so the common case pays nothing for it)
 template <int KS, bool KM, bool KD>
-__global__ __launch_bounds__(64 * kDpWaves, kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
+__global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
                                                            uint64_t *choice /* per position+1 */, float cmd_pen) {
@@ -900,29 +903,32 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
   return 0;
 }
 #endif
-// dp_kernel<2> when there are enough segments to fill the chip (1024 SIMDs: 256 CUs x 4),
-// else dp_kernel<1>
-static int dp_ks(int nsegs) {
+// dp_kernel<4> when there are enough segments for three such waves per SIMD (1024 SIMDs:
+// 256 CUs x 4; 143 VGPRs), dp_kernel<2> when there are enough for one, else dp_kernel<1>.
+// Four segments a wave: a step's node fetch, staging and table reads serve four segments and
+// text's short staircases still fit 16 lanes' chunks (C4 dp 91.7 -> 75.3 ms, one encode lane,
+// r04an; in round 3, before the LDS trim, it was slower: 106.6 -> 119.5 ms)
+// FONT mode keeps two: its longer staircases need more of the 16-lane chunks a step (C3 dp
+// 38.4 -> 46.6 ms beside the other encode lane, r04ao).
+constexpr int kKs4Segs = 3 * 4 * 1024;
+static int dp_ks(int nsegs, bool font) {
   static const int v = getenv("MIB_DP_KS") ? atoi(getenv("MIB_DP_KS")) : 0;   // experiments
-  if (v == 1 || v == 2 || v == 4) return v;   // (4: measured slower on C4, 106.6 -> 119.5 ms: 180 VGPRs, half the waves)
-  return nsegs < 2048 ? 1 : 2;
-}
-static int dp_workgroups(int nsegs) {
-  const int spw = kDpWaves * dp_ks(nsegs);
-  return (nsegs + spw - 1) / spw;
+  if (v == 1 || v == 2 || v == 4) return v;
+  return !font && nsegs >= kKs4Segs ? 4 : nsegs < 2048 ? 1 : 2;
 }
 template <bool KD>
 static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
-                        const CostModel *model, const uint32_t *matches, uint64_t *choice) {
-  const dim3 g(dp_workgroups(nsegs)), b(64 * kDpWaves);
+                        const CostModel *model, const uint32_t *matches, uint64_t *choice, bool font) {
+  const int ks = dp_ks(nsegs, font), spw = kDpWaves * ks;
+  const dim3 g((nsegs + spw - 1) / spw), b(64 * kDpWaves);
   // MIB_CMD_PENALTY (bits, experiment): added to every copy's price, fewer and longer commands
   static const float cmd_pen = getenv("MIB_CMD_PENALTY") ? (float)atof(getenv("MIB_CMD_PENALTY")) : 0.f;
-  if (dp_ks(nsegs) == 1) {
+  if (ks == 1) {
     if (model)
       hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
     else
       hipLaunchKernelGGL((dp_kernel<1, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-  } else if (dp_ks(nsegs) == 4) {
+  } else if (ks == 4) {
     if (model)
       hipLaunchKernelGGL((dp_kernel<4, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
     else
@@ -935,9 +941,9 @@ static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int ns
   }
 }
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
-               const uint32_t *matches, uint64_t *choice, bool cdict) {
-  if (cdict) launch_dp_t<true>(st, jobs, segs, nsegs, lit_h, model, matches, choice);
-  else launch_dp_t<false>(st, jobs, segs, nsegs, lit_h, model, matches, choice);
+               const uint32_t *matches, uint64_t *choice, bool cdict, bool font) {
+  if (cdict) launch_dp_t<true>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font);
+  else launch_dp_t<false>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font);
 }
 size_t cost_model_hist_bytes(int njobs) { return (size_t)njobs * kHistLen * 4; }
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,

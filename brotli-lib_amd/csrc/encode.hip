@@ -504,7 +504,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     tm.start(two_pass ? "dp_sample" : "dp_parse");
     Seg *s1 = sampled ? d_sample : two_pass ? d_segs : d_fin;
     const int n1 = s1 == d_fin ? nfin : nsegs;
-    launch_dp(st, d_jobs, s1, n1, lit_h, nullptr, matches, choice, any_cdict);
+    launch_dp(st, d_jobs, s1, n1, lit_h, nullptr, matches, choice, any_cdict, prm.font);
     tm.stop();
     tm.start("backtrack");
     launch_backtrack(st, d_jobs, s1, n1, choice, raw);
@@ -514,7 +514,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
       launch_cost_model(st, d_jobs, (int)k, s1, nsegs, raw, model_h, model);
       tm.stop();
       tm.start("dp_parse");
-      launch_dp(st, d_jobs, d_fin, nfin, lit_h, model, matches, choice, any_cdict);
+      launch_dp(st, d_jobs, d_fin, nfin, lit_h, model, matches, choice, any_cdict, prm.font);
       tm.stop();
       tm.start("backtrack");
       launch_backtrack(st, d_jobs, d_fin, nfin, choice, raw);
