@@ -1,0 +1,18 @@
+# r04ap: the match walk takes its candidates in pairs (two rejected by their first 8 bytes in
+# one step): encode / parts / lanes / dictionary tests, C4 (one lane and two), C3, C2 against
+# the committed build
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+OUT=gpurun_out/r04ap
+mkdir -p $OUT
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_encode.py tests/test_gpu_parts.py tests/test_gpu_lanes.py tests/test_gpu_custom_dict.py tests/test_gpu_configs.py -m gpu -x -v --timeout 400 --timeout-method thread > $OUT/tests.log 2>&1 || { echo "tests failed"; tail -40 $OUT/tests.log; exit 1; }
+A="--steps 3 --warmup 1 --no-cpu-baseline"
+ALT=$PWD/brotli-lib_amd/libbrotli_amd_alt.so
+MIB_ENC_LANES=1 timeout -k 10 300 python3 bench.py $A > $OUT/c4l1_new.json 2> $OUT/c4l1_new.err || { echo "c4l1 new failed"; tail $OUT/c4l1_new.err; exit 1; }
+MIB_ENC_LANES=1 BROTLI_AMD_LIB=$ALT timeout -k 10 300 python3 bench.py $A > $OUT/c4l1_base.json 2> $OUT/c4l1_base.err || { echo "c4l1 base failed"; tail $OUT/c4l1_base.err; exit 1; }
+for w in c4 c3 c2; do
+  timeout -k 10 300 python3 bench.py $A --workload $w > $OUT/${w}_new.json 2> $OUT/${w}_new.err || { echo "$w new failed"; tail $OUT/${w}_new.err; exit 1; }
+  BROTLI_AMD_LIB=$ALT timeout -k 10 300 python3 bench.py $A --workload $w > $OUT/${w}_base.json 2> $OUT/${w}_base.err || { echo "$w base failed"; tail $OUT/${w}_base.err; exit 1; }
+done
+echo "exit=0"
