@@ -979,7 +979,8 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ uint32_t h[AMAX];
   __shared__ int16_t nzs[AMAX];
   __shared__ int16_t sorted[AMAX];
-  __shared__ uint32_t cnt[2 * AMAX + 2];
+  __shared__ __attribute__((aligned(16))) uint32_t cnt[2 * AMAX + 2];   // (also the sort's keys: 8 B each)
+  static_assert((2 * AMAX + 2) * 4 >= AMAX * 8, "the sort keys fit cnt");
   __shared__ int16_t left[2 * AMAX + 2], val[2 * AMAX + 2];
   __shared__ uint8_t depth[AMAX];
   __shared__ uint16_t code[AMAX];
@@ -1046,16 +1047,40 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
     for (uint32_t lc = 1;; lc *= 2) {
       hp_att++;
       const uint64_t ta = HPT();
-      for (int a = lane; a < n; a += 64) {
-        const int si = nzs[a];
-        const uint32_t ci = h[si] > lc ? h[si] : lc;
-        int r = 0;
-        for (int b = 0; b < n; b++) {
-          const int sj = nzs[b];
-          const uint32_t cj = h[sj] > lc ? h[sj] : lc;
-          r += (cj < ci || (cj == ci && sj > si)) ? 1 : 0;
+      // rank sort by (clamped count, descending symbol): key (count << 16) | (0xFFFF - symbol),
+      // a symbol's rank = the keys below its own.  The keys in LDS (cnt's space: the tree is
+      // built after the sort), read two at a time and compared with all of a lane's symbols
+      // (one pair read per two keys, not two reads per key and symbol)
+      uint64_t *keys = reinterpret_cast<uint64_t *>(cnt);
+      for (int a = lane; a < ((n + 1) & ~1); a += 64) {
+        uint64_t k = ~0ull;   // (the pad: below no key)
+        if (a < n) {
+          const int si = nzs[a];
+          const uint32_t ci = h[si] > lc ? h[si] : lc;
+          k = ((uint64_t)ci << 16) | (uint32_t)(0xFFFF - si);
         }
-        sorted[r] = (int16_t)si;
+        keys[a] = k;
+      }
+      wave_sync();
+      constexpr int kPerLane = (AMAX + 63) / 64;
+      uint64_t mine[kPerLane];
+      uint32_t rk[kPerLane];
+#pragma unroll
+      for (int q = 0; q < kPerLane; q++) {
+        const int a = lane + 64 * q;
+        mine[q] = a < n ? keys[a] : 0ull;
+        rk[q] = 0;
+      }
+      const ulonglong2 *kp = reinterpret_cast<const ulonglong2 *>(keys);
+      for (int b = 0; b < n; b += 2) {
+        const ulonglong2 kb = kp[b >> 1];
+#pragma unroll
+        for (int q = 0; q < kPerLane; q++) rk[q] += (uint32_t)(kb.x < mine[q]) + (uint32_t)(kb.y < mine[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < kPerLane; q++) {
+        const int a = lane + 64 * q;
+        if (a < n) sorted[rk[q]] = nzs[a];
       }
       wave_sync();
       const uint64_t tb = HPT();
