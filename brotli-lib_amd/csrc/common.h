@@ -13,6 +13,16 @@ extern "C" int mib_bufs_from_device(size_t k, mib_buf *const *outs, const uint8_
 
 namespace mib {
 
+// Experiment knobs (MIB_* environment variables) are read only by the -DMIB_EXPERIMENTS build
+// the A/B scripts make (`make EXPERIMENTS=1`, scripts/README.md).  The shipped library ignores
+// the environment: its output depends on its inputs and options alone.
+const char *knob(const char *name);
+
+// Whether device `dev`'s returning LDS atomics served a wave's lanes in lane order in the
+// self-test ensure_device runs once per device (mib_selftest_lds_atomic_order): the bucket
+// sort's fast ranking relies on it, and ranks by ballots where it does not hold (enc_sort.hip).
+bool lds_rank_ordered(int dev);
+
 // One stream to decode.  Filled by the host, read/written by decode kernels.
 struct DecJob {
   const uint8_t *in;      // compressed stream (device)

@@ -1385,7 +1385,7 @@ struct SplitK { int k[3]; };
 SplitK split_k() {
   static const SplitK sk = [] {
     SplitK k{{kSplitBtLit, 4, 4}};
-    if (const char *e = getenv("MIB_SPLIT_BT")) sscanf(e, "%d,%d,%d", &k.k[0], &k.k[1], &k.k[2]);
+    if (const char *e = knob("MIB_SPLIT_BT")) sscanf(e, "%d,%d,%d", &k.k[0], &k.k[1], &k.k[2]);
     for (int c = 0; c < 3; c++) k.k[c] = std::min(kMaxBT, std::max(1, k.k[c]));
     return k;
   }();
@@ -1951,7 +1951,7 @@ void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
   // 512 threads: the 35 KiB unit histograms allow four blocks (32 waves) per CU (MIB_CODES_NT overrides)
-  static const int nt = getenv("MIB_CODES_NT") ? atoi(getenv("MIB_CODES_NT")) : 512;
+  static const int nt = knob("MIB_CODES_NT") ? atoi(knob("MIB_CODES_NT")) : 512;
   if (nt >= 512)
     hipLaunchKernelGGL(codes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
   else
@@ -1989,7 +1989,7 @@ void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mb
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
   // 1024 threads: the 64 KiB literal histogram allows two blocks per CU, so wider blocks are
   // what hides the per-literal gathers (C3 type_histo 9.6 -> 5.3 ms; MIB_HISTO_NT overrides)
-  static const int nt = getenv("MIB_HISTO_NT") ? atoi(getenv("MIB_HISTO_NT")) : 1024;
+  static const int nt = knob("MIB_HISTO_NT") ? atoi(knob("MIB_HISTO_NT")) : 1024;
   if (nt >= 1024)
     hipLaunchKernelGGL(histo_kernel<1024>, dim3(nsegs), dim3(1024), 0, st, jobs, segs, mbs, cmds, cmd_pos, units, hl, hc, hd);
   else if (nt >= 512)
@@ -2001,7 +2001,7 @@ void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, con
   hipLaunchKernelGGL(dist_ring_kernel, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs, segs, cmds);
 }
 void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
-  static const int force = getenv("MIB_CTX_MODE") ? atoi(getenv("MIB_CTX_MODE")) & 3 : -1;   // experiments
+  static const int force = knob("MIB_CTX_MODE") ? atoi(knob("MIB_CTX_MODE")) & 3 : -1;   // experiments
   hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, force);
 }
 // Literal prefix codes per metablock: at most kLitTreeCap.  The decoder keeps a metablock's
@@ -2013,7 +2013,7 @@ void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
 // context-free literals).
 constexpr int kLitTreeCap = 24;
 int lit_tree_cap() {
-  static const int cap = getenv("MIB_LIT_TREES") ? std::min(kMaxLitTrees, std::max(1, atoi(getenv("MIB_LIT_TREES")))) : kLitTreeCap;
+  static const int cap = knob("MIB_LIT_TREES") ? std::min(kMaxLitTrees, std::max(1, atoi(knob("MIB_LIT_TREES")))) : kLitTreeCap;
   return cap;
 }
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
@@ -2036,7 +2036,7 @@ void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const ui
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
-  static const int nt = getenv("MIB_SIZES_NT") ? atoi(getenv("MIB_SIZES_NT")) : 512;   // (MIB_SIZES_NT overrides)
+  static const int nt = knob("MIB_SIZES_NT") ? atoi(knob("MIB_SIZES_NT")) : 512;   // (MIB_SIZES_NT overrides)
   if (nt >= 512)
     hipLaunchKernelGGL(sizes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
   else

@@ -394,10 +394,10 @@ void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_jo
                          bool hist, bool parts, uint32_t *matches) {
   // tile of sorted entries per block: each tile also stages the kBack entries before it
   // (MIB_FM_TILE: experiment knob, 256 / 512 / 1024)
-  static const int tile = getenv("MIB_FM_TILE") ? atoi(getenv("MIB_FM_TILE")) : 256;
+  static const int tile = knob("MIB_FM_TILE") ? atoi(knob("MIB_FM_TILE")) : 256;
   // XCD-aware tile order (MIB_FM_XCD=1): measured no faster on C4 (64.9 vs 65.4 ms), off
-  static const int xcd = getenv("MIB_FM_XCD") ? atoi(getenv("MIB_FM_XCD")) : 0;
-  static const int flags = (xcd ? 1 : 0) | (getenv("MIB_FM_SORTED_STORE") ? 8 : 0);
+  static const int xcd = knob("MIB_FM_XCD") ? atoi(knob("MIB_FM_XCD")) : 0;
+  static const int flags = (xcd ? 1 : 0) | (knob("MIB_FM_SORTED_STORE") ? 8 : 0);
 #define MIB_FM(T, H, P)                                                                                                   \
   hipLaunchKernelGGL((find_matches_kernel<T, H, P>), dim3(8 * (((total + T - 1) / T + 7) / 8)), dim3(T), 0, st, jobs, pos_job, \
                      seg_ref, skeys, svals, total, depth, max_dist, matches, flags)

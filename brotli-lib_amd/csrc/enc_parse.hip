@@ -912,7 +912,7 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 // 38.4 -> 46.6 ms beside the other encode lane, r04ao).
 constexpr int kKs4Segs = 3 * 4 * 1024;
 static int dp_ks(int nsegs, bool font) {
-  static const int v = getenv("MIB_DP_KS") ? atoi(getenv("MIB_DP_KS")) : 0;   // experiments
+  static const int v = knob("MIB_DP_KS") ? atoi(knob("MIB_DP_KS")) : 0;   // experiments
   if (v == 1 || v == 2 || v == 4) return v;
   return !font && nsegs >= kKs4Segs ? 4 : nsegs < 2048 ? 1 : 2;
 }
@@ -922,7 +922,7 @@ static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int ns
   const int ks = dp_ks(nsegs, font), spw = kDpWaves * ks;
   const dim3 g((nsegs + spw - 1) / spw), b(64 * kDpWaves);
   // MIB_CMD_PENALTY (bits, experiment): added to every copy's price, fewer and longer commands
-  static const float cmd_pen = getenv("MIB_CMD_PENALTY") ? (float)atof(getenv("MIB_CMD_PENALTY")) : 0.f;
+  static const float cmd_pen = knob("MIB_CMD_PENALTY") ? (float)atof(knob("MIB_CMD_PENALTY")) : 0.f;
   if (ks == 1) {
     if (model)
       hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kDigits) void tile_scan_kernel(const Job *jobs, int
 // counts; their prefix over the waves and the tile's digit offsets give each wave its first
 // slot per digit.  Sweep 2, round by round: each item takes its digit's next slot (cur) by a
 // returning atomic.  Items go to LDS in sorted order, then out in runs.
-template <bool kFirst>
+template <bool kFirst, bool kBallotRank>
 __global__ __launch_bounds__(kSortT) void tile_scatter_kernel(const Job *jobs, const uint32_t *pos_job, int hb,
                                                               const uint32_t *in_k, const uint32_t *in_v, const uint16_t *hist,
                                                               const uint32_t *off, uint32_t *out_k, uint32_t *out_v) {
@@ -266,9 +266,27 @@ __global__ __launch_bounds__(kSortT) void tile_scatter_kernel(const Job *jobs, c
   // in the GPU tests), and a wave's LDS operations complete in issue order: so round r's items
   // take their digit's slots in (round, lane) order -- the sort is stable.  (Nine ballots per
   // round to the same effect cost ~90 VALU per round: the whole pass was VALU-bound.)
+  // kBallotRank: that ballot ranking, which does not depend on the atomics' lane order -- the
+  // build runs it on a device whose self-test (ensure_device, runtime.cpp) saw them out of order.
 #pragma unroll
   for (int r = 0; r < kRounds; r++) {
-    const uint32_t slot = atomicAdd(&cur[w][digit_of<kFirst>(key[r])], 1u);
+    const uint32_t d = digit_of<kFirst>(key[r]);
+    uint32_t slot;
+    if (kBallotRank) {
+      uint64_t m = ~0ull;
+#pragma unroll
+      for (int b = 0; b < kDigitBits; b++) {
+        const uint64_t bb = __ballot((d >> b) & 1u);
+        m &= ((d >> b) & 1u) ? bb : ~bb;
+      }
+      const int leader = __ffsll((unsigned long long)m) - 1;
+      uint32_t first = 0;
+      if ((int)lane == leader) first = atomicAdd(&cur[w][d], (uint32_t)__popcll(m));
+      first = (uint32_t)__shfl((int)first, leader);
+      slot = first + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    } else {
+      slot = atomicAdd(&cur[w][d], 1u);
+    }
     sk[slot] = key[r];
     sv[slot] = val[r];
   }
@@ -319,6 +337,11 @@ extern "C" int64_t mib_selftest_lds_atomic_order(int trials) {
 namespace mib {
 namespace enc {
 
+static uint16_t *hist_of(void *ws) { return reinterpret_cast<uint16_t *>(ws); }
+static uint32_t *off_of(void *ws, uint32_t ntiles) {
+  return reinterpret_cast<uint32_t *>((uint8_t *)ws + (((size_t)ntiles * kDigits * 2 + 255) & ~(size_t)255));
+}
+
 size_t sort_ws_bytes(uint32_t total) {
   const size_t ntiles = total >> kTileBits;
   return ntiles * kDigits * (sizeof(uint16_t) + sizeof(uint32_t)) + 512;
@@ -328,17 +351,30 @@ void launch_sort(hipStream_t st, const Job *jobs, const uint32_t *pos_job, int n
                  uint32_t *tmp_k, uint32_t *tmp_v, uint32_t *skeys, uint32_t *svals) {
   const uint32_t ntiles = total >> kTileBits;
   if (!ntiles) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (!lds_rank_ordered(dev)) {   // (the self-test found returning LDS atomics out of lane order)
+    hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, nullptr, hist_of(ws));
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(njobs), dim3(kDigits), 0, st, jobs, njobs, total, hist_of(ws), off_of(ws, ntiles));
+    hipLaunchKernelGGL((tile_scatter_kernel<true, true>), dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, nullptr, nullptr,
+                       hist_of(ws), off_of(ws, ntiles), tmp_k, tmp_v);
+    hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, tmp_k, hist_of(ws));
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(njobs), dim3(kDigits), 0, st, jobs, njobs, total, hist_of(ws), off_of(ws, ntiles));
+    hipLaunchKernelGGL((tile_scatter_kernel<false, true>), dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, tmp_k, tmp_v,
+                       hist_of(ws), off_of(ws, ntiles), skeys, svals);
+    return;
+  }
   uint16_t *hist = reinterpret_cast<uint16_t *>(ws);
   uint32_t *off = reinterpret_cast<uint32_t *>((uint8_t *)ws + (((size_t)ntiles * kDigits * 2 + 255) & ~(size_t)255));
   // pass 1: low digit, keys from the stream bytes -> tmp
   hipLaunchKernelGGL(tile_hist_kernel<true>, dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, nullptr, hist);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(njobs), dim3(kDigits), 0, st, jobs, njobs, total, hist, off);
-  hipLaunchKernelGGL(tile_scatter_kernel<true>, dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, nullptr, nullptr, hist, off,
+  hipLaunchKernelGGL((tile_scatter_kernel<true, false>), dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, nullptr, nullptr, hist, off,
                      tmp_k, tmp_v);
   // pass 2: high digit, tmp -> sorted
   hipLaunchKernelGGL(tile_hist_kernel<false>, dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, tmp_k, hist);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(njobs), dim3(kDigits), 0, st, jobs, njobs, total, hist, off);
-  hipLaunchKernelGGL(tile_scatter_kernel<false>, dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, tmp_k, tmp_v, hist, off,
+  hipLaunchKernelGGL((tile_scatter_kernel<false, false>), dim3(ntiles), dim3(kSortT), 0, st, jobs, pos_job, hb, tmp_k, tmp_v, hist, off,
                      skeys, svals);
 }
 

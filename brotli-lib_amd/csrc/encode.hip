@@ -143,13 +143,13 @@ struct StreamDesc {
 // overrides the one-shot threshold (0 disables the index).
 uint64_t part_min_stream() {
   static uint64_t v = [] {
-    const char *e = getenv("MIB_PART_MIN");
+    const char *e = knob("MIB_PART_MIN");
     return e ? (uint64_t)strtoull(e, nullptr, 10) : kPartMinStream;
   }();
   return v;
 }
 uint32_t env_u32(const char *name, uint32_t dflt, uint32_t lo, uint32_t hi) {
-  const char *e = getenv(name);
+  const char *e = knob(name);
   if (!e) return dflt;
   const unsigned long v = strtoul(e, nullptr, 10);
   return (uint32_t)std::max<unsigned long>(lo, std::min<unsigned long>(hi, v));
@@ -210,16 +210,16 @@ Params make_params(const mib_enc_opts *o) {
 // MIB_DP_PIECES=0..3 overrides.
 constexpr int kMaxPieceShift = 4;
 int dp_piece_shift(int nsegs) {
-  static const int v = getenv("MIB_DP_PIECES") ? std::min(kMaxPieceShift, std::max(0, atoi(getenv("MIB_DP_PIECES")))) : -1;
+  static const int v = knob("MIB_DP_PIECES") ? std::min(kMaxPieceShift, std::max(0, atoi(knob("MIB_DP_PIECES")))) : -1;
   (void)nsegs;
   return v >= 0 ? v : 3;
 }
 bool rep_pass(const Params &p) {
-  static const int v = getenv("MIB_REP") ? atoi(getenv("MIB_REP")) : -1;
+  static const int v = knob("MIB_REP") ? atoi(knob("MIB_REP")) : -1;
   return v < 0 ? p.font : v != 0;
 }
 int hash_bytes(const Params &p) {
-  static const int v = getenv("MIB_HASH_BYTES") ? std::min(6, std::max(4, atoi(getenv("MIB_HASH_BYTES")))) : -1;
+  static const int v = knob("MIB_HASH_BYTES") ? std::min(6, std::max(4, atoi(knob("MIB_HASH_BYTES")))) : -1;
   return v > 0 ? v : p.font ? 4 : kHashBytes;
 }
 
@@ -240,7 +240,7 @@ std::mutex g_dict_mu;
 // MIB_DICT=0 turns the dictionary references off (experiments)
 bool dict_enabled() {
   static bool v = [] {
-    const char *e = getenv("MIB_DICT");
+    const char *e = knob("MIB_DICT");
     return !e || atoi(e) != 0;
   }();
   return v;
@@ -1077,7 +1077,7 @@ mib_encoder *mib_encoder_new(const mib_enc_opts *o) {
   // stream has already encoded (a 32 MiB encode is 512 parse segments, a quarter of the DP's
   // waves: small encodes leave the chip idle).  MIB_STREAM_CHUNK (MiB, tests and experiments):
   // a fixed size.
-  if (getenv("MIB_STREAM_CHUNK")) {
+  if (knob("MIB_STREAM_CHUNK")) {
     e->chunk = (uint64_t)env_u32("MIB_STREAM_CHUNK", 32, 1, 4096) << 20;
     e->chunk_fixed = true;
   } else if (o && o->stream_chunk) {

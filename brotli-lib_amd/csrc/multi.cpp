@@ -90,10 +90,22 @@ Shard *acquire(int s, int dev) {
   sh->ctx = c;
   return sh;
 }
+// At most kKeepIdle idle shards per index stay pooled (each holds a context with up to
+// kKeepDevice per buffer and kKeepPinned of pinned memory); a burst of concurrent sharded calls
+// destroys its extra shards as they finish instead of keeping them for the process's life.
+constexpr size_t kKeepIdle = 1;
 void release(int s, Shard *sh) {
-  sh->trim();
-  std::lock_guard<std::mutex> lk(g_pool_mu);
-  g_pool[s].push_back(sh);
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool[s].size() < kKeepIdle) {
+      sh->trim();
+      g_pool[s].push_back(sh);
+      return;
+    }
+  }
+  if (sh->pin) hipHostFree(sh->pin);
+  mib_ctx_free(sh->ctx);
+  delete sh;
 }
 
 // size-balanced assignment: buffers by size, largest first, each to the least-loaded shard

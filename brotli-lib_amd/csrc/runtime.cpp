@@ -25,8 +25,19 @@ extern "C" hipError_t mib_decode_init_tables(const int16_t *host_lut);
 extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t *d_offsets, int k, uint8_t *d_heads,
                                             hipStream_t stream);
 
+const char *mib::knob(const char *name) {
+#ifdef MIB_EXPERIMENTS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
-
+namespace {
+bool g_dev_unordered_any(int dev);
+}
+bool mib::lds_rank_ordered(int dev) { return !g_dev_unordered_any(dev); }
 
 namespace {
 
@@ -40,6 +51,7 @@ std::mutex g_mu;
 int g_device = 0;                 // device of the default context (mib_init)
 constexpr int kMaxDevices = 64;
 bool g_dev_ready[kMaxDevices];    // per device: checked to be gfx950, command table uploaded
+bool g_dev_unordered[kMaxDevices];  // per device: the LDS atomic order self-test failed
 int g_dev_cus[kMaxDevices];       // per device: compute units
 
 void build_cmd_lut(int16_t *lut) {   // engine.ts:65-90
@@ -88,8 +100,19 @@ int ensure_device(int device) {
   build_cmd_lut(lut);
   HIP_OK(mib_decode_init_tables(lut));
   HIP_OK(hipDeviceSynchronize());
+  const int64_t bad = mib_selftest_lds_atomic_order(4096);
+  if (bad < 0) return MIB_E_NO_DEVICE;
+  g_dev_unordered[device] = bad != 0;
+  if (bad)
+    fprintf(stderr, "brotli_amd: device %d serves returning LDS atomics out of lane order (%lld of 262144 lanes); "
+                    "the bucket sort ranks by ballots\n", device, (long long)bad);
   g_dev_ready[device] = true;
   return 0;
+}
+
+int g_force_ballot = 0;
+bool g_dev_unordered_any(int dev) {
+  return __atomic_load_n(&g_force_ballot, __ATOMIC_RELAXED) || (dev >= 0 && dev < kMaxDevices && g_dev_unordered[dev]);
 }
 
 int ensure_init() {
@@ -647,7 +670,7 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
   uint64_t per_block = ring_bytes + mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4 + 3092 * 4;   // ... ctx-map table, block trees
   per_block = (per_block + 255) & ~(uint64_t)255;
   // (MIB_DEC_GRID: experiment knob, a smaller persistent grid -- fewer decoder waves per CU)
-  static const size_t grid_cap = getenv("MIB_DEC_GRID") ? (size_t)std::max(1, atoi(getenv("MIB_DEC_GRID"))) : 2048;
+  static const size_t grid_cap = mib::knob("MIB_DEC_GRID") ? (size_t)std::max(1, atoi(mib::knob("MIB_DEC_GRID"))) : 2048;
   int grid = (int)std::min<size_t>(k, std::min<size_t>(grid_cap, 2048));
   int rc;
   if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
@@ -1007,3 +1030,5 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
 }
 
 }  // extern "C"
+
+extern "C" void mib_force_ballot_rank(int force) { __atomic_store_n(&g_force_ballot, force ? 1 : 0, __ATOMIC_RELAXED); }

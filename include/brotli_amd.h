@@ -118,6 +118,10 @@ int mib_device_count(void);
  * order): lanes that broke it over `trials` random collision patterns (0 expected), < 0 on a
  * HIP error. */
 int64_t mib_selftest_lds_atomic_order(int trials);
+/* The library runs that self-test once per device and, where it fails, ranks the sort's
+ * items by wave ballots instead (same stream bytes, slower).  Test hook: force = 1 makes
+ * every device take the ballot ranking, 0 restores the self-test's choice. */
+void mib_force_ballot_rank(int force);
 
 void mib_buf_free(mib_buf *b);
 /* The allocator behind every mib_buf the library returns (default malloc / free), in the

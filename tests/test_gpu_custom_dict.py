@@ -96,12 +96,12 @@ def test_batch_and_device_context():
         assert o == brotli_amd.brotliEncode(b, opts)   # a batch encodes each stream as alone
 
 
-def test_streaming_with_dictionary(monkeypatch):
-    monkeypatch.setenv('MIB_STREAM_CHUNK', '4')   # several device chunks
+def test_streaming_with_dictionary():
     d = c5_dictionary()
     data = d[-150:] + datagen.enwik_text(10 << 20, 31)
     r0 = _oracle.compound_refs()
-    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'mode': 1, 'customDictionary': d})
+    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'mode': 1, 'customDictionary': d,
+                                  'streamChunk': 4 << 20})   # several device chunks
     stream = b''.join([e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)] + [e.finish()])
     _both(data, stream, d)
     assert _oracle.compound_refs() > r0

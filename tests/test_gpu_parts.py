@@ -169,10 +169,10 @@ def test_index_pointing_into_its_own_payload_is_not_followed():
     assert p1 == p0, 'the forged index was followed'
 
 
-def test_streaming_chunks_carry_chained_indexes(monkeypatch):
-    monkeypatch.setenv('MIB_STREAM_CHUNK', '8')   # 8 MiB device chunks: three chained indexes
+def test_streaming_chunks_carry_chained_indexes():
     data = datagen.enwik_text(20 << 20, 9)
-    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24})
+    # throughput mode from 8 MiB device chunks (8, 8, then 4 at finish): three chained indexes
+    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'streamChunk': 8 << 20})
     parts = [e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)]
     parts.append(e.finish())
     enc = b''.join(parts)
@@ -187,11 +187,11 @@ def test_streaming_chunks_carry_chained_indexes(monkeypatch):
     assert brotli_amd.part_stats() == (p0 + 1, f0)
 
 
-def test_streaming_exact_chunks_then_empty_finish(monkeypatch):
-    # the chunks use up the input exactly: finish() only adds the final empty metablock
-    monkeypatch.setenv('MIB_STREAM_CHUNK', '8')
+def test_streaming_exact_chunks_then_empty_finish():
+    # the chunks (8 MiB, then 8 MiB) use up the input exactly: finish() only adds the final
+    # empty metablock
     data = datagen.enwik_text(16 << 20, 11)
-    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'mode': 1})
+    e = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24, 'mode': 1, 'streamChunk': 8 << 20})
     parts = [e.update(data[i:i + (1 << 20)]) for i in range(0, len(data), 1 << 20)]
     tail = e.finish()
     assert tail == b'\x03'
