@@ -220,6 +220,66 @@ def gen_decode(tmp):
     print('decode vectors:', len(vec))
 
 
+def q59_cases():
+    """brotliEncode at qualities 5-9 (hash chains + greedy, backward-references.ts:14-134): one-shot
+    inputs below 2^lgwin (past it the reference's ring indexing is wrong: bugs C/E), lgwin 22 and
+    others, GENERIC / TEXT / FONT."""
+    ins = [
+        {'kind': 'file', 'path': 'vectors/alice29.txt', 'len': 45000},
+        {'kind': 'file', 'path': 'vectors/asyoulik.txt', 'len': 20000},
+        {'kind': 'file', 'path': 'vectors/lcet10.txt', 'len': 120000},
+        {'kind': 'enwik', 'seed': 1, 'len': 45000},
+        {'kind': 'enwik', 'seed': 3, 'len': 300000},
+        {'kind': 'fox', 'repeats': 1000},
+        {'kind': 'file', 'path': 'bench/html-content.bin'},
+        {'kind': 'file', 'path': 'bench/random-binary.bin'},
+        {'kind': 'file', 'path': 'vectors/zerosukkanooa'},
+        {'kind': 'file', 'path': 'vectors/quickfox_repeated'},
+        {'kind': 'file', 'path': 'vectors/mapsdatazrh'},
+        {'kind': 'file', 'path': 'vectors/random_chunks'},
+        {'kind': 'xorshift', 'seed': 77, 'skip': 0, 'len': 200},
+        {'kind': 'ramp', 'len': 3000},
+    ]
+    cases = []
+    for q in (5, 6, 7, 8, 9):
+        for spec in ins:
+            cases.append((spec, {'quality': q}))
+    for q in (5, 7, 9):
+        cases.append(({'kind': 'file', 'path': 'bench/enc-ttf.bin', 'len': 262144}, {'quality': q, 'mode': 2}))
+        cases.append(({'kind': 'glyf', 'seed': 1001, 'len': 65536}, {'quality': q, 'mode': 2}))
+        cases.append(({'kind': 'file', 'path': 'vectors/alice29.txt', 'len': 45000}, {'quality': q, 'mode': 1}))
+        cases.append(({'kind': 'file', 'path': 'vectors/alice29.txt', 'len': 30000}, {'quality': q, 'lgwin': 16}))
+        cases.append(({'kind': 'enwik', 'seed': 4, 'len': 1 << 20}, {'quality': q, 'lgwin': 24}))
+    cases.append(({'kind': 'enwik', 'seed': 5, 'len': (4 << 20) - 64}, {'quality': 9, 'lgwin': 22}))
+    return cases
+
+
+def gen_q59(tmp):
+    cases = q59_cases()
+    jobs = []
+    for i, (spec, opts) in enumerate(cases):
+        p = os.path.join(tmp, 'q_%d' % i)
+        with open(p, 'wb') as f:
+            f.write(_inputs.resolve(spec))
+        jobs.append({'id': str(i), 'op': 'encode', 'variant': 'fixed', 'in': p, 'opts': opts, 'inline_max': 0})
+    chunks = [jobs[k::8] for k in range(8)]
+    res = {}
+    with cf.ThreadPoolExecutor(8) as ex:
+        for out in ex.map(lambda c: run_jobs(c, tmp), chunks):
+            for r in out:
+                res[r['id']] = r
+    golden = []
+    for i, (spec, opts) in enumerate(cases):
+        r = res[str(i)]
+        golden.append({'input': spec, 'opts': opts, 'len': r['len'], 'sha256': r['sha256'], 'ref_ms': round(r['ms'], 3),
+                       'native_roundtrip': r['native_roundtrip']})
+    with open(os.path.join(GOLD, 'encode_ref_q5_9.json'), 'w') as f:
+        json.dump({'generator': 'oracle/refgen/make_goldens.py --only q59',
+                   'reference': 'countertype/brotli-lib v0.0.7 (the q5-9 path: hash chains + greedy, as is)',
+                   'cases': golden}, f, indent=0)
+    print('q5-9 encode goldens:', len(golden))
+
+
 def gen_bt(tmp):
     out = []
     for spec in ({'kind': 'file', 'path': 'vectors/alice29.txt', 'len': 4096},
@@ -241,7 +301,7 @@ def main():
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         for part in a.only.split(','):
-            {'encode': gen_encode, 'decode': gen_decode, 'bt': gen_bt}[part](tmp)
+            {'encode': gen_encode, 'decode': gen_decode, 'bt': gen_bt, 'q59': gen_q59}[part](tmp)
 
 
 if __name__ == '__main__':

@@ -73,6 +73,23 @@ def test_encode_matches_ref_fixed(chunk):
         assert (_oracle.decode(out) == data) == c['native_roundtrip'], (c['input'], o)
 
 
+def test_encode_q5_9_matches_reference():
+    """brotliEncode at qualities 5-9 (hash chains + greedy, backward-references.ts:14-134,
+    hash-chains.ts:68-153) byte-identical to the reference run as is (86 cases: text, binary,
+    fonts in FONT mode, TEXT mode, lgwin 16 / 22 / 24, up to 4 MiB at q9 lgwin 22); the golden
+    streams all decode to their inputs under native brotli, and under the oracle decoder."""
+    cases = _load('encode_ref_q5_9.json')
+    assert len(cases) == 86
+    for c in cases:
+        data = _inputs.resolve(c['input'])
+        o = c['opts']
+        out = _oracle.encode(data, o['quality'], o.get('lgwin', 22), o.get('mode', 0))
+        assert hashlib.sha256(out).hexdigest() == c['sha256'], (c['input'], o)
+        assert c['native_roundtrip']
+        if len(data) <= 300000:
+            assert _oracle.decode(out) == data
+
+
 def test_peek_decoded_size():
     assert _oracle.peek_size(_oracle.encode(b'x' * 1000)) == 1000
     assert _oracle.peek_size(_oracle.encode(b'')) == 0
