@@ -268,19 +268,39 @@ def run_stream(args, rank, world, local):
         achieved = launch_bytes / (avg_ms * 1e-3) / 1e9
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            # the oracle (reference decoder restated) decodes the same stream with the same
-            # dictionary on one host thread (it is one bit-serial stream); the oracle restates
-            # the reference's q10/q11 encoder, not its q9 hash-chain path, so decode only
+            # decode: the oracle (reference decoder restated) decodes the same stream with the
+            # same dictionary on one host thread (it is one bit-serial stream).  encode: the
+            # oracle's restatement of the reference's q9 path (hash chains + greedy,
+            # backward-references.ts:14-134; pinned by tests/golden/encode_ref_q5_9.json) on the
+            # stream's first 1 MiB pieces, one-shot at lgwin 22 (the reference's q5-9 path has
+            # no custom dictionary and indexes its ring wrongly past 2^lgwin: bugs C/E), one
+            # piece per host thread; value = 1 / (1 / encode + 1 / decode), as the GPU's
+            from concurrent.futures import ThreadPoolExecutor
             sys.path.insert(0, os.path.join(ROOT, 'tests'))
             import _oracle
+            _oracle.lib()
             c0 = time.perf_counter()
             got = _oracle.decode(stream, dictionary=cdict)
             ct = time.perf_counter() - c0
             ok = got == data
             del got
-            cpu = {'value': round(size / 1e6 / ct, 3), 'unit': 'MB/s', 'cores': 1, 'kind': 'port',
-                   'sample': 'decode only: the whole %d B C5 stream, oracle decoder with the dictionary, one host '
-                             'thread, %.1f s, %s' % (size, ct, 'bit-exact' if ok else 'MISMATCH')}
+            threads = cpu_share()
+            pieces = [bytes(view[k * MIB:(k + 1) * MIB]) for k in range(min(threads, size // MIB))]
+            e0 = time.perf_counter()
+            with ThreadPoolExecutor(threads) as ex:
+                encs = list(ex.map(lambda b: _oracle.encode(b, q, 22, 1), pieces))
+            et = time.perf_counter() - e0
+            eok = all(_oracle.decode(x) == b for x, b in zip(encs, pieces))
+            enc_mbps = len(pieces) * MIB / 1e6 / et
+            dec_mbps = size / 1e6 / ct
+            cpu = {'value': round(1.0 / (1.0 / enc_mbps + 1.0 / dec_mbps), 4), 'unit': 'MB/s', 'cores': threads,
+                   'kind': 'port', 'encode_MBps': round(enc_mbps, 4), 'decode_MBps': round(dec_mbps, 3),
+                   'compressed_ratio_sample': round(sum(map(len, encs)) / (len(pieces) * MIB), 5),
+                   'sample': 'encode: %d x 1 MiB pieces of the stream, oracle q%d lgwin22 TEXT one-shot (the '
+                             'reference\'s hash-chain path restated), one piece per host thread, %.1f s, round trip %s; '
+                             'decode: the whole %d B C5 stream, oracle decoder with the dictionary, one host thread, '
+                             '%.1f s, %s' % (len(pieces), q, et, 'ok' if eok else 'FAILED', size, ct,
+                                             'bit-exact' if ok else 'MISMATCH')}
         print(json.dumps({
             'metric': 'encode+decode MB/s at q11 lgwin=22', 'value': round(mb / dt, 3), 'unit': 'MB/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(dt * 1e3, 3),

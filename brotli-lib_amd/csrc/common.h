@@ -23,6 +23,17 @@ const char *knob(const char *name);
 // sort's fast ranking relies on it, and ranks by ballots where it does not hold (enc_sort.hip).
 bool lds_rank_ordered(int dev);
 
+// Host <-> device copies of the host-buffer entry points through a context's pinned ring
+// (runtime.cpp): upload returns once the host bytes are in the ring (copies queued on
+// `stream`), download once every byte has reached host memory.
+struct HostPiece {
+  uint8_t *dst;
+  const uint8_t *src;
+  uint64_t n;
+};
+int ctx_upload(mib_ctx *c, void *stream, const HostPiece *ps, size_t k);
+int ctx_download(mib_ctx *c, void *stream, const HostPiece *ps, size_t k);
+
 // One stream to decode.  Filled by the host, read/written by decode kernels.
 struct DecJob {
   const uint8_t *in;      // compressed stream (device)

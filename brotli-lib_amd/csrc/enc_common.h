@@ -449,6 +449,8 @@ void launch_cdict_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_j
 void launch_find_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                          const uint32_t *skeys, const uint32_t *svals, uint32_t total, int depth, uint32_t max_dist,
                          bool hist, bool parts, uint32_t *matches);
+void launch_near_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref, uint32_t total,
+                         uint32_t max_dist, bool hist, bool parts, uint32_t *matches);
 void launch_lit_histo(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, uint32_t *lit_h);
 void launch_hist_update(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const uint32_t *skeys,
                         const uint32_t *svals, uint32_t total);

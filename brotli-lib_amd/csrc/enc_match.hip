@@ -276,6 +276,156 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
   *reinterpret_cast<uint4 *>(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec) = make_uint4(0u, 0u, 0u, 0u);   // no candidates
 }
 
+// ---------------------------------------------------------------- near matches (short scan)
+// findAllMatches' first step (hash-binary-tree.ts:167-194): before the tree, the positions up
+// to kNear back are scanned nearest first for a copy of at least 2 bytes, until one of at least
+// 3 is found -- the short, cheap-distance copies the bucket keys (6 bytes in GENERIC / TEXT
+// mode, 4 in FONT mode) never offer.  Block = 256 consecutive positions of one stream (one
+// segment): the 2-byte words of the block and the kNear positions before it are staged in LDS
+// (one aligned b32 read per candidate), the bytes after each position for measuring.  The
+// entries found are merged into the position's staircase record in front of the tree matches
+// they dominate (every tree match at least as short; a nearer one would have been found first);
+// a full record keeps its longest entries, as find_matches does.
+constexpr int kNear = 64;        // the reference's shortMatchMaxBackward at q11
+constexpr int kNearMeasure = 32; // near copies are measured up to this length (longer: the tree's)
+constexpr int kNearT = 256;      // threads per block; a tile is kNearT - 1 positions (+ one for m3)
+constexpr int kNearSpan = 4096;  // positions per block (its fixed lookups amortised)
+template <bool kHist, bool kParts>
+__global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
+                                                              uint32_t total, uint32_t max_dist, uint32_t *matches) {
+  constexpr int kStage = kNear + kNearT + kNearMeasure + 8;   // staged bytes per tile
+  constexpr int kPer = (kStage + kNearT - 1) / kNearT;        // ... per thread
+  constexpr uint32_t kStep = kNearT - 1;
+  __shared__ uint32_t w4[kNear + kNearT + kNearMeasure];   // the 4 bytes at each staged offset
+  __shared__ uint8_t bytes[kPer * kNearT];  // the tile's bytes from kNear before it (zero outside the stream)
+  __shared__ uint32_t sm2[2][kNearT];       // each position's 2-byte candidate mask (lo, hi word)
+  const uint32_t gb = blockIdx.x * kNearSpan;   // (a block stays inside one 64 KiB segment)
+  if (gb >= total) return;
+  const SegRef sr = seg_ref[gb >> kSegBits];
+  if (gb >= sr.end) return;   // padding, or an uncompressed stream's positions
+  const Job &jb = jobs[pos_job[gb >> kSegBits]];
+  const uint32_t hist = kHist ? jb.hist : 0u;   // bytes before data[0] copies may reach (streaming)
+  const uint32_t n = sr.end - sr.pos_base;
+  const uint32_t pbits = kParts ? jb.part_bits : 16u, plag = kParts ? jb.part_lag : 0u;
+  const bool parts = kParts && jb.parts;
+  const uint32_t t = threadIdx.x;
+  // the tile's bytes, loaded one tile ahead (kPer per thread, in registers)
+  uint32_t nb[kPer];
+  auto load_tile = [&](uint32_t g0) {
+    const uint32_t p0 = g0 - sr.pos_base;
+    const int64_t lo = -(int64_t)min((uint64_t)p0 + hist, (uint64_t)kNear);
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const int i = k * kNearT + (int)t;
+      const int64_t o = (int64_t)i - kNear, q = (int64_t)p0 + o;
+      nb[k] = (i < kStage && o >= lo && q < (int64_t)n && g0 < sr.end) ? sr.base[(int64_t)g0 + o] : 0u;
+    }
+  };
+  load_tile(gb);
+  for (uint32_t g0 = gb; g0 < gb + kNearSpan && g0 < sr.end; g0 += kStep) {
+    __syncthreads();   // (the previous tile's readers are done)
+#pragma unroll
+    for (int k = 0; k < kPer; k++) bytes[k * kNearT + t] = (uint8_t)nb[k];
+    load_tile(g0 + kStep);   // in flight during this tile
+    __syncthreads();
+    for (uint32_t i = t; i < kNear + kNearT + kNearMeasure; i += kNearT)
+      w4[i] = (uint32_t)bytes[i] | ((uint32_t)bytes[i + 1] << 8) | ((uint32_t)bytes[i + 2] << 16) | ((uint32_t)bytes[i + 3] << 24);
+    __syncthreads();
+    const uint32_t x = kNear + t, g = g0 + t, p = g - sr.pos_base;
+    const bool here = g < sr.end && p + 2 <= n;
+    // bit d of m2: the byte pair at p matches the pair d back (1 <= d <= reach).  One LDS word
+    // holds two candidate pairs (its low half the pair at y, its high half the pair at y + 2),
+    // tested at once: 32 words for the 63 distances, a zero-half test per word.
+    const uint32_t reach = min(min((uint32_t)kNear - 1, max_dist), p + hist);   // (the reference's d < 64)
+    const uint32_t me = w4[x] & 0xFFFFu, pp = me | (me << 16);
+    uint32_t ml = 0, mh = 0;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+      // y = x - 4k - 2: pairs at d = 4k + 2 (low half), 4k (high); y = x - 4k - 3: 4k + 3, 4k + 1
+      const uint32_t ve = w4[x - 4 * k - 2] ^ pp, vo = w4[x - 4 * k - 3] ^ pp;
+      const uint32_t ze = ~(((ve & 0x7FFF7FFFu) + 0x7FFF7FFFu) | ve) & 0x80008000u;   // bit 15 / 31: a zero half
+      const uint32_t zo = ~(((vo & 0x7FFF7FFFu) + 0x7FFF7FFFu) | vo) & 0x80008000u;
+      // the four bits d = 4k .. 4k + 3: (hi of ve, hi of vo, lo of ve, lo of vo)
+      const uint32_t nib = (ze >> 31) | ((zo >> 31) << 1) | (((ze >> 15) & 1u) << 2) | (((zo >> 15) & 1u) << 3);
+      if (k < 8) ml |= nib << (4 * k);
+      else mh |= nib << (4 * (k - 8));
+    }
+    const uint64_t valid = reach >= 63 ? ~1ull : ((2ull << reach) - 2ull);   // bits 1 .. reach
+    const uint64_t m2 = here ? ((((uint64_t)mh << 32) | ml) & valid) : 0ull;
+    sm2[0][t] = (uint32_t)m2;
+    sm2[1][t] = (uint32_t)(m2 >> 32);
+    // the position's record, loaded before the exchange so the barrier hides its latency
+    uint32_t *rec = matches + (uint64_t)g * kMatchRec;
+    // (thread kStep, and a position past the block: the m2 of the position before it only)
+    const bool emit = here && m2 && t < kStep && g < gb + kNearSpan;
+    uint4 r = make_uint4(0u, 0u, 0u, 0u);
+    if (emit) r = *reinterpret_cast<const uint4 *>(rec);
+    __syncthreads();
+    if (!emit) continue;
+    // a 3-byte copy from d = the pairs at p and at p + 1 both match d back
+    const uint64_t m3 = m2 & (((uint64_t)sm2[1][t + 1] << 32) | sm2[0][t + 1]);
+    const uint32_t limit = min(((g >> kSegBits) + 1) << kSegBits, sr.end) - g;   // copies never cross a parse segment
+    const uint32_t pA = kParts ? jb.abs_base + p : 0u;
+    const uint32_t cap0 = min(limit, (uint32_t)kNearMeasure);
+    // the reference's scan (nearest first, until a copy of 3 bytes or more) keeps the nearest
+    // 2-byte copy if it is nearer than the nearest 3-byte one, and that one, measured
+    uint32_t f0 = 0, f1 = 0, best = 1;
+    const uint32_t d2 = (uint32_t)__ffsll((unsigned long long)m2) - 1u;
+    const uint32_t d3 = m3 ? (uint32_t)__ffsll((unsigned long long)m3) - 1u : 64u;
+    if (d2 < d3) {   // a 2-byte copy nearer than any longer one
+      const uint32_t cap = min(cap0, parts ? part_cap(pA, d2, pbits, plag) : ~0u);
+      if (cap >= 2) {
+        f0 = pack_match(d2, 2);
+        best = 2;
+      }
+    }
+    if (d3 < 64u) {
+      const uint32_t cap = min(cap0, parts ? part_cap(pA, d3, pbits, plag) : ~0u);
+      // measured a word at a time (up to kNearMeasure)
+      uint32_t len = kNearMeasure;
+      for (int k = 0; k < kNearMeasure / 4; k++) {
+        const uint32_t v = w4[x + 4 * k] ^ w4[x - d3 + 4 * k];
+        if (v) {
+          len = 4 * k + ((uint32_t)(__ffs(v) - 1) >> 3);
+          break;
+        }
+      }
+      len = min(len, cap);
+      if (len > best) {
+        best = len;
+        if (f0) f1 = pack_match(d3, len);
+        else f0 = pack_match(d3, len);
+      }
+    }
+    if (!f0) continue;
+    if (r.x && (match_dist(r.x) == kCDictMark || (jb.dict && is_dict(match_dist(r.x))))) continue;   // a dictionary copy: the only entry
+    // the near entries, then the tree's longer ones; a full record keeps its longest
+    const uint32_t old[kMaxMatches] = {r.x, r.y, r.z, r.w};
+    uint32_t w[2 + kMaxMatches];
+    int m = 0;
+    w[m++] = f0;
+    if (f1) w[m++] = f1;
+#pragma unroll
+    for (int q = 0; q < kMaxMatches; q++)
+      if (old[q] && match_length(old[q]) > best) w[m++] = old[q];
+    const int sk = m > kMaxMatches ? m - kMaxMatches : 0;
+    uint32_t o4[kMaxMatches] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int q = 0; q < kMaxMatches; q++)
+      if (q + sk < m) o4[q] = w[q + sk];
+    *reinterpret_cast<uint4 *>(rec) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+  }
+}
+
+void launch_near_matches(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref, uint32_t total,
+                         uint32_t max_dist, bool hist, bool parts, uint32_t *matches) {
+  const dim3 g((total + kNearSpan - 1) / kNearSpan), b(kNearT);
+  if (hist && parts) hipLaunchKernelGGL((near_matches_kernel<true, true>), g, b, 0, st, jobs, pos_job, seg_ref, total, max_dist, matches);
+  else if (hist) hipLaunchKernelGGL((near_matches_kernel<true, false>), g, b, 0, st, jobs, pos_job, seg_ref, total, max_dist, matches);
+  else if (parts) hipLaunchKernelGGL((near_matches_kernel<false, true>), g, b, 0, st, jobs, pos_job, seg_ref, total, max_dist, matches);
+  else hipLaunchKernelGGL((near_matches_kernel<false, false>), g, b, 0, st, jobs, pos_job, seg_ref, total, max_dist, matches);
+}
+
 // ---------------------------------------------------------------- streaming history update
 // After a chunk's matches: every bucket the chunk touched gets its newest kHistWays stream
 // positions (this chunk's, from the end of its sorted run, then the older table entries).

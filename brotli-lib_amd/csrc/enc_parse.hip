@@ -72,6 +72,7 @@ constexpr int kDpWavesPerSimd = MIB_DP_OCC;
 #define MIB_DP_OCC_KS4 MIB_DP_OCC   // (A/B builds: the four-segment build's occupancy target)
 #endif
 constexpr int kPtabW = 20;
+constexpr int kRepLen = 16;   // last-distance copies relaxed up to this length (<= the lanes per segment)
 static_assert(kLongCopy <= 325, "copy codes of lengths <= 325 are < 20 (command.ts getCopyLengthCode)");
 
 typedef const __attribute__((address_space(1))) uint8_t GCU8;
@@ -139,16 +140,19 @@ __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
 
 // KM: the second iteration (prices from the stream's CostModel; a separate build, so
 // profiles tell the two passes apart).  KD: some stream has a custom dictionary (records with
-// kCDictMark; a separate build, so the common case pays nothing for it)
-template <int KS, bool KM, bool KD>
+// kCDictMark; a separate build, so the common case pays nothing for it).  KR: the parse relaxes
+// last-distance copies (rp_d below; FONT mode: C3 -1 % bytes, text -0.1 %, a separate build so
+// text pays nothing for it)
+template <int KS, bool KM, bool KD, bool KR>
 __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
-                                                           uint64_t *choice /* per position+1 */, float cmd_pen) {
+                                                           uint64_t *choice /* per position+1 */, float cmd_pen, int use_rep) {
   constexpr int kS = KS;                // segments per wave
   constexpr int kL = 64 / kS;           // lanes per segment
   constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
   static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
+  static_assert(kRepLen <= kL, "a last-distance copy is measured by one lane per byte");
   constexpr uint64_t kLaneMask = kL == 64 ? ~0ull : ((1ull << kL) - 1);
   __shared__ uint32_t ptab_all[kDpWaves * kS][24 * kPtabW];   // per segment: (insert code, copy code) -> fp16 (explicit distance) | fp16 (short code 0) << 16
   __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
   // (one spare entry per 32 lanes: the groups' entries i and 32 + i fall 12 banks apart, not on
   // the same banks -- two segments at the same offset read them in one instruction)
   __shared__ StageEnt stg_all[kDpWaves][64 + 2];
-  for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 4 ? copy_code((uint32_t)t) : 0);
+  for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 2 ? copy_code((uint32_t)t) : 0);
   for (int t = threadIdx.x; t < kInsTab; t += 64 * kDpWaves) {
     const int ic = ins_code((uint32_t)t);
     itab[t] = (uint16_t)(ic | (ins_extra(ic) << 8));
@@ -240,6 +244,12 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
   uint32_t pf_at = a;
   if (a + hl < b) load_staged(pf, matches, data, gbase + a + hl, a + hl);
   uint32_t chd = 0, chm = 0;   // choices of the batch
+  // the pending last-distance candidate (a6): node j reached by a literal, with last distance
+  // rp_d, loads the bytes at j + hl and j - rp_d + hl in its step; the step of node j + 1 (the
+  // loads' latency hidden behind one step) measures the match and relaxes lengths 2 .. R out
+  // of j, priced with short code 0 (rp_base / rp_ic: node j's cost + insert extra, insert code)
+  uint32_t rp_d = 0, rp_ic = 0, rp_cb = 0, rp_sb = 1;
+  float rp_base = 0.f;
   uint32_t i = a, i0 = a;
   bool done = a >= b;
 #ifdef MIB_PROF
@@ -289,7 +299,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
         maxlen = ln;
       }
     }
-    e.info = (maxlen ? nm : 0u) | (maxlen << 8) | ((word ? maxlen : 4u) << 16);   // | the shortest usable length
+    e.info = (maxlen ? nm : 0u) | (maxlen << 8) | ((word ? maxlen : 2u) << 16);   // | the shortest usable length
     e.pad[0] = e.pad[1] = 0;
     stg[lane + (lane >> 5)] = e;
     DPCOUNT(6, 1);
@@ -317,7 +327,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     const StageEnt &e = stg[src + (src >> 5)];
     const uint32_t info = e.info;
     const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? ((info >> 8) & 0xFF) : 0u;
-    const uint32_t minlen = info >> 16;   // 4, or a dictionary word's length: that length only
+    const uint32_t minlen = info >> 16;   // 2, or a dictionary word's length: that length only
     const float litcost = e.lc;
     const uint32_t ins = mm >> 16;
     // the node's insert code and extra bits came with it (its literal edge carried them: see
@@ -385,6 +395,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
         }
         i += fl;
         i0 = i;
+        rp_d = 0;
 #pragma unroll
         for (int c = 0; c < kC; c++) wc[c] = kInf;
         if (hl == 0) {
@@ -406,8 +417,19 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     const uint32_t mL[kMaxMatches] = {match_length(em.x) & actm, match_length(em.y) & actm, match_length(em.z) & actm,
                                       match_length(em.w) & actm};   // 0 past nm
     const uint32_t vpk[kMaxMatches] = {emc.x, emc.y, emc.z, emc.w};
-    const uint32_t maxrel = max(1u, maxlen);
+    // the last-distance copy out of node i - 1 (see rp_d): its length R from the loaded bytes
+    uint32_t R = 0;
+    if (KR) {
+      // (at most kRepLen bytes whatever the lanes per segment: a stream's parse must not
+      // depend on how many segments share its wave -- a batch encodes each stream as alone)
+      const uint64_t eqm = (__ballot(rp_cb == rp_sb) >> hbase) & ((1ull << kRepLen) - 1);
+      R = (act && rp_d) ? (eqm == (1ull << kRepLen) - 1 ? (uint32_t)kRepLen : (uint32_t)__ffsll((unsigned long long)~eqm) - 1u) : 0u;
+      if (parts && R) R = min(R, part_cap(abs0 + i - 1, rp_d, pbits, plag));
+      R = R >= 2 ? R : 0u;
+    }
+    const uint32_t maxrel = max(max(1u, maxlen), R ? R - 1 : 0u);
     const uint32_t *trow = ptab + ic * kPtabW;
+
     // relax every edge out of i: lane j of chunk k takes length kL k + j - off
 #pragma unroll
     for (int c = 0; c < kC; c++) {
@@ -437,6 +459,38 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
         wc[c] = cand;
         wd[c] = nd;
         wm[c] = nmeta;
+      }
+    }
+    if (KR && __ballot(R != 0)) {
+      // the last-distance copies of lengths 2 .. R <= kRepLen out of node i - 1: lane j of chunk
+      // c holds length kL c + j - off + 1 (chunks 0 and 1 hold them all)
+      const uint32_t *rrow = ptab + rp_ic * kPtabW;
+#pragma unroll
+      for (int c = 0; c < 2 && c < kC; c++) {
+        const uint32_t lr = (uint32_t)(kL * c) + hl - off + 1u;   // wraps (huge) below the node
+        if (lr >= 2u && lr <= R) {
+          const uint32_t tv = rrow[cctab[lr]];
+          const float cr = rp_base + (float)__builtin_bit_cast(_Float16, (uint16_t)(tv >> 16));
+          if (cr < wc[c]) {
+            wc[c] = cr;
+            wd[c] = rp_d;
+            wm[c] = lr;
+          }
+        }
+      }
+    }
+    // node i's own last-distance candidate: loads now, measured in the next step (a window
+    // distance only: not a dictionary word's or a custom-dictionary copy's)
+    if (KR) {
+      const bool rv = act && use_rep && ins > 0 && ld != 0u && !(words && is_dict(ld)) && ld <= min(wabs + i, maxback);
+      rp_d = rv ? ld : 0u;
+      rp_base = base;
+      rp_ic = (uint32_t)ic;
+      rp_cb = 0;
+      rp_sb = 1;
+      if (rv && hl < (uint32_t)kRepLen && i + hl < b) {
+        rp_cb = ((GCU8 *)data)[i + hl];
+        rp_sb = ((GCU8 *)data)[(int64_t)(i + hl) - (int64_t)ld];
       }
     }
     if (act) i++;
@@ -923,22 +977,22 @@ static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int ns
   const dim3 g((nsegs + spw - 1) / spw), b(64 * kDpWaves);
   // MIB_CMD_PENALTY (bits, experiment): added to every copy's price, fewer and longer commands
   static const float cmd_pen = knob("MIB_CMD_PENALTY") ? (float)atof(knob("MIB_CMD_PENALTY")) : 0.f;
-  if (ks == 1) {
-    if (model)
-      hipLaunchKernelGGL((dp_kernel<1, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-    else
-      hipLaunchKernelGGL((dp_kernel<1, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-  } else if (ks == 4) {
-    if (model)
-      hipLaunchKernelGGL((dp_kernel<4, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-    else
-      hipLaunchKernelGGL((dp_kernel<4, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-  } else {
-    if (model)
-      hipLaunchKernelGGL((dp_kernel<2, true, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-    else
-      hipLaunchKernelGGL((dp_kernel<2, false, KD>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen);
-  }
+  // last-distance candidates in the parse: FONT mode (MIB_DP_REP, experiments: 0 off, 2 every mode)
+  static const int rep_knob = knob("MIB_DP_REP") ? atoi(knob("MIB_DP_REP")) : 1;
+  const bool rep = rep_knob == 2 || (rep_knob == 1 && font);
+#define MIB_DP(K, M, R) hipLaunchKernelGGL((dp_kernel<K, M, KD, R>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen, 1)
+#define MIB_DP_KS(K)                \
+  do {                              \
+    if (model && rep) MIB_DP(K, true, true);   \
+    else if (model) MIB_DP(K, true, false);    \
+    else if (rep) MIB_DP(K, false, true);      \
+    else MIB_DP(K, false, false);              \
+  } while (0)
+  if (ks == 1) MIB_DP_KS(1);
+  else if (ks == 4) MIB_DP_KS(4);
+  else MIB_DP_KS(2);
+#undef MIB_DP_KS
+#undef MIB_DP
 }
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
                const uint32_t *matches, uint64_t *choice, bool cdict, bool font) {

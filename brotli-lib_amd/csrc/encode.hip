@@ -68,6 +68,8 @@ namespace {
 struct Workspace {
   size_t cap = 0;
   uint8_t *buf = nullptr;
+  uint64_t need = 0;   // the most the calls since the last trim needed (mib_encode_ws_trim's hysteresis)
+  int quiet = 0;
 };
 
 struct Arena {
@@ -217,6 +219,14 @@ int dp_piece_shift(int nsegs) {
 bool rep_pass(const Params &p) {
   static const int v = knob("MIB_REP") ? atoi(knob("MIB_REP")) : -1;
   return v < 0 ? p.font : v != 0;
+}
+// the short scan before the tree (near_matches_kernel), at q10+ outside FONT mode: there the
+// 4-byte keys already offer 4-5 byte copies and the scan's 2-3 byte ones changed C3 by -0.02 %
+// for 10 % of its encode time (r05g); text's 6-byte keys offer none (C4 -0.23 %).
+// (MIB_NEAR, experiment builds: 0 off, 2 every mode)
+bool near_scan(const Params &p) {
+  static const int v = knob("MIB_NEAR") ? atoi(knob("MIB_NEAR")) : 1;
+  return p.quality >= 10 && (v == 2 || (v == 1 && !p.font));
 }
 int hash_bytes(const Params &p) {
   static const int v = knob("MIB_HASH_BYTES") ? std::min(6, std::max(4, atoi(knob("MIB_HASH_BYTES")))) : -1;
@@ -421,6 +431,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     ws = new Workspace();
     *ws_slot = ws;
   }
+  ws->need = std::max<uint64_t>(ws->need, need);
   if (ws->cap < need) {
     if (ws->buf) hipFree(ws->buf);
     ws->buf = nullptr;
@@ -496,6 +507,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
                         any_parts, matches);
     if (dd) launch_dict_matches(st, d_jobs, (int)k, dict_span(), dd->tab, dd->data, matches);
     if (any_cdict) launch_cdict_matches(st, d_jobs, d_seg_job, total, matches);
+    if (near_scan(prm)) launch_near_matches(st, d_jobs, d_seg_job, d_seg_ref, total, (1u << prm.lgwin) - 16, any_hist, any_parts, matches);
     if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
     tm.stop();
     tm.start("lit_histo");
@@ -820,9 +832,12 @@ void mib_encode_ws_free(void *p) {
 }
 int mib_live_encoders(void) { return g_live_encoders.load(); }
 // the default context after a host call: a workspace above `keep` bytes is released
-void mib_encode_ws_trim(void **p, uint64_t keep) {
+void mib_encode_ws_trim(void **p, uint64_t keep) {   // (the hysteresis of runtime.cpp release_large)
   Workspace *ws = reinterpret_cast<Workspace *>(*p);
-  if (ws && ws->cap > keep) {
+  if (!ws) return;
+  ws->quiet = ws->need > keep ? 0 : ws->quiet + 1;
+  ws->need = 0;
+  if (ws->cap > keep && ws->quiet >= 4) {
     mib_encode_ws_free(ws);
     *p = nullptr;
   }
@@ -876,10 +891,13 @@ static int encode_host(const mib_span *in, size_t k, const mib_enc_opts *o, mib_
   uint8_t *d_in = mib_ctx_stage(c, 0, ioff[k] + 64), *d_out = mib_ctx_stage(c, 1, cap + 64);
   if (!d_in || !d_out) return MIB_E_OUT_OF_MEMORY;
   hipMemsetAsync(d_in, 0, ioff[k] + 64, st);
+  std::vector<HostPiece> up;
   for (size_t i = 0; i < k; i++)
-    if (in[i].size) hipMemcpyAsync(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice, st);
+    if (in[i].size) up.push_back(HostPiece{d_in + ioff[i], in[i].data, in[i].size});
+  int rc = ctx_upload(c, st, up.data(), up.size());   // (through the context's pinned ring)
+  if (rc) return rc;
   DevDict dd;
-  int rc = o ? dd.upload(o->dict, o->dict_len, st) : 0;
+  rc = o ? dd.upload(o->dict, o->dict_len, st) : 0;
   if (rc) return rc;
   std::vector<StreamDesc> sd(k);
   for (size_t i = 0; i < k; i++) {

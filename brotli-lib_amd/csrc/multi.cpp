@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/brotli_amd.h"
+#include "common.h"
 
 // runtime.cpp: result buffers (mib_set_allocator's allocator), the context's stream and staging
 extern "C" uint8_t *mib_buf_alloc(size_t n);
@@ -35,7 +36,6 @@ namespace {
 constexpr int kMaxShards = 64;
 // a shard's buffers above these sizes are released after the call (a batch of the usual size
 // keeps its buffers; one huge batch does not pin GiBs of host and device memory forever)
-constexpr uint64_t kKeepPinned = 1ull << 30;
 constexpr uint64_t kKeepDevice = 4ull << 30;
 
 int device_count() {
@@ -43,32 +43,11 @@ int device_count() {
   return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
+// A shard: its own context (stream, device buffers, pinned transfer ring: runtime.cpp)
 struct Shard {
   int device = -1;
   mib_ctx *ctx = nullptr;
-  uint8_t *pin = nullptr;   // pinned host staging (inputs in, results out)
-  uint64_t pin_cap = 0;
-  uint8_t *pinned(uint64_t need) {
-    if (pin_cap >= need) return pin;
-    if (pin) hipHostFree(pin);
-    pin = nullptr;
-    pin_cap = 0;
-    const uint64_t n = std::max<uint64_t>(need, 1 << 20);
-    if (hipHostMalloc((void **)&pin, n, hipHostMallocDefault) != hipSuccess) {
-      pin = nullptr;
-      return nullptr;
-    }
-    pin_cap = n;
-    return pin;
-  }
-  void trim() {
-    if (pin && pin_cap > kKeepPinned) {
-      hipHostFree(pin);
-      pin = nullptr;
-      pin_cap = 0;
-    }
-    mib_ctx_trim(ctx, kKeepDevice, kKeepDevice);
-  }
+  void trim() { mib_ctx_trim(ctx, kKeepDevice, kKeepDevice); }
 };
 
 std::mutex g_pool_mu;                        // guards the free lists only
@@ -103,7 +82,6 @@ void release(int s, Shard *sh) {
       return;
     }
   }
-  if (sh->pin) hipHostFree(sh->pin);
   mib_ctx_free(sh->ctx);
   delete sh;
 }
@@ -127,36 +105,28 @@ std::vector<std::vector<size_t>> assign(const mib_span *in, size_t k, int shards
 uint64_t align256(uint64_t n) { return (n + 255) & ~255ull; }
 
 // The shard's inputs packed back to back (the device-resident ABI reads stream i from
-// [in_offsets[i], in_offsets[i + 1])) into the pinned buffer, 64 zero bytes after the last,
-// then one copy to device staging slot 0.
+// [in_offsets[i], in_offsets[i + 1])) into device staging slot 0 through the shard context's
+// pinned ring, 64 zero bytes after the last.
 int upload(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, std::vector<uint64_t> &ioff, uint8_t **d_in,
            hipStream_t st) {
   const size_t k = idx.size();
   ioff.assign(k + 1, 0);
   for (size_t q = 0; q < k; q++) ioff[q + 1] = ioff[q] + in[idx[q]].size;
-  uint8_t *pin = sh.pinned(ioff[k] + 64);
   *d_in = mib_ctx_stage(sh.ctx, 0, ioff[k] + 64);
-  if (!pin || !*d_in) return MIB_E_OUT_OF_MEMORY;
+  if (!*d_in) return MIB_E_OUT_OF_MEMORY;
+  std::vector<mib::HostPiece> ps;
   for (size_t q = 0; q < k; q++)
-    if (in[idx[q]].size) memcpy(pin + ioff[q], in[idx[q]].data, in[idx[q]].size);
-  memset(pin + ioff[k], 0, 64);
-  if (hipMemcpyAsync(*d_in, pin, ioff[k] + 64, hipMemcpyHostToDevice, st) != hipSuccess) return MIB_E_NO_DEVICE;
-  return 0;
+    if (in[idx[q]].size) ps.push_back(mib::HostPiece{*d_in + ioff[q], in[idx[q]].data, in[idx[q]].size});
+  if (hipMemsetAsync(*d_in + ioff[k], 0, 64, st) != hipSuccess) return MIB_E_NO_DEVICE;
+  return mib::ctx_upload(sh.ctx, st, ps.data(), ps.size());
 }
 
-// Results [d_src[q], + len[q]) on the device -> out[idx[q]]: packed into the pinned buffer by
-// one asynchronous copy per result (no pageable copies, one wait), then host copies.
+// Results [d_src[q], + len[q]) on the device -> out[idx[q]]: allocated, then copied through
+// the shard context's pinned ring.
 int download(Shard &sh, const std::vector<size_t> &idx, const std::vector<const uint8_t *> &d_src,
              const std::vector<uint64_t> &len, const std::vector<bool> &want, mib_buf *out, hipStream_t st) {
   const size_t k = idx.size();
-  std::vector<uint64_t> poff(k + 1, 0);
-  for (size_t q = 0; q < k; q++) poff[q + 1] = poff[q] + (want[q] ? align256(len[q]) : 0);
-  uint8_t *pin = sh.pinned(poff[k] + 64);
-  if (!pin) return MIB_E_OUT_OF_MEMORY;
-  for (size_t q = 0; q < k; q++)
-    if (want[q] && len[q] && hipMemcpyAsync(pin + poff[q], d_src[q], len[q], hipMemcpyDeviceToHost, st) != hipSuccess)
-      return MIB_E_NO_DEVICE;
-  if (hipStreamSynchronize(st) != hipSuccess) return MIB_E_NO_DEVICE;
+  std::vector<mib::HostPiece> ps;
   for (size_t q = 0; q < k; q++) {
     if (!want[q]) continue;
     mib_buf &o = out[idx[q]];
@@ -164,9 +134,9 @@ int download(Shard &sh, const std::vector<size_t> &idx, const std::vector<const 
     o.size = 0;
     if (!o.data) return MIB_E_OUT_OF_MEMORY;
     o.size = len[q];
-    if (len[q]) memcpy(o.data, pin + poff[q], len[q]);
+    if (len[q]) ps.push_back(mib::HostPiece{o.data, d_src[q], len[q]});
   }
-  return 0;
+  return mib::ctx_download(sh.ctx, st, ps.data(), ps.size());
 }
 
 int encode_shard(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, const mib_enc_opts *o, mib_buf *out,

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "common.h"
@@ -323,6 +324,16 @@ struct mib_ctx {
   // hipMalloc / hipFree
   uint8_t *stage[kStageSlots] = {};
   uint64_t stage_cap[kStageSlots] = {};
+  // what the calls since the last trim needed of each buffer (trim's hysteresis, below)
+  struct Trim {
+    uint64_t need = 0;
+    int quiet = 0;   // trims in a row whose calls needed no more than the keep size
+  } stage_trim[kStageSlots], scratch_trim, parts_trim;
+  // pinned host ring of the host <-> device transfers (host_io below): two halves, one filling
+  // on the host while the other is in flight; allocated once, 2 x kRingHalf
+  uint8_t *ring = nullptr;
+  hipEvent_t ring_ev[2] = {nullptr, nullptr};
+  bool ring_failed = false;
   // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
   uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
@@ -363,9 +374,152 @@ int grow(void **p, uint64_t *cap, uint64_t need);
 // a staging buffer of at least `need` bytes (its content is not kept when it grows)
 extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need) {
   if (slot < 0 || slot >= kStageSlots) return nullptr;
+  c->stage_trim[slot].need = std::max(c->stage_trim[slot].need, need);
   return grow((void **)&c->stage[slot], &c->stage_cap[slot], need) == 0 ? c->stage[slot] : nullptr;
 }
 extern "C" void mib_encode_ws_free(void *ws);
+
+// ---------------------------------------------------------------- host <-> device transfers
+// Host buffers cross PCIe through the context's pinned ring: the host copies a ring half while
+// the other half is in flight, and host copies of more than a few MiB run on several threads.
+// Pageable hipMemcpy of many 1 MiB results into fresh host memory ran at 0.5-2 GB/s and varied
+// by 8x between runs; pinned halves move at PCIe speed, and the page faults
+// of fresh result buffers are spread over the copy threads.
+namespace {
+constexpr uint64_t kRingHalf = 32ull << 20;
+constexpr uint64_t kParCopyMin = 4ull << 20;   // below this, one thread copies
+constexpr int kCopyThreads = 8;
+using Piece = mib::HostPiece;
+void par_copy(const std::vector<Piece> &ps) {
+  uint64_t total = 0;
+  for (const Piece &p : ps) total += p.n;
+  const int nt = (int)std::min<uint64_t>(kCopyThreads, std::max<uint64_t>(1, total / kParCopyMin));
+  auto run = [&](uint64_t lo, uint64_t hi) {   // bytes [lo, hi) of the concatenated pieces
+    uint64_t at = 0;
+    for (const Piece &p : ps) {
+      const uint64_t a = std::max(lo, at), b = std::min(hi, at + p.n);
+      if (a < b) memcpy(p.dst + (a - at), p.src + (a - at), b - a);
+      at += p.n;
+      if (at >= hi) break;
+    }
+  };
+  if (nt <= 1) {
+    run(0, total);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; t++) th.emplace_back(run, total * t / nt, total * (t + 1) / nt);
+  run(0, total / nt);
+  for (auto &x : th) x.join();
+}
+bool ring_ready(mib_ctx *c) {
+  if (c->ring) return true;
+  if (c->ring_failed) return false;
+  hipSetDevice(c->device);
+  if (hipHostMalloc((void **)&c->ring, 2 * kRingHalf, hipHostMallocDefault) != hipSuccess) c->ring = nullptr;
+  for (int h = 0; h < 2 && c->ring; h++)
+    if (hipEventCreateWithFlags(&c->ring_ev[h], hipEventDisableTiming) != hipSuccess) {
+      hipHostFree(c->ring);
+      c->ring = nullptr;
+    }
+  if (!c->ring) c->ring_failed = true;
+  return c->ring != nullptr;
+}
+// the pieces cut at ring-half boundaries: chunk j = the pieces' bytes [j H, (j + 1) H)
+template <class F>
+void for_chunks(const Piece *ps, size_t k, F fn) {
+  std::vector<Piece> cur;
+  uint64_t fill = 0;
+  for (size_t i = 0; i < k; i++) {
+    uint64_t off = 0;
+    while (off < ps[i].n) {
+      const uint64_t take = std::min(ps[i].n - off, kRingHalf - fill);
+      cur.push_back(Piece{ps[i].dst + off, ps[i].src + off, take});
+      off += take;
+      fill += take;
+      if (fill == kRingHalf) {
+        fn(cur, fill);
+        cur.clear();
+        fill = 0;
+      }
+    }
+  }
+  if (fill) fn(cur, fill);
+}
+}  // namespace
+
+// host -> device: ps[i].src host, ps[i].dst device; asynchronous on st (returns once every
+// source byte is in the ring: the caller may reuse its buffers)
+int mib::ctx_upload(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
+  hipStream_t st = (hipStream_t)stream;
+  uint64_t total = 0;
+  for (size_t i = 0; i < k; i++) total += ps[i].n;
+  if (total < kParCopyMin || !ring_ready(c)) {   // small: pageable copies
+    for (size_t i = 0; i < k; i++)
+      if (ps[i].n && hipMemcpyAsync(ps[i].dst, ps[i].src, ps[i].n, hipMemcpyHostToDevice, st) != hipSuccess) return MIB_E_NO_DEVICE;
+    return 0;
+  }
+  int h = 0, rc = 0;
+  for_chunks(ps, k, [&](const std::vector<Piece> &ch, uint64_t) {
+    if (rc) return;
+    if (hipEventSynchronize(c->ring_ev[h]) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }   // the half's last copies are done
+    uint8_t *pin = c->ring + (uint64_t)h * kRingHalf;
+    std::vector<Piece> hc;
+    uint64_t po = 0;
+    for (const Piece &p : ch) {
+      hc.push_back(Piece{pin + po, p.src, p.n});
+      po += p.n;
+    }
+    par_copy(hc);
+    po = 0;
+    for (const Piece &p : ch) {
+      if (hipMemcpyAsync(p.dst, pin + po, p.n, hipMemcpyHostToDevice, st) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }
+      po += p.n;
+    }
+    if (hipEventRecord(c->ring_ev[h], st) != hipSuccess) rc = MIB_E_NO_DEVICE;
+    h ^= 1;
+  });
+  return rc;
+}
+// device -> host: ps[i].src device (written by work queued on st), ps[i].dst host; returns
+// when every byte has arrived
+int mib::ctx_download(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
+  hipStream_t st = (hipStream_t)stream;
+  uint64_t total = 0;
+  for (size_t i = 0; i < k; i++) total += ps[i].n;
+  if (total < kParCopyMin || !ring_ready(c)) {
+    for (size_t i = 0; i < k; i++)
+      if (ps[i].n && hipMemcpyAsync(ps[i].dst, ps[i].src, ps[i].n, hipMemcpyDeviceToHost, st) != hipSuccess) return MIB_E_NO_DEVICE;
+    return hipStreamSynchronize(st) == hipSuccess ? 0 : MIB_E_NO_DEVICE;
+  }
+  int h = 0, rc = 0;
+  std::vector<Piece> pending;   // the previous chunk: ring -> host once its copies are done
+  int ph = 0;
+  auto drain = [&]() {
+    if (pending.empty() || rc) return;
+    if (hipEventSynchronize(c->ring_ev[ph]) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }
+    par_copy(pending);
+    pending.clear();
+  };
+  for_chunks(ps, k, [&](const std::vector<Piece> &ch, uint64_t) {
+    if (rc) return;
+    uint8_t *pin = c->ring + (uint64_t)h * kRingHalf;
+    std::vector<Piece> out;
+    uint64_t po = 0;
+    for (const Piece &p : ch) {
+      if (hipMemcpyAsync(pin + po, p.src, p.n, hipMemcpyDeviceToHost, st) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }
+      out.push_back(Piece{p.dst, pin + po, p.n});
+      po += p.n;
+    }
+    if (hipEventRecord(c->ring_ev[h], st) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }
+    drain();   // the other half, while this one is in flight
+    pending = std::move(out);
+    ph = h;
+    h ^= 1;
+  });
+  drain();
+  return rc;
+}
 
 namespace {
 
@@ -465,7 +619,11 @@ int mib_buf_from_device(mib_buf *out, const void *d_src, uint64_t len) {
   out->size = 0;
   if (!out->data) return MIB_E_OUT_OF_MEMORY;
   out->size = len;
-  if (len && hipMemcpy(out->data, d_src, len, hipMemcpyDeviceToHost) != hipSuccess) {
+  // (called with the default context held: its stream produced d_src; large results go
+  // through its pinned ring)
+  mib_ctx *c = default_ctx();
+  const mib::HostPiece p{out->data, (const uint8_t *)d_src, len};
+  if (len && (!c || mib::ctx_download(c, c->stream, &p, 1) != 0)) {
     mib_buf_free(out);
     return MIB_E_NO_DEVICE;
   }
@@ -491,14 +649,21 @@ static int bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const
     hi = std::max(hi, d_src[i] + len[i]);
     sum += len[i];
   }
-  // large results: one copy each, straight into the result buffer; many small ones: one copy
-  // of the span that holds them all, then host copies (a copy call costs ~10 us)
-  if (sum / k >= (256u << 10) || (uint64_t)(hi - lo) > 4 * sum + (1u << 20)) {
+  // large results: through the default context's pinned ring, straight into the result
+  // buffers; many small ones: one copy of the span that holds them all, then host copies (a
+  // copy call costs ~10 us)
+  if (sum >= (4u << 20) || (uint64_t)(hi - lo) > 4 * sum + (1u << 20)) {
+    mib_ctx *c = default_ctx();
+    if (!c) return MIB_E_NO_DEVICE;
+    std::vector<mib::HostPiece> ps;
     for (size_t i = 0; i < k; i++) {
-      const int rc = mib_buf_from_device(outs[i], d_src[i], len[i]);
-      if (rc) return rc;
+      outs[i]->data = mib_buf_alloc(len[i]);
+      outs[i]->size = 0;
+      if (!outs[i]->data) return MIB_E_OUT_OF_MEMORY;
+      outs[i]->size = len[i];
+      if (len[i]) ps.push_back(mib::HostPiece{outs[i]->data, d_src[i], len[i]});
     }
-    return 0;
+    return mib::ctx_download(c, c->stream, ps.data(), ps.size());
   }
   std::vector<uint8_t> host(hi - lo);
   if (hipMemcpy(host.data(), lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
@@ -574,6 +739,9 @@ void mib_ctx_free(mib_ctx *c) {
   for (int i = 0; i < kStageSlots; i++)
     if (c->stage[i]) hipFree(c->stage[i]);
   if (c->enc_ws) mib_encode_ws_free(c->enc_ws);
+  if (c->ring) hipHostFree(c->ring);
+  for (int h = 0; h < 2; h++)
+    if (c->ring_ev[h]) hipEventDestroy(c->ring_ev[h]);
   if (c->stream) hipStreamDestroy(c->stream);
   for (int l = 0; l < kEncLanes; l++) {
     if (c->lane_ws[l]) mib_encode_ws_free(c->lane_ws[l]);
@@ -602,8 +770,16 @@ constexpr uint64_t kKeepScratch = 1ull << 30;     // decoder scratch, part table
 int g_default_depth = 0;                          // (guarded by g_default_mu)
 extern "C" void mib_encode_ws_trim(void **ws, uint64_t keep);
 extern "C" int mib_live_encoders(void);
-static void release_large(uint8_t **p, uint64_t *cap, uint64_t keep) {
-  if (*p && *cap > keep) {
+// Hysteresis: a buffer above its keep size is released only once kQuietCalls trims in a row
+// saw calls that needed no more than that -- a service whose every call is large keeps its
+// buffers (a hipFree syncs the device and a fresh hipMalloc of GiBs costs more than the call:
+// the r04 host-batch legs varied by 2 s from it), one large call among
+// small ones gives its memory back a few calls later.
+constexpr int kQuietCalls = 4;
+static void release_large(uint8_t **p, uint64_t *cap, uint64_t keep, mib_ctx::Trim &tr) {
+  tr.quiet = tr.need > keep ? 0 : tr.quiet + 1;
+  tr.need = 0;
+  if (*p && *cap > keep && tr.quiet >= kQuietCalls) {
     hipFree(*p);
     *p = nullptr;
     *cap = 0;
@@ -615,9 +791,9 @@ static void trim_default_ctx(mib_ctx *c) {
   // output stage: kept)
   const bool streaming = mib_live_encoders() > 0;
   for (int i = 0; i < kStageSlots; i++)
-    if (!(streaming && i == 3)) release_large(&c->stage[i], &c->stage_cap[i], kKeepStage);
-  release_large(&c->d_scratch, &c->scratch_bytes, kKeepScratch);
-  release_large(&c->d_parts, &c->parts_bytes, kKeepScratch);
+    if (!(streaming && i == 3)) release_large(&c->stage[i], &c->stage_cap[i], kKeepStage, c->stage_trim[i]);
+  release_large(&c->d_scratch, &c->scratch_bytes, kKeepScratch, c->scratch_trim);
+  release_large(&c->d_parts, &c->parts_bytes, kKeepScratch, c->parts_trim);
   if (!streaming) {
     mib_encode_ws_trim(&c->enc_ws, kKeepScratch);
     for (int l = 0; l < kEncLanes; l++) mib_encode_ws_trim(&c->lane_ws[l], kKeepScratch);
@@ -627,9 +803,9 @@ static void trim_default_ctx(mib_ctx *c) {
 // encoder workspace), released (multi.cpp's shard contexts after each sharded call)
 void mib_ctx_trim(mib_ctx *c, uint64_t keep_stage, uint64_t keep_scratch) {
   hipSetDevice(c->device);
-  for (int i = 0; i < kStageSlots; i++) release_large(&c->stage[i], &c->stage_cap[i], keep_stage);
-  release_large(&c->d_scratch, &c->scratch_bytes, keep_scratch);
-  release_large(&c->d_parts, &c->parts_bytes, keep_scratch);
+  for (int i = 0; i < kStageSlots; i++) release_large(&c->stage[i], &c->stage_cap[i], keep_stage, c->stage_trim[i]);
+  release_large(&c->d_scratch, &c->scratch_bytes, keep_scratch, c->scratch_trim);
+  release_large(&c->d_parts, &c->parts_bytes, keep_scratch, c->parts_trim);
   mib_encode_ws_trim(&c->enc_ws, keep_scratch);
   for (int l = 0; l < kEncLanes; l++) mib_encode_ws_trim(&c->lane_ws[l], keep_scratch);
 }
@@ -673,6 +849,7 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
   static const size_t grid_cap = mib::knob("MIB_DEC_GRID") ? (size_t)std::max(1, atoi(mib::knob("MIB_DEC_GRID"))) : 2048;
   int grid = (int)std::min<size_t>(k, std::min<size_t>(grid_cap, 2048));
   int rc;
+  c->scratch_trim.need = std::max(c->scratch_trim.need, per_block * (uint64_t)grid);
   if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
   if (k > c->jobs_cap) {
     if (c->d_jobs) hipFree(c->d_jobs);
@@ -727,6 +904,7 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
   const uint64_t pos_b = (((ne + ps.size()) * 8) + 255) & ~255ull;
   const uint64_t prog_b = ((ne * 8) + 255) & ~255ull;
   int rc;
+  c->parts_trim.need = std::max(c->parts_trim.need, ent_b + pos_b + prog_b + 256);
   if ((rc = grow((void **)&c->d_parts, &c->parts_bytes, ent_b + pos_b + prog_b + 256)) != 0) return rc;
   mib::PartEntry *d_ent = reinterpret_cast<mib::PartEntry *>(c->d_parts);
   int64_t *d_pos = reinterpret_cast<int64_t *>(c->d_parts + ent_b);
@@ -770,6 +948,7 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
   uint64_t per_block = mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4 + 3092 * 4;
   per_block = (per_block + 255) & ~(uint64_t)255;
   const int grid = (int)std::min<size_t>(nj, 2048);
+  c->scratch_trim.need = std::max(c->scratch_trim.need, per_block * (uint64_t)grid);
   if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
   if (nj > c->jobs_cap) {
     if (c->d_jobs) hipFree(c->d_jobs);
@@ -912,10 +1091,10 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
   uint8_t *d_in = nullptr, *d_out = nullptr, *d_dict = nullptr;
   int rc = 0;
   if (!(d_in = mib_ctx_stage(c, 0, n + 16))) return MIB_E_OUT_OF_MEMORY;
-  if (n) hipMemcpy(d_in, in, n, hipMemcpyHostToDevice);
-  if (dict) {
-    if (!(d_dict = mib_ctx_stage(c, 2, dict_n + 16))) return MIB_E_OUT_OF_MEMORY;
-    if (dict_n) hipMemcpy(d_dict, dict, dict_n, hipMemcpyHostToDevice);
+  if (dict && !(d_dict = mib_ctx_stage(c, 2, dict_n + 16))) return MIB_E_OUT_OF_MEMORY;
+  {
+    const mib::HostPiece up[2] = {{d_in, in, n}, {d_dict, dict, dict ? dict_n : 0}};
+    if ((rc = mib::ctx_upload(c, c->stream, up, dict ? 2 : 1))) return rc;
   }
   if (exact_out < 0) {   // a stream with a part index: part-parallel, checked
     PartPlan plan;
@@ -990,9 +1169,13 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
   }
   uint8_t *d_in = mib_ctx_stage(c, 0, ioff[k] + 16), *d_out = mib_ctx_stage(c, 1, ooff[k] + 64);
   if (!d_in || !d_out) return MIB_E_OUT_OF_MEMORY;
-  for (size_t i = 0; i < k; i++)
-    if (in[i].size) hipMemcpy(d_in + ioff[i], in[i].data, in[i].size, hipMemcpyHostToDevice);
   int rc = 0;
+  {
+    std::vector<mib::HostPiece> up;
+    for (size_t i = 0; i < k; i++)
+      if (in[i].size) up.push_back(mib::HostPiece{d_in + ioff[i], in[i].data, in[i].size});
+    if ((rc = mib::ctx_upload(c, c->stream, up.data(), up.size()))) return rc;
+  }
   for (size_t i = 0; i < k; i++) out[i].data = nullptr, out[i].size = 0;
   // exact input lengths, padded slots
   std::vector<mib::DecJob> jobs(k);

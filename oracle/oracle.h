@@ -25,6 +25,9 @@ int oracle_decode_probe(const uint8_t *in, size_t n, const uint64_t *pos, size_t
 /* static-dictionary word references decoded so far by this process (test instrumentation) */
 uint64_t oracle_word_refs(void);
 uint64_t oracle_compound_refs(void);
+/* out[4]: the copies decoded on this thread since the last call, by distance code: implicit
+ * (command code < 128), explicit code 0, short codes 1-15, explicit distances (>= 16) */
+void oracle_dist_code_counts(uint64_t *out);
 
 /* encode.ts:50 brotliEncode (bugs A,B fixed = the survey's "ref-fixed"; C,E fixed too).
  * quality 0..11, lgwin 10..24, mode 0 GENERIC / 1 TEXT / 2 FONT. */

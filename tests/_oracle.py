@@ -90,6 +90,14 @@ def compound_refs():
     return lib().oracle_compound_refs()
 
 
+def dist_code_counts():
+    """copies the oracle decoder has decoded on this thread since the last call, by distance
+    code: [implicit (command code < 128), code 0, short codes 1-15, explicit distances]"""
+    out = (ctypes.c_uint64 * 4)()
+    lib().oracle_dist_code_counts(out)
+    return list(out)
+
+
 def probe(data, positions):
     """decoder states (parts.h PartEntry layout) at the given ascending output positions:
     the command starting there, or the metablock header starting there (flags bit 2)."""

@@ -1,0 +1,52 @@
+"""The parse prices the distance cache (backward-references-hq.ts:309-345).
+
+Record-structured input -- each 48-byte record repeats the one one or two records back with a
+couple of bytes changed, as glyph records do -- makes the cheapest parse reuse the record
+stride: after a changed byte (a literal) the copy from the same distance as the copy before it
+is a last-distance copy (RFC 7932 distance code 0, implicit in command codes < 128), and a copy
+from the other stride is a short code 1-15.  The parse's last-distance candidates (dp_kernel KR,
+FONT mode) and the near scan's 2-3 byte copies (GENERIC / TEXT) must choose them: the oracle
+decoder (the reference decoder restated) counts the distance codes of the GPU's stream, and the
+stream round-trips through the oracle and the HIP decoder.
+"""
+import random
+
+import pytest
+
+import _oracle
+import brotli_amd
+
+pytestmark = pytest.mark.gpu
+
+
+def records(n, seed, rec=48):
+    rng = random.Random(seed)
+    out = bytearray(rng.getrandbits(8) for _ in range(2 * rec))
+    while len(out) < n:
+        back = rec if rng.random() < 0.7 else 2 * rec
+        r = bytearray(out[len(out) - back:len(out) - back + rec])
+        for _ in range(rng.randrange(1, 4)):
+            r[rng.randrange(rec)] = rng.getrandbits(8)
+        out += r
+    return bytes(out[:n])
+
+
+@pytest.mark.parametrize('mode', [brotli_amd.EncoderMode.FONT, brotli_amd.EncoderMode.GENERIC])
+def test_record_stride_parse_uses_the_distance_cache(mode):
+    data = records(200000, 7)
+    enc = brotli_amd.brotliEncode(data, {'quality': 11, 'mode': mode})
+    _oracle.dist_code_counts()
+    assert _oracle.decode(enc) == data
+    implicit, code0, short, explicit = _oracle.dist_code_counts()
+    copies = implicit + code0 + short + explicit
+    print('mode %d: %d copies: implicit %d, code 0 %d, short 1-15 %d, explicit %d; %d bytes' %
+          (mode, copies, implicit, code0, short, explicit, len(enc)))
+    assert brotli_amd.brotliDecode(enc) == data
+    # the strides come back through the cache, not as explicit distances
+    assert implicit + code0 > copies // 2
+    assert short > 0
+    assert explicit < copies // 4
+    # and the stream is far smaller than ref-fixed's on the same bytes
+    ref = _oracle.encode(data[:60000], 11, 22, 2 if mode == brotli_amd.EncoderMode.FONT else 0)
+    ours = brotli_amd.brotliEncode(data[:60000], {'quality': 11, 'mode': mode})
+    assert len(ours) < len(ref)
