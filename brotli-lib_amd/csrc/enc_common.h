@@ -136,7 +136,7 @@ struct Seg {
   uint32_t carry_in;          // carry: literals owed by earlier segments of the metablock
   uint32_t prev_dist;         // carry: the decoder's last distance when the segment starts
   uint32_t extra_ins;         // carry: trailing insert-only command of the metablock (0: none)
-  uint32_t pad;
+  uint32_t pieces;            // its parse pieces: first piece index << 3 | log2 of their count
   uint32_t ring_in[4];        // ring_scan: the decoder's distance ring at the segment start, most recent first
   uint64_t bit_off;           // offsets: stream-relative bit position
   uint64_t bits;              // sizes
@@ -330,23 +330,44 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Serial LSB-first bit writer into a zeroed byte buffer (headers, prefix codes).
+// Serial LSB-first bit writer into a zeroed byte buffer (headers, prefix codes).  Bits gather
+// in a register and reach the buffer 32 at a time (OR'ed bytewise: the start need not be byte
+// aligned); the rest at flush() or when the writer goes out of scope -- read the buffer after
+// either.  (Byte read-modify-writes per put were most of a single metablock's header and tree
+// time, r05o.)
 struct BitW {
   uint8_t *buf;
-  uint64_t pos;
+  uint64_t pos;        // bits written, the pending ones included
+  uint64_t acc = 0;    // pending bits; the first lands at bit pos - nacc
+  int nacc = 0;
+  __device__ void emit(uint64_t p0, uint32_t v, int n) {   // OR n <= 32 bits of v in at bit p0
+    uint8_t *b = buf + (p0 >> 3);
+    const int sh = (int)(p0 & 7);
+    const uint64_t x = (uint64_t)v << sh;
+    const int nb = (sh + n + 7) >> 3;
+    for (int i = 0; i < nb; i++) b[i] |= (uint8_t)(x >> (8 * i));
+  }
   __device__ void put(int nbits, uint64_t v) {
     while (nbits > 0) {
-      int k = nbits < 32 ? nbits : 32;
-      uint64_t vv = v & ((1ull << k) - 1);
-      uint64_t word = vv << (pos & 7);
-      uint8_t *b = buf + (pos >> 3);
-      int nb = (int)(((pos & 7) + k + 7) >> 3);
-      for (int i = 0; i < nb; i++) b[i] |= (uint8_t)(word >> (8 * i));
+      const int k = nbits < 32 ? nbits : 32;
+      acc |= (v & ((1ull << k) - 1)) << nacc;
+      nacc += k;
       pos += k;
       v >>= k;
       nbits -= k;
+      if (nacc >= 32) {
+        emit(pos - nacc, (uint32_t)acc, 32);
+        acc >>= 32;
+        nacc -= 32;
+      }
     }
   }
+  __device__ void flush() {
+    if (nacc) emit(pos - nacc, (uint32_t)acc, nacc);
+    acc = 0;
+    nacc = 0;
+  }
+  __device__ ~BitW() { flush(); }
 };
 
 // encodeWindowBits (bit-writer.ts:172-194)
@@ -461,8 +482,8 @@ void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, cons
                const uint32_t *matches, uint64_t *choice, bool cdict, bool font);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
-void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces);
-void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw);
+void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, Seg *pieces);
+void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, RawCmd *raw);
 void launch_rep(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const CostModel *model, RawCmd *raw, uint32_t *cnts);
 size_t sort_ws_bytes(uint32_t total);
 void launch_sort(hipStream_t st, const Job *jobs, const uint32_t *pos_job, int njobs, uint32_t total, int hb, void *ws,

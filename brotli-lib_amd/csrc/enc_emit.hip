@@ -47,20 +47,41 @@ struct Acc {   // lane-private bit accumulator writing 32-bit words; edge words 
 
 
 // metablock header (with its context maps) + its prefix codes in stream order: literal
-// clusters, command code, distance clusters.  Lane per metablock.
-__global__ void headers_kernel(const Job *jobs, const Mb *mbs, int nmbs, const uint8_t *hdr, const uint8_t *trees,
-                               uint8_t *out) {
-  int m = blockIdx.x * blockDim.x + threadIdx.x;
+// clusters, command code, distance clusters.  Wave per metablock: part 0 is the header, part
+// k + 1 tree slot k; lane l copies the parts [l P, (l + 1) P) to their bit offsets (a wave
+// scan of the part sizes), its own contiguous range of the output (edge words atomicOr'ed).
+// (One lane per metablock copied ~3 KiB bit by bit: 0.2 ms for a single metablock, r05m.)
+constexpr int kHdrParts = kTreeSlots + 1;
+constexpr int kHdrPer = (kHdrParts + 63) / 64;
+__global__ __launch_bounds__(64) void headers_kernel(const Job *jobs, const Mb *mbs, int nmbs, const uint8_t *hdr,
+                                                     const uint8_t *trees, uint8_t *out) {
+  const int m = blockIdx.x, lane = threadIdx.x;
   if (m >= nmbs) return;
   const Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
+  auto bits_of = [&](int part) -> uint64_t { return part >= kHdrParts ? 0u : part == 0 ? mb.hdr_bits : mb.tree_bits[part - 1]; };
+  uint64_t mine = 0;
+#pragma unroll
+  for (int q = 0; q < kHdrPer; q++) mine += bits_of(lane * kHdrPer + q);
+  uint64_t incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (!mine) return;
   Acc a;
-  a.init(reinterpret_cast<uint32_t *>(out + jb.out_off), mb.bit_off);
-  for (int part = -1; part < kTreeSlots; part++) {
-    const uint8_t *src = part < 0 ? hdr + (size_t)m * kHdrBytes : trees + ((size_t)m * kTreeSlots + part) * kTreeBytes;
-    const uint64_t nbits = part < 0 ? mb.hdr_bits : mb.tree_bits[part];
+  a.init(reinterpret_cast<uint32_t *>(out + jb.out_off), mb.bit_off + incl - mine);
+  for (int q = 0; q < kHdrPer; q++) {
+    const int part = lane * kHdrPer + q;
+    const uint64_t nbits = bits_of(part);
+    if (!nbits) continue;
+    const uint8_t *src = part == 0 ? hdr + (size_t)m * kHdrBytes : trees + ((size_t)m * kTreeSlots + part - 1) * kTreeBytes;
     uint64_t i = 0;
+    for (; i + 32 <= nbits; i += 32)
+      a.put(32, (uint32_t)src[i >> 3] | ((uint32_t)src[(i >> 3) + 1] << 8) | ((uint32_t)src[(i >> 3) + 2] << 16) |
+                    ((uint32_t)src[(i >> 3) + 3] << 24));
     for (; i + 8 <= nbits; i += 8) a.put(8, src[i >> 3]);
     if (i < nbits) a.put((int)(nbits - i), src[i >> 3]);
   }
@@ -359,7 +380,7 @@ __global__ void pack_kernel(const Job *jobs, const uint64_t *dst_off, const uint
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint8_t *trees, const uint8_t *hdr,
                  uint8_t *out) {
-  hipLaunchKernelGGL(headers_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, trees, out);
+  if (nmbs) hipLaunchKernelGGL(headers_kernel, dim3(nmbs), dim3(64), 0, st, jobs, mbs, nmbs, hdr, trees, out);
   hipLaunchKernelGGL(emit_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, out);
 }
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out) {

@@ -82,40 +82,62 @@ __global__ __launch_bounds__(64) void carry_kernel(Job *jobs, int njobs, Seg *se
 // at q >= 10 UTF8 contexts when at least 3/4 of the metablock's first kCtxScan bytes parse as
 // UTF-8, else SIGNED; below q10 UTF8.  The reference's picks cost C4 1.4 % (it took SIGNED for
 // enwik-style text: 0.36997 vs 0.36469 with UTF8) and fonts 0.5 % (LSB6 vs SIGNED).
-// Lane per metablock.  Values: 0 LSB6, 1 MSB6, 2 UTF8, 3 SIGNED (RFC 7932 section 7.1).
+// Values: 0 LSB6, 1 MSB6, 2 UTF8, 3 SIGNED (RFC 7932 section 7.1).  Block (one wave) per
+// metablock: the first kCtxScan bytes are staged in LDS and lane t parses bytes [64 t, 64 t + 64)
+// from each of the four offsets a parse can enter them at (a sequence is at most 4 bytes);
+// lane 0 then chains the 64 pieces from offset 0 -- the serial parse's count exactly (one lane
+// parsing 4 KiB of global bytes took 0.4 ms per metablock, r05m).
 constexpr int kCtxScan = 4096;
-__global__ void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs, int force) {
-  int m = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ int utf8_step(const uint8_t *d, int i, int len, int *ok) {   // BrotliParseAsUTF8
+  const int b0 = d[i];
+  int n = 1;
+  *ok = 0;
+  if (b0 < 0x80) {
+    *ok = 1;
+  } else if ((b0 & 0xE0) == 0xC0 && i + 1 < len && (d[i + 1] & 0xC0) == 0x80) {
+    n = 2;
+    *ok = (((b0 & 0x1F) << 6) | (d[i + 1] & 0x3F)) >= 0x80;
+  } else if ((b0 & 0xF0) == 0xE0 && i + 2 < len && (d[i + 1] & 0xC0) == 0x80 && (d[i + 2] & 0xC0) == 0x80) {
+    n = 3;
+    *ok = (((b0 & 0x0F) << 12) | ((d[i + 1] & 0x3F) << 6) | (d[i + 2] & 0x3F)) >= 0x800;
+  } else if ((b0 & 0xF8) == 0xF0 && i + 3 < len && (d[i + 1] & 0xC0) == 0x80 && (d[i + 2] & 0xC0) == 0x80 &&
+             (d[i + 3] & 0xC0) == 0x80) {
+    n = 4;
+    const int v = ((b0 & 0x07) << 18) | ((d[i + 1] & 0x3F) << 12) | ((d[i + 2] & 0x3F) << 6) | (d[i + 3] & 0x3F);
+    *ok = v >= 0x10000 && v <= 0x10FFFF;
+  }
+  return *ok ? n : 1;
+}
+__global__ __launch_bounds__(64) void context_mode_kernel(const Job *jobs, Mb *mbs, int nmbs, int force) {
+  __shared__ uint8_t d[kCtxScan];
+  __shared__ uint16_t cnt[64][4];
+  __shared__ uint8_t nxt[64][4];
+  const int m = blockIdx.x, t = threadIdx.x;
   if (m >= nmbs) return;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
-  const uint8_t *d = jb.data + mb.start;
+  const uint8_t *src = jb.data + mb.start;
   const int len = (int)min(mb.end - mb.start, (uint32_t)kCtxScan);
-  int valid = 0;
-  for (int i = 0; i < len;) {   // BrotliParseAsUTF8: bytes of well-formed sequences
-    const int b0 = d[i];
-    int n = 1, ok = 0;
-    if (b0 < 0x80) {
-      ok = 1;
-    } else if ((b0 & 0xE0) == 0xC0 && i + 1 < len && (d[i + 1] & 0xC0) == 0x80) {
-      n = 2;
-      ok = (((b0 & 0x1F) << 6) | (d[i + 1] & 0x3F)) >= 0x80;
-    } else if ((b0 & 0xF0) == 0xE0 && i + 2 < len && (d[i + 1] & 0xC0) == 0x80 && (d[i + 2] & 0xC0) == 0x80) {
-      n = 3;
-      ok = (((b0 & 0x0F) << 12) | ((d[i + 1] & 0x3F) << 6) | (d[i + 2] & 0x3F)) >= 0x800;
-    } else if ((b0 & 0xF8) == 0xF0 && i + 3 < len && (d[i + 1] & 0xC0) == 0x80 && (d[i + 2] & 0xC0) == 0x80 &&
-               (d[i + 3] & 0xC0) == 0x80) {
-      n = 4;
-      const int v = ((b0 & 0x07) << 18) | ((d[i + 1] & 0x3F) << 12) | ((d[i + 2] & 0x3F) << 6) | (d[i + 3] & 0x3F);
-      ok = v >= 0x10000 && v <= 0x10FFFF;
-    }
-    if (ok) {
-      valid += n;
+  for (int i = t; i < len; i += 64) d[i] = src[i];
+  __syncthreads();
+  const int c0 = 64 * t, c1 = min(c0 + 64, len);
+  for (int e = 0; e < 4; e++) {
+    int i = c0 + e, valid = 0, ok;
+    while (i < c1) {
+      const int n = utf8_step(d, i, len, &ok);
+      valid += ok ? n : 0;
       i += n;
-    } else {
-      i++;
     }
+    cnt[t][e] = (uint16_t)valid;
+    nxt[t][e] = (uint8_t)(i - c1);   // (0..3: where the parse enters the next piece)
+  }
+  __syncthreads();
+  if (t) return;
+  int valid = 0, e = 0;
+  for (int q = 0; 64 * q < len; q++) {
+    valid += cnt[q][e];
+    e = nxt[q][e];
   }
   const int mode = !jb.hq || 4 * valid > 3 * len ? 2 : 3;
   mb.ctx_mode = (uint32_t)(force >= 0 ? force : mode);
@@ -922,11 +944,16 @@ __device__ void store_code(BitW &w, int n, const int16_t *nzs, int max_bits, uin
   store_code(w, n, nzs, max_bits, depth, code, asize, ts, false);
 }
 
-// serial length-limited Huffman depths for small alphabets (<= 80 symbols)
-__device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *depth) {
+// serial length-limited Huffman depths for small alphabets (<= 80 symbols); the work arrays
+// in `ws` (LDS in the header kernel: private arrays indexed by data live in scratch memory)
+struct SerialWs {
   int16_t sorted[80];
   uint32_t cnt[2 * 80 + 2];
   int16_t left[2 * 80 + 2], val[2 * 80 + 2];
+};
+__device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *depth, SerialWs &ws) {
+  int16_t *sorted = ws.sorted, *left = ws.left, *val = ws.val;
+  uint32_t *cnt = ws.cnt;
   for (int i = 0; i < len; i++) depth[i] = 0;
   int n = 0;
   for (int i = len - 1; i >= 0; i--)
@@ -957,6 +984,10 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
     if (ok) return;
     for (int i = 0; i < len; i++) depth[i] = 0;
   }
+}
+__device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *depth) {
+  SerialWs ws;
+  serial_depths(h, len, limit, depth, ws);
 }
 
 // Block (one wave) per (metablock, code slot): literal (block type, cluster), command (block
@@ -1701,19 +1732,40 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
 // encodeContextMap (context-map.ts:114-170): NTREES, then (NTREES > 1) move-to-front, runs
 // of zeros as RLEMAX-prefixed run codes, a prefix code over NTREES + RLEMAX symbols, and the
 // IMTF bit (RFC 7932 section 7.3).  Serial, one lane.
-__device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int ntrees) {
+struct CmapWs {   // encode_context_map's work arrays (LDS)
+  uint8_t mtf[kMaxLitTrees];
+  uint8_t v[kLitSlots], sym[kLitSlots], nb[kLitSlots];
+  uint16_t ex[kLitSlots];
+  uint32_t hist[kMaxLitTrees + 16];
+  uint8_t depth[kMaxLitTrees + 16];
+  uint16_t code[kMaxLitTrees + 16];
+  int16_t nzs[kMaxLitTrees + 16];
+  SerialWs sw;
+  TreeScratch ts;
+};
+// The move-to-front transform of a context map by the wave (all 64 lanes): lane l holds list
+// entry l; per entry one ballot finds the value's place and one shuffle moves the ones before it
+// back (~10 instructions, against ~10 dependent LDS round trips of the serial list walk).
+__device__ void mtf_wave(const uint8_t *cmap, int size, uint8_t *v) {
+  const int lane = threadIdx.x & 63;
+  int m = lane;
+  for (int i = 0; i < size; i++) {
+    const int c = cmap[i];
+    const uint64_t hit = __ballot(m == c);
+    const int idx = __ffsll((unsigned long long)hit) - 1;
+    if (lane == 0) v[i] = (uint8_t)idx;
+    const int prev = __shfl_up(m, 1);
+    m = lane == 0 ? c : lane <= idx ? prev : m;
+  }
+}
+// (v: the context map's move-to-front values, mtf_wave)
+__device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int ntrees, CmapWs &ws) {
   put_varlen_u8(w, ntrees - 1);
   if (ntrees <= 1) return;
-  uint8_t mtf[kMaxLitTrees];
-  for (int i = 0; i < ntrees; i++) mtf[i] = (uint8_t)i;
-  uint8_t v[kLitSlots];
-  for (int i = 0; i < size; i++) {
-    int idx = 0;
-    while (mtf[idx] != cmap[i]) idx++;
-    v[i] = (uint8_t)idx;
-    for (int k = idx; k > 0; k--) mtf[k] = mtf[k - 1];
-    mtf[0] = cmap[i];
-  }
+  uint8_t *v = ws.v, *sym = ws.sym, *nb = ws.nb, *depth = ws.depth;
+  uint16_t *ex = ws.ex, *code = ws.code;
+  uint32_t *hist = ws.hist;
+  int16_t *nzs = ws.nzs;
   int maxrun = 0;
   for (int i = 0; i < size;) {
     int r = 0;
@@ -1724,8 +1776,6 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
   int rlemax = 0;
   while ((2 << rlemax) <= maxrun && rlemax < 16) rlemax++;   // largest p with 2^p <= maxrun
   // symbols (code, extra bits, extra)
-  uint8_t sym[kLitSlots], nb[kLitSlots];
-  uint16_t ex[kLitSlots];
   int ns = 0;
   for (int i = 0; i < size;) {
     if (v[i] != 0) {
@@ -1756,21 +1806,17 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
     }
   }
   const int asize = ntrees + rlemax;
-  uint32_t hist[kMaxLitTrees + 16];
   for (int i = 0; i < asize; i++) hist[i] = 0;
   for (int k = 0; k < ns; k++) hist[sym[k]]++;
   w.put(1, rlemax > 0 ? 1 : 0);
   if (rlemax) w.put(4, (uint32_t)(rlemax - 1));
-  uint8_t depth[kMaxLitTrees + 16];
-  uint16_t code[kMaxLitTrees + 16];
-  int16_t nzs[kMaxLitTrees + 16];
   int n = 0;
   for (int i = 0; i < asize; i++)
     if (hist[i]) nzs[n++] = (int16_t)i;
-  serial_depths(hist, asize, 15, depth);
+  serial_depths(hist, asize, 15, depth, ws.sw);
   int max_bits = 0;
   for (int c = asize - 1; c; c >>= 1) max_bits++;
-  store_code(w, n, nzs, max_bits, depth, code, asize);
+  store_code(w, n, nzs, max_bits, depth, code, asize, ws.ts, false);
   for (int k = 0; k < ns; k++) {
     w.put(depth[sym[k]], code[sym[k]]);
     if (nb[k]) w.put(nb[k], ex[k]);
@@ -1780,66 +1826,91 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
 
 // NBLTYPES and, for a split category, its block type and block count prefix codes and the
 // first block count (storeBlockSwitch's header part, metablock.ts:150-220)
-__device__ void put_block_split(BitW &w, int nbt, uint8_t *td, uint16_t *tc, uint8_t *cdp, uint16_t *cc, uint32_t first) {
+__device__ void put_block_split(BitW &w, int nbt, uint8_t *td, uint16_t *tc, uint8_t *cdp, uint16_t *cc, uint32_t first,
+                                int16_t *nzs, TreeScratch &ts) {
   put_varlen_u8(w, nbt - 1);
   if (nbt <= 1) return;
-  int16_t nzs[26];
   int n = 0;
   const int ta = nbt + 2;
   for (int i = 0; i < ta; i++)
     if (td[i]) nzs[n++] = (int16_t)i;
   int mb_bits = 0;
   for (int c = ta - 1; c; c >>= 1) mb_bits++;
-  store_code(w, n, nzs, mb_bits, td, tc, ta);
+  store_code(w, n, nzs, mb_bits, td, tc, ta, ts, false);
   n = 0;
   for (int i = 0; i < 26; i++)
     if (cdp[i]) nzs[n++] = (int16_t)i;
-  store_code(w, n, nzs, 5, cdp, cc, 26);
+  store_code(w, n, nzs, 5, cdp, cc, 26, ts, false);
   const int bc = block_count_code(first);
   w.put(cdp[bc], cc[bc]);
   w.put((int)kBlkBits[bc], first - kBlkOff[bc]);
 }
 
-// The metablock header before the prefix codes, lane per metablock (storeMetaBlock's
-// header part, metablock.ts:690-705).
-__global__ void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hdr, Codes *codes) {
-  int m = blockIdx.x * blockDim.x + threadIdx.x;
+// The metablock header before the prefix codes (storeMetaBlock's header part,
+// metablock.ts:690-705).  Block (one wave) per metablock: the header is written serially by
+// lane 0 into LDS -- its bit writer's read-modify-write bytes and the context-map coder's work
+// arrays were global / scratch memory round trips, 0.8 ms for a single metablock (a 1 MiB
+// streaming chunk, r05m) -- then copied out by the wave.
+__global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hdr, Codes *codes) {
+  __shared__ uint8_t hb[kHdrBytes];
+  __shared__ uint8_t map[kLitSlots];
+  __shared__ int16_t nzs[26];
+  __shared__ int sh_n, sh_ntrees;
+  __shared__ CmapWs cws;
+  const int m = blockIdx.x;
   if (m >= nmbs) return;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
-  uint8_t *hb = hdr + (size_t)m * kHdrBytes;
-  for (int i = 0; i < kHdrBytes; i++) hb[i] = 0;
-  BitW w{hb, 0};
-  if (mb.start == 0 && jb.hdr_lgwin && !jb.parts) put_window_bits(w, (int)jb.hdr_lgwin);   // (else: part_index_kernel)
-  const uint32_t length = mb.end - mb.start;
-  w.put(1, mb.is_last);
-  if (mb.is_last) w.put(1, 0);
-  const int lg = length == 1 ? 1 : 32 - __clz(length - 1);
-  const int mn = (lg < 16 ? 16 : lg + 3) / 4;
-  w.put(2, (uint32_t)(mn - 4));
-  w.put(mn * 4, length - 1);
-  if (!mb.is_last) w.put(1, 0);
-  Codes &cd = codes[m];
-  for (int c = 0; c < 3; c++) put_block_split(w, (int)mb.nbt[c], cd.btd[c], cd.btc[c], cd.bcd[c], cd.bcc[c], mb.first_count[c]);
-  w.put(2, jb.npostfix);
-  w.put(4, jb.ndirect >> jb.npostfix);
-  for (uint32_t ty = 0; ty < mb.nbt[0]; ty++) w.put(2, mb.ctx_mode);
-  // context maps over dense code indices (slots of type ty start at the codes of the types before it)
-  uint8_t map[kLitSlots];
-  int base = 0;
-  for (uint32_t ty = 0; ty < mb.nbt[0]; ty++) {
-    for (int q = 0; q < kLitCtx; q++) map[ty * kLitCtx + q] = (uint8_t)(base + mb.lit_cmap[ty * kLitCtx + q] - ty * kLitCtx);
-    base += (int)mb.nlit_t[ty];
+  const int t = threadIdx.x;
+  for (int i = t; i < kHdrBytes; i += 64) hb[i] = 0;
+  wave_sync();
+  BitW w{hb, 0};   // (lane 0's)
+  if (t == 0) {
+    if (mb.start == 0 && jb.hdr_lgwin && !jb.parts) put_window_bits(w, (int)jb.hdr_lgwin);   // (else: part_index_kernel)
+    const uint32_t length = mb.end - mb.start;
+    w.put(1, mb.is_last);
+    if (mb.is_last) w.put(1, 0);
+    const int lg = length == 1 ? 1 : 32 - __clz(length - 1);
+    const int mn = (lg < 16 ? 16 : lg + 3) / 4;
+    w.put(2, (uint32_t)(mn - 4));
+    w.put(mn * 4, length - 1);
+    if (!mb.is_last) w.put(1, 0);
+    Codes &cd = codes[m];
+    for (int c = 0; c < 3; c++)
+      put_block_split(w, (int)mb.nbt[c], cd.btd[c], cd.btc[c], cd.bcd[c], cd.bcc[c], mb.first_count[c], nzs, cws.ts);
+    w.put(2, jb.npostfix);
+    w.put(4, jb.ndirect >> jb.npostfix);
+    for (uint32_t ty = 0; ty < mb.nbt[0]; ty++) w.put(2, mb.ctx_mode);
   }
-  encode_context_map(w, map, (int)mb.nbt[0] * kLitCtx, base);
-  base = 0;
-  for (uint32_t ty = 0; ty < mb.nbt[2]; ty++) {
-    for (int q = 0; q < kDistCtx; q++) map[ty * kDistCtx + q] = (uint8_t)(base + mb.dist_cmap[ty * kDistCtx + q] - ty * kDistCtx);
-    base += (int)mb.ndist_t[ty];
+  // the two context maps (literal, distance) over dense code indices: slots of type ty start at
+  // the codes of the types before it; each map's move-to-front by the wave, its coding by lane 0
+  for (int cat = 0; cat < 2; cat++) {
+    const int nty = (int)(cat == 0 ? mb.nbt[0] : mb.nbt[2]), nctx = cat == 0 ? kLitCtx : kDistCtx;
+    if (t == 0) {
+      int base = 0;
+      for (int ty = 0; ty < nty; ty++) {
+        for (int q = 0; q < nctx; q++)
+          map[ty * nctx + q] = (uint8_t)(base + (cat == 0 ? mb.lit_cmap[ty * kLitCtx + q] - ty * kLitCtx
+                                                          : mb.dist_cmap[ty * kDistCtx + q] - ty * kDistCtx));
+        base += (int)(cat == 0 ? mb.nlit_t[ty] : mb.ndist_t[ty]);
+      }
+      sh_n = nty * nctx;
+      sh_ntrees = base;
+    }
+    wave_sync();
+    if (sh_ntrees > 1) mtf_wave(map, sh_n, cws.v);
+    wave_sync();
+    if (t == 0) encode_context_map(w, map, sh_n, sh_ntrees, cws);
+    wave_sync();
   }
-  encode_context_map(w, map, (int)mb.nbt[2] * kDistCtx, base);
-  mb.hdr_bits = (uint32_t)w.pos;
+  if (t == 0) {
+    w.flush();
+    mb.hdr_bits = (uint32_t)w.pos;
+  }
+  wave_sync();
+  uint8_t *out = hdr + (size_t)m * kHdrBytes;
+  for (int i = t; i < kHdrBytes; i += 64) out[i] = hb[i];
 }
 
 // ---------------------------------------------------------------- sizes: block per segment
@@ -2002,7 +2073,7 @@ void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, con
 }
 void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs) {
   static const int force = knob("MIB_CTX_MODE") ? atoi(knob("MIB_CTX_MODE")) & 3 : -1;   // experiments
-  hipLaunchKernelGGL(context_mode_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, force);
+  hipLaunchKernelGGL(context_mode_kernel, dim3(nmbs), dim3(64), 0, st, jobs, mbs, nmbs, force);
 }
 // Literal prefix codes per metablock: at most kLitTreeCap.  The decoder keeps a metablock's
 // tables in its LDS table area only when they fit (12,224 entries, >= 256 per code); past
@@ -2032,7 +2103,7 @@ void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const ui
   const int nl = std::max(lit_tree_cap(), sk.k[0]), nr = nl + sk.k[1] + sk.k[2] * kDistCtx;
   hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * nr), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, nl, sk.k[1],
                      nr);
-  hipLaunchKernelGGL(mb_header_kernel, dim3((nmbs + 63) / 64), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
+  hipLaunchKernelGGL(mb_header_kernel, dim3(nmbs), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {

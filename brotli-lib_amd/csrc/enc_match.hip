@@ -293,11 +293,10 @@ constexpr int kNearSpan = 4096;  // positions per block (its fixed lookups amort
 template <bool kHist, bool kParts>
 __global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref,
                                                               uint32_t total, uint32_t max_dist, uint32_t *matches) {
-  constexpr int kStage = kNear + kNearT + kNearMeasure + 8;   // staged bytes per tile
-  constexpr int kPer = (kStage + kNearT - 1) / kNearT;        // ... per thread
+  constexpr int kW = kNear + kNearT + kNearMeasure;   // staged words per tile
+  constexpr int kPer = (kW + kNearT - 1) / kNearT;    // ... per thread
   constexpr uint32_t kStep = kNearT - 1;
-  __shared__ uint32_t w4[kNear + kNearT + kNearMeasure];   // the 4 bytes at each staged offset
-  __shared__ uint8_t bytes[kPer * kNearT];  // the tile's bytes from kNear before it (zero outside the stream)
+  __shared__ uint32_t w4[kPer * kNearT];    // the 4 bytes at each staged offset (zero outside the stream)
   __shared__ uint32_t sm2[2][kNearT];       // each position's 2-byte candidate mask (lo, hi word)
   const uint32_t gb = blockIdx.x * kNearSpan;   // (a block stays inside one 64 KiB segment)
   if (gb >= total) return;
@@ -309,27 +308,39 @@ __global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, c
   const uint32_t pbits = kParts ? jb.part_bits : 16u, plag = kParts ? jb.part_lag : 0u;
   const bool parts = kParts && jb.parts;
   const uint32_t t = threadIdx.x;
-  // the tile's bytes, loaded one tile ahead (kPer per thread, in registers)
-  uint32_t nb[kPer];
+  typedef const __attribute__((address_space(1))) uint32_t GU32;
+  // the tile's words, loaded one tile ahead (kPer per thread, in registers): word i = the 4
+  // bytes at g0 - kNear + i, each 0 outside [the earliest reachable byte, the stream's end).
+  // Inside, from two aligned dwords; at the edges byte by byte.
+  uint32_t nw[kPer];
   auto load_tile = [&](uint32_t g0) {
-    const uint32_t p0 = g0 - sr.pos_base;
-    const int64_t lo = -(int64_t)min((uint64_t)p0 + hist, (uint64_t)kNear);
+    const int64_t p0 = (int64_t)g0 - sr.pos_base;
+    const int64_t lo = -(int64_t)min((uint64_t)p0 + hist, (uint64_t)kNear);   // earliest offset with a byte
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
       const int i = k * kNearT + (int)t;
-      const int64_t o = (int64_t)i - kNear, q = (int64_t)p0 + o;
-      nb[k] = (i < kStage && o >= lo && q < (int64_t)n && g0 < sr.end) ? sr.base[(int64_t)g0 + o] : 0u;
+      const int64_t o = (int64_t)i - kNear, q = p0 + o;   // the word's first byte, stream-relative
+      uint32_t v = 0;
+      if (i < kW && g0 < sr.end) {
+        if (o >= lo && q + 8 <= (int64_t)n) {
+          const uintptr_t a = (uintptr_t)(sr.base + (int64_t)g0 + o);
+          GU32 *w = (GU32 *)(a & ~(uintptr_t)3);
+          v = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3));
+        } else {
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (o + b >= lo && q + b < (int64_t)n) v |= (uint32_t)sr.base[(int64_t)g0 + o + b] << (8 * b);
+        }
+      }
+      nw[k] = v;
     }
   };
   load_tile(gb);
   for (uint32_t g0 = gb; g0 < gb + kNearSpan && g0 < sr.end; g0 += kStep) {
     __syncthreads();   // (the previous tile's readers are done)
 #pragma unroll
-    for (int k = 0; k < kPer; k++) bytes[k * kNearT + t] = (uint8_t)nb[k];
+    for (int k = 0; k < kPer; k++) w4[k * kNearT + t] = nw[k];
     load_tile(g0 + kStep);   // in flight during this tile
-    __syncthreads();
-    for (uint32_t i = t; i < kNear + kNearT + kNearMeasure; i += kNearT)
-      w4[i] = (uint32_t)bytes[i] | ((uint32_t)bytes[i + 1] << 8) | ((uint32_t)bytes[i + 2] << 16) | ((uint32_t)bytes[i + 3] << 24);
     __syncthreads();
     const uint32_t x = kNear + t, g = g0 + t, p = g - sr.pos_base;
     const bool here = g < sr.end && p + 2 <= n;

@@ -621,16 +621,16 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
 // carry_kernel does between segments; a copy that ends a piece and one that starts the next
 // at the same distance become one copy (a run of zeros stays one command per segment).
 // Wave per segment.
-__global__ __launch_bounds__(64) void merge_pieces_kernel(const Job *jobs, Seg *segs, const Seg *pieces, int ps,
-                                                          RawCmd *raw) {
+__global__ __launch_bounds__(64) void merge_pieces_kernel(const Job *jobs, Seg *segs, const Seg *pieces, RawCmd *raw) {
   Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
-  const int P = 1 << ps;
+  const int P = 1 << (sg.pieces & 7);
+  const Seg *mine = pieces + (sg.pieces >> 3);
   const uint32_t lane = threadIdx.x;
   RawCmd *dst = raw + sg.cmd_off;
   uint32_t n = 0, carry = 0, last = 0;
   for (int k = 0; k < P; k++) {
-    const Seg &pc = pieces[(size_t)blockIdx.x * P + k];
+    const Seg &pc = mine[k];
     const RawCmd *src = raw + pc.cmd_off;   // (at or above dst + n: chunks are read before they are written)
     uint32_t m = pc.ncmd;
     if (m && n && carry == 0) {   // the previous piece ended in a copy: does this one continue it?
@@ -676,7 +676,7 @@ __global__ __launch_bounds__(64) void merge_pieces_kernel(const Job *jobs, Seg *
 // the sampled copy of the segment table (each segment's first `sample` bytes) and the parse
 // pieces (2^ps per segment: kSeg >> ps bytes each, command slices back to back inside the
 // segment's, backtrack_kernel's capacity each); thread per segment
-__global__ void derive_segs_kernel(const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces) {
+__global__ void derive_segs_kernel(const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, Seg *pieces) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nsegs) return;
   const Seg sg = segs[i];
@@ -686,6 +686,7 @@ __global__ void derive_segs_kernel(const Seg *segs, int nsegs, uint32_t sample, 
     d_sample[i] = sm;
   }
   if (pieces) {
+    const int ps = (int)(sg.pieces & 7);
     const uint32_t plen = kSeg >> ps;
     uint32_t off = sg.cmd_off;
     for (int q = 0; q < (1 << ps); q++) {
@@ -694,17 +695,16 @@ __global__ void derive_segs_kernel(const Seg *segs, int nsegs, uint32_t sample, 
       pc.end = min(sg.end, pc.start + plen);
       pc.cmd_off = off;
       off += (pc.end - pc.start) / 2 + 2;
-      pieces[((size_t)i << ps) + q] = pc;
+      pieces[(sg.pieces >> 3) + q] = pc;
     }
   }
 }
-void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, int ps, Seg *pieces) {
-  if (!d_sample && !ps) return;
-  hipLaunchKernelGGL(derive_segs_kernel, dim3((nsegs + 255) / 256), dim3(256), 0, st, segs, nsegs, sample, d_sample, ps,
-                     ps ? pieces : nullptr);
+void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, Seg *pieces) {
+  if (!d_sample && !pieces) return;
+  hipLaunchKernelGGL(derive_segs_kernel, dim3((nsegs + 255) / 256), dim3(256), 0, st, segs, nsegs, sample, d_sample, pieces);
 }
-void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, int ps, RawCmd *raw) {
-  if (nsegs) hipLaunchKernelGGL(merge_pieces_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, pieces, ps, raw);
+void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const Seg *pieces, RawCmd *raw) {
+  if (nsegs) hipLaunchKernelGGL(merge_pieces_kernel, dim3(nsegs), dim3(64), 0, st, jobs, segs, pieces, raw);
 }
 
 // ---------------------------------------------------------------- 5. second-iteration prices

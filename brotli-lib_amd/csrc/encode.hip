@@ -210,11 +210,17 @@ Params make_params(const mib_enc_opts *o) {
 // Pieces cut the parse more often (a piece's first node starts a fresh path; copies stop at
 // the piece end): C4 dp 123 -> 105 ms for +0.03 % bytes, C2 39 -> 8.5 ms.
 // MIB_DP_PIECES=0..3 overrides.
-constexpr int kMaxPieceShift = 4;
-int dp_piece_shift(int nsegs) {
+constexpr int kMaxPieceShift = 5;
+constexpr uint64_t kSmallStream = 1ull << 20;
+// Pieces per segment (2^shift) by the stream itself, so a stream parses the same in any batch:
+// 8 KiB pieces; 2 KiB for one-shot streams below 1 MiB and streaming chunks of up to 4 MiB --
+// a lone small stream or a 1 MiB streaming chunk gets 512 DP waves instead of 128 (its parse
+// was 4.7 of the 9.2 ms a reference-cadence update() took, r05m; 1.2 ms now, r05n).  C4's 1 MiB
+// buffers keep 8 KiB pieces (2 KiB: 0.36296 vs 0.36281, r05n).  (MIB_DP_PIECES, experiment
+// builds: one shift for every stream.)
+int dp_piece_shift(uint64_t n, bool streaming) {
   static const int v = knob("MIB_DP_PIECES") ? std::min(kMaxPieceShift, std::max(0, atoi(knob("MIB_DP_PIECES")))) : -1;
-  (void)nsegs;
-  return v >= 0 ? v : 3;
+  return v >= 0 ? v : (streaming ? n <= 4 * kSmallStream : n < kSmallStream) ? 5 : 3;
 }
 bool rep_pass(const Params &p) {
   static const int v = knob("MIB_REP") ? atoi(knob("MIB_REP")) : -1;
@@ -311,7 +317,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   std::vector<Mb> mbs;
   std::vector<uint32_t> seg_job;   // per 64 KiB of global positions: its stream
   std::vector<SegRef> seg_ref;     // ... and where its bytes are
-  uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0;
+  uint64_t pos_total = 0, out_scratch = 0, cmd_total = 0, npieces = 0;
   bool any_hist = false, any_parts = false, any_dict = false, any_cdict = false;
   for (size_t j = 0; j < k; j++) {
     Job &jb = jobs[j];
@@ -382,6 +388,10 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
           sg.mb = (uint32_t)mbs.size();
           sg.cmd_off = (uint32_t)cmd_total;
           cmd_total += (sg.end - sg.start) / 2 + 4 + (2 << kMaxPieceShift);   // (room for the parse pieces' slices)
+          // the segment's parse pieces: 2^shift of them from piece index npieces (Seg.pieces)
+          const int pshift = dp_piece_shift(n, sd[j].streaming);
+          sg.pieces = (uint32_t)(npieces << 3) | (uint32_t)pshift;
+          npieces += 1ull << pshift;
           segs.push_back(sg);
         }
         mb.nseg = (uint32_t)segs.size() - mb.first_seg;
@@ -424,7 +434,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += ns1 * part_push_bytes();
   const bool two_pass = prm.quality >= 11 && zopfli_iterations() > 1;   // backward-references-hq.ts:562-605
   need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
-  need += ns1 * sizeof(Seg) << kMaxPieceShift;   // parse pieces
+  need += std::max<uint64_t>(npieces, 1) * sizeof(Seg);   // parse pieces
   need += 40 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*ws_slot);
   if (!ws) {
@@ -472,9 +482,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   // zopfli_sample() bytes of every segment (its own copy of the segment table)
   const bool sampled = two_pass && zopfli_sample() < kSeg;
   Seg *d_sample = sampled ? ar.take<Seg>(ns1) : nullptr;
-  // the final parse on 2^ps pieces per segment when there are few segments (merge_pieces_kernel)
-  const int ps = dp_piece_shift(nsegs);
-  Seg *d_pieces = ps ? ar.take<Seg>(ns1 << ps) : nullptr;
+  // the final parse on pieces of the segments (merge_pieces_kernel)
+  const bool ps = npieces > (uint64_t)nsegs;
+  Seg *d_pieces = ps ? ar.take<Seg>(std::max<uint64_t>(npieces, 1)) : nullptr;
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
   Timer tm{ctx, st, mib_ctx_profiling(ctx) != 0, {}};
@@ -484,9 +494,9 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   // the sampled first iteration's and the parse pieces' segment tables, derived on the device
   // (the pieces' table of a C4 call is 12.6 MB: built on the host it was a host loop and a
   // pageable copy every call)
-  if (nsegs) launch_derive_segs(st, d_segs, nsegs, sampled ? zopfli_sample() : 0u, d_sample, ps, d_pieces);
+  if (nsegs) launch_derive_segs(st, d_segs, nsegs, sampled ? zopfli_sample() : 0u, d_sample, d_pieces);
   Seg *const d_fin = ps ? d_pieces : d_segs;   // the final parse's segment table
-  const int nfin = nsegs << ps;
+  const int nfin = ps ? (int)npieces : nsegs;
   CK(hipMemcpyAsync(d_seg_job, seg_job.data(), seg_job.size() * 4, hipMemcpyHostToDevice, st));
   CK(hipMemcpyAsync(d_seg_ref, seg_ref.data(), seg_ref.size() * sizeof(SegRef), hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
@@ -532,7 +542,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
       launch_backtrack(st, d_jobs, d_fin, nfin, choice, raw);
       tm.stop();
     }
-    if (ps) launch_merge_pieces(st, d_jobs, d_segs, nsegs, d_pieces, ps, raw);
+    if (ps) launch_merge_pieces(st, d_jobs, d_segs, nsegs, d_pieces, raw);
     tm.start("codes");
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
     if (two_pass && rep_pass(prm)) launch_rep(st, d_jobs, d_segs, nsegs, model, raw, cmd_pos);   // (cmd_pos: scratch until codes)
@@ -603,12 +613,9 @@ uint64_t group_position_limit(mib_ctx *ctx) {
   size_t free_b = 0, total_b = 0;
   uint64_t lim = (1ull << 31) - 4 * (uint64_t)kSeg;
   if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    // (only the workspace a group grows is freed before it grows: the other lanes' stay held)
     const Workspace *ws = reinterpret_cast<const Workspace *>(*mib_ctx_enc_ws(ctx));
-    uint64_t held = ws ? ws->cap : 0;
-    for (int l = 1; l < kMaxLanes; l++) {
-      const Workspace *wl = reinterpret_cast<const Workspace *>(*mib_ctx_lane_ws(ctx, l));
-      held += wl ? wl->cap : 0;
-    }
+    const uint64_t held = ws ? ws->cap : 0;
     const uint64_t usable = ((uint64_t)free_b + held) / 10 * 8;   // leave 20% to the caller
     lim = std::min<uint64_t>(lim, std::max<uint64_t>(usable / kWsBytesPerPosition, 1ull << 24));
   }

@@ -83,11 +83,15 @@ void build_cmd_lut(int16_t *lut) {   // engine.ts:65-90
 
 // Every device a context runs on is checked (gfx950) and gets its own copy of the decoder's
 // __constant__ command table: module globals are per device.  Leaves `device` current.
+int g_ndev = -1;   // visible devices, counted once (hipGetDeviceCount cost ~0.4 ms a call, r05m)
 int ensure_device(int device) {
   std::lock_guard<std::mutex> lk(g_mu);
-  int n = 0;
-  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MIB_E_NO_DEVICE;
-  if (device < 0 || device >= n || device >= kMaxDevices) return MIB_E_NO_DEVICE;
+  if (g_ndev <= 0) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return MIB_E_NO_DEVICE;
+    g_ndev = n;
+  }
+  if (device < 0 || device >= g_ndev || device >= kMaxDevices) return MIB_E_NO_DEVICE;
   HIP_OK(hipSetDevice(device));
   if (g_dev_ready[device]) return 0;
   hipDeviceProp_t prop;
@@ -334,6 +338,9 @@ struct mib_ctx {
   uint8_t *ring = nullptr;
   hipEvent_t ring_ev[2] = {nullptr, nullptr};
   bool ring_failed = false;
+  // contexts decoding on this device at once (multi.cpp: shards sharing a GPU): the decoder's
+  // one-stream-per-CU build is chosen only when the streams of ALL of them fit one per CU
+  int dev_share = 1;
   // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
   uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
@@ -865,7 +872,7 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
     hipEventCreate(&e1);
     hipEventRecord(e0, stream);
   }
-  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, waves_per_cu(c->device, (size_t)grid),
+  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, waves_per_cu(c->device, (size_t)grid * (size_t)c->dev_share),
                            stream));
   if (c->profiling) hipEventRecord(e1, stream);
   HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * k, hipMemcpyDeviceToHost, stream));
@@ -968,7 +975,7 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
     hipEventRecord(e0, stream);
   }
   HIP_OK(mib_decode_parts_launch(c->d_jobs, (int)nj, c->d_scratch, per_block, d_ticket, grid,
-                                 waves_per_cu(c->device, (size_t)grid), stream));
+                                 waves_per_cu(c->device, (size_t)grid * (size_t)c->dev_share), stream));
   if (c->profiling) hipEventRecord(e1, stream);
   HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * nj, hipMemcpyDeviceToHost, stream));
   HIP_OK(hipStreamSynchronize(stream));
@@ -1215,3 +1222,5 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
 }  // extern "C"
 
 extern "C" void mib_force_ballot_rank(int force) { __atomic_store_n(&g_force_ballot, force ? 1 : 0, __ATOMIC_RELAXED); }
+// internal (multi.cpp): how many contexts decode on this context's device at once
+extern "C" void mib_ctx_set_share(mib_ctx *c, int n) { c->dev_share = n > 1 ? n : 1; }

@@ -3,9 +3,12 @@ profiles/<tag>/<workload>_kernel_stats.csv, profiles/pmc_summary.json (HBM bytes
 per workload and kernel) and profiles/<tag>/sq_counters.json.
 
 HBM bytes per launch = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 / launches: FETCH_SIZE and
-WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide streaming reads
-(MI355X_MICROARCH.md, HBM section), hence the doubling -- exact for 16 B/lane streams only,
-an upper bound for byte-granular gathers.  SQ counters are in the SQ's units (cycle counters
+WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE tallies each 128 B memory-side read request
+(TCC_EA0_RDREQ) at 64 B, hence the doubling.  Calibrated per access width in round 5
+(scripts/probe/traffic_probe.hip, profiles/r05/traffic_calibration.json): 1, 4, 16 and 32-byte
+gathers and 1-byte LDS-DMA loads each make exactly one 128 B request per missed line, so the
+doubled figure is the line traffic for the gather-bound kernels too (a 36 B access across a
+128 B boundary is two requests).  Requests served by the Infinity Cache are counted as well.  SQ counters are in the SQ's units (cycle counters
 in quad-cycles), summed over a kernel's dispatches and divided by their number."""
 import csv
 import glob
@@ -46,7 +49,8 @@ def main(tag):
     os.makedirs(dst, exist_ok=True)
     summary = {'tag': tag, 'source': 'rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of bench.py --steps 1 '
                                       '--warmup 1 --workload <w> (scripts/gpu_profile_all.sh)',
-               'correction': 'hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB -> B); gfx950 FETCH_SIZE halves wide reads',
+               'correction': 'hbm = 2*FETCH_SIZE + WRITE_SIZE (KiB -> B); gfx950 FETCH_SIZE tallies each 128 B read request at 64 B, '
+                             'for every access width (profiles/r05/traffic_calibration.json)',
                'workloads': {}}
     for tr in sorted(glob.glob(os.path.join(base, 'trace_*'))):
         if not os.path.isdir(tr):
