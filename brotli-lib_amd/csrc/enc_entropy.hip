@@ -1857,6 +1857,8 @@ __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs,
   __shared__ int16_t nzs[26];
   __shared__ int sh_n, sh_ntrees;
   __shared__ CmapWs cws;
+  __shared__ uint8_t btd[3][kMaxBT + 2], bcd[3][26];   // the block-split codes, staged by the wave
+  __shared__ uint16_t btc[3][kMaxBT + 2], bcc[3][26];
   const int m = blockIdx.x;
   if (m >= nmbs) return;
   Mb &mb = mbs[m];
@@ -1864,6 +1866,17 @@ __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs,
   if (jb.uncompressed) return;
   const int t = threadIdx.x;
   for (int i = t; i < kHdrBytes; i += 64) hb[i] = 0;
+  {
+    const Codes &cd = codes[m];
+    for (int i = t; i < 3 * (kMaxBT + 2); i += 64) {
+      btd[i / (kMaxBT + 2)][i % (kMaxBT + 2)] = cd.btd[i / (kMaxBT + 2)][i % (kMaxBT + 2)];
+      btc[i / (kMaxBT + 2)][i % (kMaxBT + 2)] = cd.btc[i / (kMaxBT + 2)][i % (kMaxBT + 2)];
+    }
+    for (int i = t; i < 3 * 26; i += 64) {
+      bcd[i / 26][i % 26] = cd.bcd[i / 26][i % 26];
+      bcc[i / 26][i % 26] = cd.bcc[i / 26][i % 26];
+    }
+  }
   wave_sync();
   BitW w{hb, 0};   // (lane 0's)
   if (t == 0) {
@@ -1876,27 +1889,44 @@ __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs,
     w.put(2, (uint32_t)(mn - 4));
     w.put(mn * 4, length - 1);
     if (!mb.is_last) w.put(1, 0);
-    Codes &cd = codes[m];
     for (int c = 0; c < 3; c++)
-      put_block_split(w, (int)mb.nbt[c], cd.btd[c], cd.btc[c], cd.bcd[c], cd.bcc[c], mb.first_count[c], nzs, cws.ts);
+      put_block_split(w, (int)mb.nbt[c], btd[c], btc[c], bcd[c], bcc[c], mb.first_count[c], nzs, cws.ts);
     w.put(2, jb.npostfix);
     w.put(4, jb.ndirect >> jb.npostfix);
     for (uint32_t ty = 0; ty < mb.nbt[0]; ty++) w.put(2, mb.ctx_mode);
+  }
+  wave_sync();
+  {   // store_code settles the codes it writes (a lone symbol's depth 0): back for the emitter
+    Codes &cd = codes[m];
+    for (int i = t; i < 3 * (kMaxBT + 2); i += 64) {
+      cd.btd[i / (kMaxBT + 2)][i % (kMaxBT + 2)] = btd[i / (kMaxBT + 2)][i % (kMaxBT + 2)];
+      cd.btc[i / (kMaxBT + 2)][i % (kMaxBT + 2)] = btc[i / (kMaxBT + 2)][i % (kMaxBT + 2)];
+    }
+    for (int i = t; i < 3 * 26; i += 64) {
+      cd.bcd[i / 26][i % 26] = bcd[i / 26][i % 26];
+      cd.bcc[i / 26][i % 26] = bcc[i / 26][i % 26];
+    }
   }
   // the two context maps (literal, distance) over dense code indices: slots of type ty start at
   // the codes of the types before it; each map's move-to-front by the wave, its coding by lane 0
   for (int cat = 0; cat < 2; cat++) {
     const int nty = (int)(cat == 0 ? mb.nbt[0] : mb.nbt[2]), nctx = cat == 0 ? kLitCtx : kDistCtx;
+    // (built by the wave from global memory: lane 0's loop of dependent loads took most of the
+    // kernel's 0.36 ms, r05p)
+    int base = 0, tbase = 0;   // codes of the types before mine / all types
+    for (int ty = 0; ty < nty; ty++) {
+      const int c = (int)(cat == 0 ? mb.nlit_t[ty] : mb.ndist_t[ty]);
+      tbase += c;
+    }
+    for (int i = t; i < nty * nctx; i += 64) {
+      const int ty = i / nctx;
+      base = 0;
+      for (int u = 0; u < ty; u++) base += (int)(cat == 0 ? mb.nlit_t[u] : mb.ndist_t[u]);
+      map[i] = (uint8_t)(base + (cat == 0 ? mb.lit_cmap[i] - ty * kLitCtx : mb.dist_cmap[i] - ty * kDistCtx));
+    }
     if (t == 0) {
-      int base = 0;
-      for (int ty = 0; ty < nty; ty++) {
-        for (int q = 0; q < nctx; q++)
-          map[ty * nctx + q] = (uint8_t)(base + (cat == 0 ? mb.lit_cmap[ty * kLitCtx + q] - ty * kLitCtx
-                                                          : mb.dist_cmap[ty * kDistCtx + q] - ty * kDistCtx));
-        base += (int)(cat == 0 ? mb.nlit_t[ty] : mb.ndist_t[ty]);
-      }
       sh_n = nty * nctx;
-      sh_ntrees = base;
+      sh_ntrees = tbase;
     }
     wave_sync();
     if (sh_ntrees > 1) mtf_wave(map, sh_n, cws.v);
