@@ -1784,9 +1784,14 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   // the back edge, whatever the order of the code: hence LDS-DMA.)  Destinations ascend, and
   // in the context-modelled build no literal lies between two pending copies (literals first
   // complete every copy), so completing them in order leaves (c1, c2b) = the last two bytes.
+  // The queue's entries sit in lanes 0..3 of two VGPRs (qdv: destination, qcv: length), slot
+  // k in lane k, written by v_writelane at the new copy's slot; the oldest one's are also kept
+  // in SGPRs (qd0, qc0) for the overlap test and its stores.  (As eight SGPRs shifted down on
+  // every completion, the selects and the compiler's phi copies cost ~40 scalar instructions a
+  // copy, r05 ISA listing.)
   int qn = 0, qhead = 0;
-  int qd0 = 0, qd1 = 0, qd2 = 0, qd3 = 0, qc0 = 0, qc1 = 0, qc2 = 0, qc3 = 0;
-  static_assert(kCopyQ == 4, "the pending queue is four registers deep");
+  int qdv = 0, qcv = 0, qd0 = 0, qc0 = 0;
+  static_assert(kCopyQ <= 64, "the pending queue lives in lanes");
   auto ensure = [&]() {   // at least 32 bits of W at P (every read is <= 24 bits)
     if (P - Pw >= 32) {
       W = (W >> 32) | ((uint64_t)N << 32);
@@ -1831,10 +1836,10 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
       c2b = qc0 >= 2 ? __builtin_amdgcn_readlane(v, qc0 - 2) : c1;
       c1 = __builtin_amdgcn_readlane(v, qc0 - 1);
     }
-    qd0 = qd1; qd1 = qd2; qd2 = qd3;
-    qc0 = qc1; qc1 = qc2; qc2 = qc3;
     qhead = (qhead + 1) & (kCopyQ - 1);
     qn--;
+    qd0 = __builtin_amdgcn_readlane(qdv, qhead);   // (the next oldest; stale when qn = 0, unused)
+    qc0 = __builtin_amdgcn_readlane(qcv, qhead);
   };
   auto complete_oldest = [&]() {
     wait_vm(qn - 1);
@@ -2206,14 +2211,10 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
         typedef __attribute__((address_space(1))) void GV;
         const int slot = (qhead + qn) & (kCopyQ - 1);
         __builtin_amdgcn_global_load_lds((GV *)(ring + at), (LV *)g_cp[slot], 1, 0, 0);   // lane l -> dword l
-        qd0 = qn == 0 ? pos : qd0;   // (selects: the new copy is entry qn)
+        qdv = (int)write_lane((uint32_t)qdv, (uint32_t)pos, (uint32_t)slot);
+        qcv = (int)write_lane((uint32_t)qcv, (uint32_t)cl, (uint32_t)slot);
+        qd0 = qn == 0 ? pos : qd0;
         qc0 = qn == 0 ? cl : qc0;
-        qd1 = qn == 1 ? pos : qd1;
-        qc1 = qn == 1 ? cl : qc1;
-        qd2 = qn == 2 ? pos : qd2;
-        qc2 = qn == 2 ? cl : qc2;
-        qd3 = qn == 3 ? pos : qd3;
-        qc3 = qn == 3 ? cl : qc3;
         qn++;
       } else {
         finish_copy();   // (this copy may read it)
