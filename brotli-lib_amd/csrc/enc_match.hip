@@ -136,17 +136,32 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     if constexpr (!kHist) {
       const uint64_t mine0 = spre[0][me];
       const int dmax = min(depth, kBack), nwalk = min(dmax, nrun);
-      for (int t = 1; t <= nwalk; t++) {
-        const int e = me - t;
-        // one exit test and one reject test per candidate, computed without branches (the
-        // nested ifs were four exec-mask branches per candidate: 65.8 -> 62.6 ms on C4, r04t2);
-        // the bucket run's end is the trip count
+      // The walk steps t in lockstep over the wave (a scalar loop: the run's end per lane is a
+      // compare, not a divergent exit) and screens each candidate by its first word: it needs the
+      // exact tests below iff the word's low best + 1 bytes all match (first difference past byte
+      // best, or none in the word) or it lies beyond the window.  Most candidates fail the screen,
+      // ~25 instructions each; the exact tests run under a branch the wave skips when no lane
+      // needs them.  (As one per-lane loop with break / continue every candidate paid the exit-mask
+      // bookkeeping of the rare paths, ~48 instructions, r05 ISA listing; as a per-lane skip loop
+      // the lanes' different skip lengths multiplied the steps.)  Same candidates, same order,
+      // same records.
+      auto low_bytes = [](uint32_t n) -> uint64_t { return n >= 7 ? ~0ull : (1ull << (8 * (n + 1))) - 1; };
+      uint64_t bmask = low_bytes(best);
+      int tend = best >= limit ? 0 : nwalk;   // this lane's last step (0: done)
+      for (int t = 1; t <= kBack; t++) {
+        if (__ballot(t <= tend) == 0) break;
+        const int e = me - min(t, nwalk);   // (an in-range entry for lanes past their run)
         const uint32_t pe = spos[e];
-        const uint64_t x0 = mine0 ^ spre[0][e];
+        const uint64_t c0 = spre[0][e];
+        asm volatile("" ::"v"(pe), "v"(c0));   // (both reads issued before one wait)
+        const uint64_t x0 = mine0 ^ c0;
         const uint32_t d = g - pe;
-        if ((d > max_dist) | (best >= limit)) break;
+        if (!((t <= tend) & ((d > max_dist) | ((x0 & bmask) == 0)))) continue;
+        if (d > max_dist) {   // (farther candidates only: positions ascend in a run)
+          tend = 0;
+          continue;
+        }
         const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
-        if ((x0 != 0) & (qlen <= best)) continue;   // known exactly and not longer
         const uint32_t pc = parts ? part_cap(pA, d, pbits, plag) : ~0u;   // part index: lagging source
         if (pc <= best) continue;
         uint32_t len;
@@ -183,7 +198,9 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
             cnt--;
           }
           local[cnt++] = pack_match(d, len);
-          if (len >= limit || len >= kMatchLenSat) break;   // the parse measures a long copy itself
+          bmask = low_bytes(best);
+          // the parse measures a long copy itself; best >= limit ends the walk as well
+          if (len >= limit || len >= kMatchLenSat) tend = 0;
         }
       }
       } else {
@@ -212,7 +229,9 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
         const int e = me - t;
         // (the tests flattened as in the window-only walk above; the run's end is the trip count)
         const uint32_t pe = spos[e];
-        const uint64_t x0 = mine0 ^ spre[0][e];
+        const uint64_t c0 = spre[0][e];
+        asm volatile("" ::"v"(pe), "v"(c0));   // (one wait for both reads, as above)
+        const uint64_t x0 = mine0 ^ c0;
         const uint32_t d = g - pe;
         if ((d > max_dist) | (best >= limit)) {
           stop = true;

@@ -158,9 +158,11 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
   __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
   __shared__ uint16_t itab[kInsTab];                       // insert length -> insert code | its extra bits << 8
   __shared__ uint16_t litc_all[kDpWaves * kS][256];   // literal costs in 1/256 bits (exact: they are quantised so)
-  // (one spare entry per 32 lanes: the groups' entries i and 32 + i fall 12 banks apart, not on
-  // the same banks -- two segments at the same offset read them in one instruction)
-  __shared__ StageEnt stg_all[kDpWaves][64 + 2];
+  // (one spare entry per 32 lanes, per 16 with four segments: the entries the segments read at
+  // the same offset in one instruction -- i and 32 + i, or i, 16 + i, 32 + i, 48 + i -- fall 12
+  // banks apart instead of on the same banks: 16 entries are 192 words, a multiple of the 64)
+  constexpr int kPadSh = KS == 4 ? 4 : 5;
+  __shared__ StageEnt stg_all[kDpWaves][64 + (64 >> kPadSh)];
   for (int t = threadIdx.x; t < kLenTab; t += 64 * kDpWaves) cctab[t] = (uint8_t)(t >= 2 ? copy_code((uint32_t)t) : 0);
   for (int t = threadIdx.x; t < kInsTab; t += 64 * kDpWaves) {
     const int ic = ins_code((uint32_t)t);
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     }
     e.info = (maxlen ? nm : 0u) | (maxlen << 8) | ((word ? maxlen : 2u) << 16);   // | the shortest usable length
     e.pad[0] = e.pad[1] = 0;
-    stg[lane + (lane >> 5)] = e;
+    stg[lane + (lane >> kPadSh)] = e;
     DPCOUNT(6, 1);
   };
   if (!done) stage();
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
       }
     }
     const bool act = !done;
-    const StageEnt &e = stg[src + (src >> 5)];
+    const StageEnt &e = stg[src + (src >> kPadSh)];
     const uint32_t info = e.info;
     const uint32_t nm = act ? (info & 0xFF) : 0u, maxlen = act ? ((info >> 8) & 0xFF) : 0u;
     const uint32_t minlen = info >> 16;   // 2, or a dictionary word's length: that length only
