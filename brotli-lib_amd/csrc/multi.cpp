@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <mutex>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -186,12 +187,17 @@ int decode_shard(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, 
   }
   uint8_t *d_in = nullptr;
   int rc;
+  static const bool timing = mib::knob("MIB_HOST_TIMING") != nullptr;
+  const auto t_in = std::chrono::steady_clock::now();
+  auto ms_since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_in).count(); };
   if ((rc = upload(sh, in, idx, ioff, &d_in, st))) return rc;
   uint8_t *d_out = mib_ctx_stage(sh.ctx, 1, ooff[k] + 64);
   if (!d_out) return MIB_E_OUT_OF_MEMORY;
   std::vector<int64_t> sizes(k);
   std::vector<int> stv(k);
+  const double t_up = timing ? ms_since() : 0.0;
   rc = mib_ctx_decode(sh.ctx, d_in, ioff.data(), k, d_out, ooff.data(), sizes.data(), stv.data(), st);
+  if (timing) fprintf(stderr, "[mib] shard %d: %zu streams, upload done %.2f ms, decode done %.2f\n", sh.device, k, t_up, ms_since());
   if (rc && rc != MIB_E_NEED_SPACE) return rc;
   std::vector<const uint8_t *> src(k);
   std::vector<uint64_t> lens(k);
@@ -209,12 +215,16 @@ int decode_shard(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, 
   return 0;
 }
 
-// run fn(shard, indices) on `shards` host threads; the first error wins
+// run fn(shard, indices) on `shards` host threads; the first error wins.  per_device: at most
+// one shard per device, a device's streams in one call (the decoder: four 256-stream shards on
+// one GPU left one shard's kernel queued behind the others' on a shared hardware queue, 298 vs
+// 159 ms, r05u -- the call ~25 % slower than one launch of all 1,024)
 template <class F>
-int run_shards(const mib_span *in, size_t k, int n_gpus, F fn) {
+int run_shards(const mib_span *in, size_t k, int n_gpus, F fn, bool per_device = false) {
   const int ndev = device_count();
   if (ndev <= 0) return MIB_E_NO_DEVICE;
   int shards = n_gpus <= 0 ? ndev : n_gpus;
+  if (per_device) shards = std::min(shards, ndev);
   shards = std::max(1, std::min<int>({shards, kMaxShards, (int)std::max<size_t>(k, 1)}));
   std::vector<Shard *> sh(shards, nullptr);
   int rc = 0;
@@ -255,6 +265,8 @@ int mib_encode_batch_n(const mib_span *in, size_t k, const mib_enc_opts *o, int 
     if ((!in[i].data && in[i].size) || in[i].size >= (1ull << 31)) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
+  // (encode shards may share a device: their uploads and downloads overlap the others' kernels,
+  // 250-303 ms against one context's 268-281 on one GPU, r05v)
   const int rc = run_shards(in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) {
     return encode_shard(sh, in, idx, o, out, status);
   });
@@ -272,9 +284,9 @@ int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, i
     if (!in[i].data && in[i].size) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
-  const int rc = run_shards(in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) {
-    return decode_shard(sh, in, idx, out, status);
-  });
+  const int rc = run_shards(
+      in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) { return decode_shard(sh, in, idx, out, status); },
+      true);
   if (rc)
     for (size_t i = 0; i < k; i++) mib_buf_free(&out[i]);
   return rc;

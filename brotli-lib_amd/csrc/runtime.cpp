@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -455,6 +456,30 @@ void for_chunks(const Piece *ps, size_t k, F fn) {
 }
 }  // namespace
 
+// MIB_HOST_TIMING (experiment builds): each ring transfer's time waiting for the device and
+// copying on the host, to stderr
+namespace {
+struct XferClock {
+  const bool on = mib::knob("MIB_HOST_TIMING") != nullptr;
+  const char *what;
+  uint64_t bytes = 0;
+  double wait_ms = 0, copy_ms = 0;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  explicit XferClock(const char *w) : what(w) {}
+  template <class F>
+  void timed(double &acc, F fn) {
+    if (!on) return fn();
+    const auto a = std::chrono::steady_clock::now();
+    fn();
+    acc += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  }
+  ~XferClock() {
+    if (on)
+      fprintf(stderr, "[mib] %s %.1f MiB: %.2f ms (device wait %.2f, host copy %.2f)\n", what, bytes / 1048576.0,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), wait_ms, copy_ms);
+  }
+};
+}  // namespace
 // host -> device: ps[i].src host, ps[i].dst device; asynchronous on st (returns once every
 // source byte is in the ring: the caller may reuse its buffers)
 int mib::ctx_upload(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
@@ -467,9 +492,14 @@ int mib::ctx_upload(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
     return 0;
   }
   int h = 0, rc = 0;
+  XferClock clk("upload");
+  clk.bytes = total;
   for_chunks(ps, k, [&](const std::vector<Piece> &ch, uint64_t) {
     if (rc) return;
-    if (hipEventSynchronize(c->ring_ev[h]) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }   // the half's last copies are done
+    clk.timed(clk.wait_ms, [&] {   // the half's last copies are done
+      if (hipEventSynchronize(c->ring_ev[h]) != hipSuccess) rc = MIB_E_NO_DEVICE;
+    });
+    if (rc) return;
     uint8_t *pin = c->ring + (uint64_t)h * kRingHalf;
     std::vector<Piece> hc;
     uint64_t po = 0;
@@ -477,7 +507,7 @@ int mib::ctx_upload(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
       hc.push_back(Piece{pin + po, p.src, p.n});
       po += p.n;
     }
-    par_copy(hc);
+    clk.timed(clk.copy_ms, [&] { par_copy(hc); });
     po = 0;
     for (const Piece &p : ch) {
       if (hipMemcpyAsync(p.dst, pin + po, p.n, hipMemcpyHostToDevice, st) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }
@@ -494,6 +524,8 @@ int mib::ctx_download(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
   hipStream_t st = (hipStream_t)stream;
   uint64_t total = 0;
   for (size_t i = 0; i < k; i++) total += ps[i].n;
+  XferClock clk("download");
+  clk.bytes = total;
   if (total < kParCopyMin || !ring_ready(c)) {
     for (size_t i = 0; i < k; i++)
       if (ps[i].n && hipMemcpyAsync(ps[i].dst, ps[i].src, ps[i].n, hipMemcpyDeviceToHost, st) != hipSuccess) return MIB_E_NO_DEVICE;
@@ -504,8 +536,11 @@ int mib::ctx_download(mib_ctx *c, void *stream, const HostPiece *ps, size_t k) {
   int ph = 0;
   auto drain = [&]() {
     if (pending.empty() || rc) return;
-    if (hipEventSynchronize(c->ring_ev[ph]) != hipSuccess) { rc = MIB_E_NO_DEVICE; return; }
-    par_copy(pending);
+    clk.timed(clk.wait_ms, [&] {
+      if (hipEventSynchronize(c->ring_ev[ph]) != hipSuccess) rc = MIB_E_NO_DEVICE;
+    });
+    if (rc) return;
+    clk.timed(clk.copy_ms, [&] { par_copy(pending); });
     pending.clear();
   };
   for_chunks(ps, k, [&](const std::vector<Piece> &ch, uint64_t) {
@@ -1163,6 +1198,9 @@ int mib_decode(const uint8_t *in, size_t n, const uint8_t *dict, size_t dict_n, 
 }
 
 int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
+  static const bool timing = mib::knob("MIB_HOST_TIMING") != nullptr;
+  const auto t_in = std::chrono::steady_clock::now();
+  auto ms_since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_in).count(); };
   DefaultUse use;
   mib_ctx *c = default_ctx();
   if (!c) return MIB_E_NO_DEVICE;
@@ -1197,7 +1235,9 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
     j.out_size = est > 0 ? est : -1;
     j.max_ring_log = peek_window_bits(in[i].data, in[i].size);
   }
+  const double t_up = timing ? ms_since() : 0.0;
   rc = decode_jobs(c, jobs, c->stream);
+  const double t_dec = timing ? ms_since() : 0.0;
   if (rc == 0) {
     std::vector<mib_buf *> outs;
     std::vector<const uint8_t *> src;
@@ -1216,6 +1256,9 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
     for (size_t i = 0; i < k; i++)
       if (jobs[i].status == MIB_E_NEED_SPACE) status[i] = mib_decode(in[i].data, in[i].size, nullptr, 0, -1, -1, &out[i]);
   }
+  if (timing)
+    fprintf(stderr, "[mib] decode_batch %zu streams: upload done %.2f ms, decode done %.2f, results %.2f\n", k, t_up, t_dec,
+            ms_since());
   return rc;
 }
 
