@@ -148,19 +148,24 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       auto low_bytes = [](uint32_t n) -> uint64_t { return n >= 7 ? ~0ull : (1ull << (8 * (n + 1))) - 1; };
       uint64_t bmask = low_bytes(best);
       int tend = best >= limit ? 0 : nwalk;   // this lane's last step (0: done)
+      // The walk ends before the first candidate beyond the window (positions ascend in a run,
+      // so distances grow with t): found up front -- by a binary search in the rare run that
+      // reaches that far -- so the steps need no distance, and read only the candidate's word.
+      if (tend > 0 && g - spos[me - nwalk] > max_dist) {
+        int lo = 0, hi = nwalk;   // d(lo) <= max_dist < d(hi)
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (g - spos[me - mid] > max_dist) hi = mid;
+          else lo = mid;
+        }
+        tend = lo;
+      }
       for (int t = 1; t <= kBack; t++) {
         if (__ballot(t <= tend) == 0) break;
-        const int e = me - min(t, nwalk);   // (an in-range entry for lanes past their run)
-        const uint32_t pe = spos[e];
-        const uint64_t c0 = spre[0][e];
-        asm volatile("" ::"v"(pe), "v"(c0));   // (both reads issued before one wait)
-        const uint64_t x0 = mine0 ^ c0;
-        const uint32_t d = g - pe;
-        if (!((t <= tend) & ((d > max_dist) | ((x0 & bmask) == 0)))) continue;
-        if (d > max_dist) {   // (farther candidates only: positions ascend in a run)
-          tend = 0;
-          continue;
-        }
+        const int e = me - t;   // (>= 0: me >= kBack; lanes past their run read another run's entry, unused)
+        const uint64_t x0 = mine0 ^ spre[0][e];
+        if (!((t <= tend) & ((x0 & bmask) == 0))) continue;
+        const uint32_t d = g - spos[e];
         const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
         const uint32_t pc = parts ? part_cap(pA, d, pbits, plag) : ~0u;   // part index: lagging source
         if (pc <= best) continue;
