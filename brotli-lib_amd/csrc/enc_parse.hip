@@ -498,17 +498,21 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     if (act) i++;
     const bool bend = act && i - i0 == (uint32_t)kL;
     if (__ballot(bend)) {
-      if (bend) {
-        // batch end: store its choices, move the window down one chunk, stage the next batch
-        if (i0 + hl != a) choice[gbase + i0 + hl] = choice_of(chd, chm);   // node a belongs to the previous segment
+      // batch end: the window moves down one chunk -- by selects of the whole wave, outside the
+      // divergent branch (as moves under the branch, the register allocator copied the window
+      // back and forth on every step instead, ~25 moves a step, r05 ISA listing)
 #pragma unroll
-        for (int c = 0; c + 1 < kC; c++) {
-          wc[c] = wc[c + 1];
-          wd[c] = wd[c + 1];
-          wm[c] = wm[c + 1];
-        }
-        wc[kC - 1] = kInf;
-        wd[kC - 1] = wm[kC - 1] = 0;
+      for (int c = 0; c + 1 < kC; c++) {
+        wc[c] = bend ? wc[c + 1] : wc[c];
+        wd[c] = bend ? wd[c + 1] : wd[c];
+        wm[c] = bend ? wm[c + 1] : wm[c];
+      }
+      wc[kC - 1] = bend ? kInf : wc[kC - 1];
+      wd[kC - 1] = bend ? 0u : wd[kC - 1];
+      wm[kC - 1] = bend ? 0u : wm[kC - 1];
+      if (bend) {
+        // store the batch's choices, stage the next batch
+        if (i0 + hl != a) choice[gbase + i0 + hl] = choice_of(chd, chm);   // node a belongs to the previous segment
         i0 = i;
         stage();
       }
