@@ -227,23 +227,31 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
       }                                                                      \
     } while (0)
       const int dmax = min(depth, kBack);
-      int t = 1;
-      bool stop = false;
       const int nwalk = min(dmax, nrun);
-      for (; t <= nwalk; t++) {
-        const int e = me - t;
-        // (the tests flattened as in the window-only walk above; the run's end is the trip count)
-        const uint32_t pe = spos[e];
-        const uint64_t c0 = spre[0][e];
-        asm volatile("" ::"v"(pe), "v"(c0));   // (one wait for both reads, as above)
-        const uint64_t x0 = mine0 ^ c0;
-        const uint32_t d = g - pe;
-        if ((d > max_dist) | (best >= limit)) {
-          stop = true;
-          break;
+      // (the window walk as in the window-only build above: lockstep steps, the first word's
+      // screen, the window end found up front; `stop` skips the history part as the serial walk's
+      // break did -- at a candidate beyond the window, or once a copy reaches the limit)
+      auto low_bytes = [](uint32_t n) -> uint64_t { return n >= 7 ? ~0ull : (1ull << (8 * (n + 1))) - 1; };
+      uint64_t bmask = low_bytes(best);
+      bool stop = nwalk > 0 && best >= limit;
+      int tend = stop ? 0 : nwalk;
+      if (tend > 0 && g - spos[me - nwalk] > max_dist) {
+        int lo = 0, hi = nwalk;   // d(lo) <= max_dist < d(hi)
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (g - spos[me - mid] > max_dist) hi = mid;
+          else lo = mid;
         }
+        tend = lo;
+        stop = true;
+      }
+      for (int s = 1; s <= kBack; s++) {
+        if (__ballot(s <= tend) == 0) break;
+        const int e = me - s;
+        const uint64_t x0 = mine0 ^ spre[0][e];
+        if (!((s <= tend) & ((x0 & bmask) == 0))) continue;
+        const uint32_t d = g - spos[e];
         const uint32_t qlen = (uint32_t)(__ffsll((unsigned long long)x0) - 1) >> 3;   // (x0 == 0: not used)
-        if ((x0 != 0) & (qlen <= best)) continue;
         uint32_t len;
         if (x0) {
           len = qlen;
@@ -270,9 +278,15 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
             if (lim > len) len += match_len(cur + len, (cur - d) + len, lim - len);
           }
         }
-        TAKE(d, len, { stop = true; break; });
-        if (stop) break;
+        bool fin = false;
+        TAKE(d, len, fin = true);
+        bmask = low_bytes(best);
+        if (fin) {
+          stop = true;
+          tend = 0;
+        }
       }
+      int t = nwalk + 1;   // (the history part's candidates count on from the window's)
       // streaming: then the bucket's occurrences before this chunk (farther, newest first)
       if (kHist && jb.hist_tab && !stop && t <= dmax) {
         const uint32_t *slot = jb.hist_tab + (size_t)(key & ((1u << kHashBits) - 1)) * kHistWays;
