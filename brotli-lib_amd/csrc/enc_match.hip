@@ -387,18 +387,33 @@ __global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, c
     // tested at once: 32 words for the 63 distances, a zero-half test per word.
     const uint32_t reach = min(min((uint32_t)kNear - 1, max_dist), p + hist);   // (the reference's d < 64)
     const uint32_t me = w4[x] & 0xFFFFu, pp = me | (me << 16);
-    uint32_t ml = 0, mh = 0;
+    // Per word a packed 16-bit min with 1 gives each half's "differs" bit (v_pk_min_u16: bit 0
+    // for the low half, bit 16 for the high); two words' bits are gathered two at a time into
+    // acc (bits 2k, 2k + 1: the low halves, d = 4k + 2, 4k + 3; bits 16 + 2k, 17 + 2k: the high
+    // halves, d = 4k, 4k + 1), ~6 VALU ops a k where the zero-half tests and the nibble took
+    // ~20; the bits are put in distance order once at the end.
+    // (asm: written as a vector min, the compiler turned it into two compares and selects a half)
+    auto differs = [](uint32_t v) -> uint32_t {
+      uint32_t r;
+      asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(v), "s"(0x00010001u));
+      return r;
+    };
+    uint32_t acc[2] = {0u, 0u};
 #pragma unroll
     for (int k = 0; k < 16; k++) {
       // y = x - 4k - 2: pairs at d = 4k + 2 (low half), 4k (high); y = x - 4k - 3: 4k + 3, 4k + 1
       const uint32_t ve = w4[x - 4 * k - 2] ^ pp, vo = w4[x - 4 * k - 3] ^ pp;
-      const uint32_t ze = ~(((ve & 0x7FFF7FFFu) + 0x7FFF7FFFu) | ve) & 0x80008000u;   // bit 15 / 31: a zero half
-      const uint32_t zo = ~(((vo & 0x7FFF7FFFu) + 0x7FFF7FFFu) | vo) & 0x80008000u;
-      // the four bits d = 4k .. 4k + 3: (hi of ve, hi of vo, lo of ve, lo of vo)
-      const uint32_t nib = (ze >> 31) | ((zo >> 31) << 1) | (((ze >> 15) & 1u) << 2) | (((zo >> 15) & 1u) << 3);
-      if (k < 8) ml |= nib << (4 * k);
-      else mh |= nib << (4 * (k - 8));
+      acc[k >> 3] |= (differs(ve) | (differs(vo) << 1)) << (2 * (k & 7));
     }
+    // (the 2-bit groups of a 16-bit half spread to every other 2-bit slot)
+    auto spread2 = [](uint32_t v) -> uint32_t {
+      v = (v | (v << 8)) & 0x00FF00FFu;
+      v = (v | (v << 4)) & 0x0F0F0F0Fu;
+      return (v | (v << 2)) & 0x33333333u;
+    };
+    const uint32_t ea = ~acc[0], eb = ~acc[1];   // 1: the pair matches
+    const uint32_t ml = spread2(ea >> 16) | (spread2(ea & 0xFFFFu) << 2);
+    const uint32_t mh = spread2(eb >> 16) | (spread2(eb & 0xFFFFu) << 2);
     const uint64_t valid = reach >= 63 ? ~1ull : ((2ull << reach) - 2ull);   // bits 1 .. reach
     const uint64_t m2 = here ? ((((uint64_t)mh << 32) | ml) & valid) : 0ull;
     sm2[0][t] = (uint32_t)m2;
