@@ -1704,18 +1704,32 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
     }
   }
   __syncthreads();
+  // the block-type and block-count codes by thread 0, every work array in LDS (as private
+  // arrays indexed by data they lived in scratch memory: 1.7 KiB a lane, a global round trip
+  // per access of the serial sort and tree walk)
+  __shared__ SerialWs sws;
+  __shared__ uint32_t sbl[16], snx[16];
+  __shared__ uint8_t sdt[kMaxBT + 2], sdc[26];
+  __shared__ uint16_t sct[kMaxBT + 2], scc[26];
   if (t == 0) {
-    uint32_t hcode[kMaxBT + 2], hcount[26];
-    for (int q = 0; q < kMaxBT + 2; q++) hcode[q] = sh_hcode[q];
-    for (int q = 0; q < 26; q++) hcount[q] = sh_hcount[q];
     mb.nbt[cat] = (uint32_t)nt;
-    Codes &cd = codes[m];
-    serial_depths(hcode, nt + 2, 15, cd.btd[cat]);
-    depths_to_codes(cd.btd[cat], nt + 2, cd.btc[cat]);
-    serial_depths(hcount, 26, 15, cd.bcd[cat]);
-    depths_to_codes(cd.bcd[cat], 26, cd.bcc[cat]);
+    serial_depths(sh_hcode, nt + 2, 15, sdt, sws);
+    depths_to_codes(sdt, nt + 2, sct, sbl, snx);
+    serial_depths(sh_hcount, 26, 15, sdc, sws);
+    depths_to_codes(sdc, 26, scc, sbl, snx);
   }
   __syncthreads();
+  {
+    Codes &cd = codes[m];
+    if (t < nt + 2) {
+      cd.btd[cat][t] = sdt[t];
+      cd.btc[cat][t] = sct[t];
+    }
+    if (t < 26) {
+      cd.bcd[cat][t] = sdc[t];
+      cd.bcc[cat][t] = scc[t];
+    }
+  }
   for (int i = t; i < nu; i += kSplitT) {
     Unit &u = U[i];
     u.type[cat] = lty[i];
