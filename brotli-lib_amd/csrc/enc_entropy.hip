@@ -713,6 +713,79 @@ __device__ void tree_depths(const uint32_t *h, const int16_t *sorted, int n, uin
   }
 }
 
+// tree_depths for the Huffman kernel's codes, by the wave (all 64 lanes call it; the same depths
+// and the same success test): the leaf counts are clamped by the wave; lane 0 runs the two-queue
+// merge with the heads of both queues and the entries after them in registers -- each step's
+// compares wait for no LDS read, the next entries load behind them -- and records parent links;
+// the internal nodes' depths follow by one walk down from the root (a parent's index is above
+// its children's), the leaves' by the wave.  (The serial merge and the stack walk re-read every
+// node from LDS: 1.2 M cycles for the largest code of a 1 MiB metablock, r05ah.)
+// par / dint: 2n entries each.
+__device__ bool tree_depths_wave(const uint32_t *h, const int16_t *sorted, int n, uint32_t lc, int limit, uint8_t *depth,
+                                 uint32_t *cnt, int16_t *par, int16_t *dint) {
+  const int lane = threadIdx.x & 63;
+  constexpr uint32_t kInfC = 0xFFFFFFFFu;
+  for (int k = lane; k < n; k += 64) {
+    const uint32_t c = h[sorted[k]];
+    cnt[k] = c > lc ? c : lc;
+  }
+  wave_sync();
+  if (lane == 0) {
+    // leaves 0 .. n-1, internal nodes n+1 .. 2n-1 in creation order (tree_depths' layout); a
+    // queue's head and the entry after it: leaves a, a2 (at i, i + 1), internal b, b2 (at j,
+    // j + 1), an entry not there (yet) being "infinite"; ties take the leaf
+    int i = 0, j = n + 1, made = n;
+    uint32_t a = cnt[0], a2 = n > 1 ? cnt[1] : kInfC, b = kInfC, b2 = kInfC;
+    for (int k = n - 1; k > 0; k--) {
+      const int je = 2 * n - k;
+      int l, r;
+      uint32_t cl, cr;
+      if (a <= b) {
+        l = i++;
+        cl = a;
+        a = a2;
+        a2 = i + 1 < n ? cnt[i + 1] : kInfC;
+      } else {
+        l = j++;
+        cl = b;
+        b = b2;
+        b2 = j + 1 <= made ? cnt[j + 1] : kInfC;
+      }
+      if (a <= b) {
+        r = i++;
+        cr = a;
+        a = a2;
+        a2 = i + 1 < n ? cnt[i + 1] : kInfC;
+      } else {
+        r = j++;
+        cr = b;
+        b = b2;
+        b2 = j + 1 <= made ? cnt[j + 1] : kInfC;
+      }
+      const uint32_t sum = cl + cr;
+      cnt[je] = sum;
+      par[l] = (int16_t)je;
+      par[r] = (int16_t)je;
+      made = je;
+      if (j == je) b = sum;
+      else if (j + 1 == je) b2 = sum;
+    }
+    dint[2 * n - 1] = 0;   // the root
+    for (int x = 2 * n - 2; x > n; x--) dint[x] = (int16_t)(dint[par[x]] + 1);
+  }
+  wave_sync();
+  int mx = 0;
+  for (int k = lane; k < n; k += 64) {
+    const int d = dint[par[k]] + 1;
+    depth[sorted[k]] = (uint8_t)d;
+    mx = max(mx, d);
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+  wave_sync();
+  return mx <= limit;
+}
+
 // Scratch of the serial tree helpers.  The Huffman kernel keeps one in LDS: as private arrays
 // (dynamically indexed, so in scratch memory) they made serialising a code cost ~600-850 K
 // cycles -- most of the kernel (r03m, scripts/huff_timing.py).
@@ -994,7 +1067,7 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
 // type), distance (block type, cluster); slots beyond the metablock's counts are empty.
 // blocks per metablock: the used codes only (literal codes are at most kMaxLitTrees in all)
 #ifdef MIB_PROF   // timing experiment: trees, count-limit attempts, cycles in rank sort / tree / store, per block
-__device__ unsigned long long g_huff_prof[8];
+__device__ unsigned long long g_huff_prof[12];   // + maxima: block, sort, tree, store cycles
 #define HPT() __builtin_amdgcn_s_memtime()
 #else
 #define HPT() 0ull
@@ -1016,7 +1089,6 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ uint8_t depth[AMAX];
   __shared__ uint16_t code[AMAX];
   __shared__ uint8_t buf[kTreeBytes];
-  __shared__ int sh_ok;
   __shared__ TreeScratch ts;
   const int m = blockIdx.x / nr, r = (int)(blockIdx.x % nr);
   const int lane = threadIdx.x;
@@ -1116,16 +1188,12 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
       wave_sync();
       const uint64_t tb = HPT();
       hp_sort += tb - ta;
-      if (lane == 0) {
-        bool ok;
-        tree_depths(h, sorted, n, lc, 15, depth, cnt, left, val, &ok);
-        if (!ok)
-          for (int i = 0; i < asize; i++) depth[i] = 0;
-        sh_ok = ok ? 1 : 0;
-      }
+      const bool ok = tree_depths_wave(h, sorted, n, lc, 15, depth, cnt, val, left);
+      if (!ok)
+        for (int i = lane; i < asize; i += 64) depth[i] = 0;
       wave_sync();
       hp_tree += HPT() - tb;
-      if (sh_ok) break;
+      if (ok) break;
     }
   }
   const uint64_t tc = HPT();
@@ -1180,6 +1248,10 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
     atomicAdd(&g_huff_prof[5], (unsigned long long)(te - hp0));
     atomicAdd(&g_huff_prof[6], (unsigned long long)n);
     if (hp_att > 1) atomicAdd(&g_huff_prof[7], 1ull);
+    atomicMax(&g_huff_prof[8], (unsigned long long)(te - hp0));
+    atomicMax(&g_huff_prof[9], (unsigned long long)hp_sort);
+    atomicMax(&g_huff_prof[10], (unsigned long long)hp_tree);
+    atomicMax(&g_huff_prof[11], (unsigned long long)(te - tc));
   }
 #endif
   wave_sync();
@@ -2165,8 +2237,8 @@ void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, ui
 }  // namespace mib
 #ifdef MIB_PROF
 extern "C" int mib_debug_read_huff_prof(unsigned long long *out) {
-  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_huff_prof), sizeof(unsigned long long) * 8);
-  unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::enc::g_huff_prof), sizeof(unsigned long long) * 12);
+  unsigned long long z[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   hipMemcpyToSymbol(HIP_SYMBOL(mib::enc::g_huff_prof), z, sizeof(z));
   return 0;
 }
