@@ -872,11 +872,10 @@ __device__ void put_varlen_u8(BitW &w, int n) {
 
 // complex prefix code serialisation: run-length code the depths (16 / 17), then a
 // depth-5 code for those (writeHuffmanTree / storeHuffmanTreeOfHuffmanTree)
-__device__ void store_complex(BitW &w, const uint8_t *depth, int asize, TreeScratch &ts) {
+// The run-length codes of depth[0 .. nl) into ts.rle_code / rle_extra; returns their number
+__device__ int rle_depths(const uint8_t *depth, int nl, TreeScratch &ts) {
   uint8_t *rle_code = ts.rle_code, *rle_extra = ts.rle_extra;
   int nr = 0;
-  int nl = asize;
-  while (nl > 0 && depth[nl - 1] == 0) nl--;
   int prev = 8;
   for (int i = 0; i < nl;) {
     int v = depth[i], reps = 1;
@@ -942,9 +941,12 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize, TreeScra
       prev = v;
     }
   }
+  return nr;
+}
+// The code-length code of the histogram ts.clh (limit 5) and its header part: HSKIP and the
+// stored code lengths (storeHuffmanTreeOfHuffmanTree); leaves ts.cld / ts.clc for the symbols
+__device__ void put_cl_code(BitW &w, TreeScratch &ts) {
   uint32_t *clh = ts.clh;
-  for (int k = 0; k < 18; k++) clh[k] = 0;
-  for (int k = 0; k < nr; k++) clh[rle_code[k]]++;
   int ncodes = 0, first = 0;
   for (int k = 0; k < 18; k++)
     if (clh[k]) {
@@ -972,12 +974,80 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize, TreeScra
     w.put(blen[l], sym[l]);
   }
   if (ncodes == 1) cld[first] = 0;
+}
+__device__ void store_complex(BitW &w, const uint8_t *depth, int asize, TreeScratch &ts) {
+  int nl = asize;
+  while (nl > 0 && depth[nl - 1] == 0) nl--;
+  const int nr = rle_depths(depth, nl, ts);
+  uint32_t *clh = ts.clh;
+  for (int k = 0; k < 18; k++) clh[k] = 0;
+  for (int k = 0; k < nr; k++) clh[ts.rle_code[k]]++;
+  put_cl_code(w, ts);
   for (int k = 0; k < nr; k++) {
-    int c = rle_code[k];
-    w.put(cld[c], clc[c]);
-    if (c == 16) w.put(2, rle_extra[k]);
-    else if (c == 17) w.put(3, rle_extra[k]);
+    int c = ts.rle_code[k];
+    w.put(ts.cld[c], ts.clc[c]);
+    if (c == 16) w.put(2, ts.rle_extra[k]);
+    else if (c == 17) w.put(3, ts.rle_extra[k]);
   }
+}
+// store_complex with the wave (all 64 lanes call it; w is lane 0's writer, the others' copies
+// follow its position): the last used symbol by ballots, the run-length codes' histogram by LDS
+// atomics, and their bits -- each lane one code's, placed by a wave prefix sum and ORed into the
+// 4-byte-aligned buffer -- around lane 0's serial run-length coding and code-length code.
+// (Serially, the scan, the histogram and the writes were three dependent LDS round trips a
+// code: ~2/3 of a 704-symbol code's 0.6 M cycles, r05ai.)
+__device__ void store_complex_wave(BitW &w, const uint8_t *depth, int asize, TreeScratch &ts, uint32_t *buf32, int *sh_nr) {
+  const int lane = threadIdx.x & 63;
+  int nl = 0;
+  for (int x0 = (asize - 1) & ~63; x0 >= 0; x0 -= 64) {
+    const int x = x0 + lane;
+    const uint64_t m = __ballot(x < asize && depth[x] != 0);
+    if (m) {
+      nl = x0 + 64 - __clzll((long long)m);
+      break;
+    }
+  }
+  if (lane < 18) ts.clh[lane] = 0;
+  if (lane == 0) *sh_nr = rle_depths(depth, nl, ts);
+  wave_sync();
+  const int nr = *sh_nr;
+  for (int k = lane; k < nr; k += 64) atomicAdd(&ts.clh[ts.rle_code[k]], 1u);
+  wave_sync();
+  if (lane == 0) {
+    put_cl_code(w, ts);
+    w.flush();
+  }
+  wave_sync();
+  uint64_t pos = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w.pos) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w.pos >> 32)) << 32);
+  for (int k0 = 0; k0 < nr; k0 += 64) {
+    const int k = k0 + lane;
+    uint32_t nb = 0, v = 0;
+    if (k < nr) {
+      const int c = ts.rle_code[k];
+      const uint32_t d = ts.cld[c], ne = c == 16 ? 2u : c == 17 ? 3u : 0u;
+      nb = d + ne;
+      v = (uint32_t)ts.clc[c] | ((uint32_t)ts.rle_extra[k] << d);
+    }
+    uint32_t incl = nb;   // wave inclusive prefix sum of the codes' bit counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (nb) {
+      const uint64_t b = pos + incl - nb;
+      const uint32_t wi = (uint32_t)(b >> 5), sh = (uint32_t)(b & 31);
+      const uint64_t x = (uint64_t)v << sh;
+      atomicOr(buf32 + wi, (uint32_t)x);
+      if (sh + nb > 32) atomicOr(buf32 + wi + 1, (uint32_t)(x >> 32));
+    }
+    pos += (uint32_t)__shfl((int)incl, 63);
+  }
+  wave_sync();
+  w.pos = pos;
+  w.acc = 0;
+  w.nacc = 0;
 }
 
 // One prefix code: simple form for up to 4 used symbols (zero-length codeword for one),
@@ -1088,7 +1158,8 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ int16_t left[2 * AMAX + 2], val[2 * AMAX + 2];
   __shared__ uint8_t depth[AMAX];
   __shared__ uint16_t code[AMAX];
-  __shared__ uint8_t buf[kTreeBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kTreeBytes];   // (words for store_complex_wave)
+  __shared__ int sh_nr;
   __shared__ TreeScratch ts;
   const int m = blockIdx.x / nr, r = (int)(blockIdx.x % nr);
   const int lane = threadIdx.x;
@@ -1232,10 +1303,17 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
     }
     wave_sync();
   }
-  if (lane == 0) {
+  {
     BitW w{buf, 0};
-    store_code(w, n, nzs, max_bits, depth, code, asize, ts, n > 1);
-    mb.tree_bits[t] = (uint32_t)w.pos;
+    if (n > 4) {   // the complex form (the codes are assigned above)
+      store_complex_wave(w, depth, asize, ts, reinterpret_cast<uint32_t *>(buf), &sh_nr);
+    } else if (lane == 0) {
+      store_code(w, n, nzs, max_bits, depth, code, asize, ts, n > 1);
+    }
+    if (lane == 0) {
+      w.flush();
+      mb.tree_bits[t] = (uint32_t)w.pos;
+    }
   }
 #ifdef MIB_PROF
   if (lane == 0) {
