@@ -873,7 +873,7 @@ __device__ void put_varlen_u8(BitW &w, int n) {
 // complex prefix code serialisation: run-length code the depths (16 / 17), then a
 // depth-5 code for those (writeHuffmanTree / storeHuffmanTreeOfHuffmanTree)
 // The run-length codes of depth[0 .. nl) into ts.rle_code / rle_extra; returns their number
-__device__ int rle_depths(const uint8_t *depth, int nl, TreeScratch &ts) {
+__device__ __forceinline__ int rle_depths(const uint8_t *depth, int nl, TreeScratch &ts) {
   uint8_t *rle_code = ts.rle_code, *rle_extra = ts.rle_extra;
   int nr = 0;
   int prev = 8;
@@ -943,9 +943,11 @@ __device__ int rle_depths(const uint8_t *depth, int nl, TreeScratch &ts) {
   }
   return nr;
 }
+__device__ const uint8_t kClOrder[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
+__device__ const uint8_t kClSym[6] = {0, 7, 3, 2, 1, 15}, kClLen[6] = {2, 4, 3, 2, 2, 4};
 // The code-length code of the histogram ts.clh (limit 5) and its header part: HSKIP and the
 // stored code lengths (storeHuffmanTreeOfHuffmanTree); leaves ts.cld / ts.clc for the symbols
-__device__ void put_cl_code(BitW &w, TreeScratch &ts) {
+__device__ __forceinline__ void put_cl_code(BitW &w, TreeScratch &ts) {
   uint32_t *clh = ts.clh;
   int ncodes = 0, first = 0;
   for (int k = 0; k < 18; k++)
@@ -957,9 +959,8 @@ __device__ void put_cl_code(BitW &w, TreeScratch &ts) {
   uint16_t *clc = ts.clc;
   small_depths(clh, 18, 5, cld, ts);
   depths_to_codes(cld, 18, clc, ts.bl, ts.next);
-  const int order[18] = {1, 2, 3, 4, 0, 5, 17, 6, 16, 7, 8, 9, 10, 11, 12, 13, 14, 15};
-  const uint32_t sym[6] = {0, 7, 3, 2, 1, 15};
-  const int blen[6] = {2, 4, 3, 2, 2, 4};
+  // (tables in constant memory: as local arrays indexed by data they were copied to scratch)
+  const uint8_t *order = kClOrder, *sym = kClSym, *blen = kClLen;
   int to_store = 18;
   if (ncodes > 1)
     while (to_store > 0 && cld[order[to_store - 1]] == 0) to_store--;
@@ -990,6 +991,38 @@ __device__ void store_complex(BitW &w, const uint8_t *depth, int asize, TreeScra
     else if (c == 17) w.put(3, ts.rle_extra[k]);
   }
 }
+// Bits of `count` items by the wave at lane 0's writer position (all 64 lanes call it; lane 0
+// has flushed w): item k's (bits, value) from item(k), placed by a wave prefix sum and ORed into
+// the zeroed, 4-byte-aligned buffer; every lane's w then continues after them.
+template <class F>
+__device__ void wave_put_items(BitW &w, uint32_t *buf32, int count, F item) {
+  const int lane = threadIdx.x & 63;
+  uint64_t pos = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w.pos) |
+                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w.pos >> 32)) << 32);
+  for (int k0 = 0; k0 < count; k0 += 64) {
+    const int k = k0 + lane;
+    uint32_t nb = 0, v = 0;
+    if (k < count) item(k, nb, v);
+    uint32_t incl = nb;   // inclusive prefix sum of the items' bit counts
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
+      if (lane >= o) incl += y;
+    }
+    if (nb) {
+      const uint64_t b = pos + incl - nb;
+      const uint32_t wi = (uint32_t)(b >> 5), sh = (uint32_t)(b & 31);
+      const uint64_t x = (uint64_t)v << sh;
+      atomicOr(buf32 + wi, (uint32_t)x);
+      if (sh + nb > 32) atomicOr(buf32 + wi + 1, (uint32_t)(x >> 32));
+    }
+    pos += (uint32_t)__shfl((int)incl, 63);
+  }
+  wave_sync();
+  w.pos = pos;
+  w.acc = 0;
+  w.nacc = 0;
+}
 // store_complex with the wave (all 64 lanes call it; w is lane 0's writer, the others' copies
 // follow its position): the last used symbol by ballots, the run-length codes' histogram by LDS
 // atomics, and their bits -- each lane one code's, placed by a wave prefix sum and ORed into the
@@ -1018,36 +1051,12 @@ __device__ void store_complex_wave(BitW &w, const uint8_t *depth, int asize, Tre
     w.flush();
   }
   wave_sync();
-  uint64_t pos = (uint64_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)w.pos) |
-                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(w.pos >> 32)) << 32);
-  for (int k0 = 0; k0 < nr; k0 += 64) {
-    const int k = k0 + lane;
-    uint32_t nb = 0, v = 0;
-    if (k < nr) {
-      const int c = ts.rle_code[k];
-      const uint32_t d = ts.cld[c], ne = c == 16 ? 2u : c == 17 ? 3u : 0u;
-      nb = d + ne;
-      v = (uint32_t)ts.clc[c] | ((uint32_t)ts.rle_extra[k] << d);
-    }
-    uint32_t incl = nb;   // wave inclusive prefix sum of the codes' bit counts
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, o);
-      if (lane >= o) incl += y;
-    }
-    if (nb) {
-      const uint64_t b = pos + incl - nb;
-      const uint32_t wi = (uint32_t)(b >> 5), sh = (uint32_t)(b & 31);
-      const uint64_t x = (uint64_t)v << sh;
-      atomicOr(buf32 + wi, (uint32_t)x);
-      if (sh + nb > 32) atomicOr(buf32 + wi + 1, (uint32_t)(x >> 32));
-    }
-    pos += (uint32_t)__shfl((int)incl, 63);
-  }
-  wave_sync();
-  w.pos = pos;
-  w.acc = 0;
-  w.nacc = 0;
+  wave_put_items(w, buf32, nr, [&](int k, uint32_t &nb, uint32_t &v) {
+    const int c = ts.rle_code[k];
+    const uint32_t d = ts.cld[c], ne = c == 16 ? 2u : c == 17 ? 3u : 0u;
+    nb = d + ne;
+    v = (uint32_t)ts.clc[c] | ((uint32_t)ts.rle_extra[k] << d);
+  });
 }
 
 // One prefix code: simple form for up to 4 used symbols (zero-length codeword for one),
@@ -1093,6 +1102,8 @@ struct SerialWs {
   int16_t sorted[80];
   uint32_t cnt[2 * 80 + 2];
   int16_t left[2 * 80 + 2], val[2 * 80 + 2];
+  int16_t nz[80];   // (serial_depths_wave: the used symbols)
+  int n;
 };
 __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *depth, SerialWs &ws) {
   int16_t *sorted = ws.sorted, *left = ws.left, *val = ws.val;
@@ -1131,6 +1142,61 @@ __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *de
 __device__ void serial_depths(const uint32_t *h, int len, int limit, uint8_t *depth) {
   SerialWs ws;
   serial_depths(h, len, limit, depth, ws);
+}
+// serial_depths by the wave (all 64 lanes call it; the same depths): the used symbols compacted
+// by ballots, ranked by (clamped count, descending symbol) with every lane comparing its symbols
+// against all keys, the tree by tree_depths_wave.  (Serially the insertion sort alone re-read two
+// LDS words per step: ~0.4 M cycles for an 80-symbol context-map code, r05.)
+__device__ void serial_depths_wave(const uint32_t *h, int len, int limit, uint8_t *depth, SerialWs &ws) {
+  const int lane = threadIdx.x & 63;
+  int n = 0;
+  for (int c0 = 0; c0 < len; c0 += 64) {
+    const int i = c0 + lane;
+    const bool f = i < len && h[i] != 0;
+    const uint64_t m = __ballot(f);
+    if (i < len) depth[i] = 0;
+    if (f) ws.nz[n + __popcll(m & ((1ull << lane) - 1))] = (int16_t)i;
+    n += __popcll(m);
+  }
+  wave_sync();
+  if (n == 0) return;
+  if (n == 1) {
+    if (lane == 0) depth[ws.nz[0]] = 1;
+    wave_sync();
+    return;
+  }
+  uint64_t *keys = reinterpret_cast<uint64_t *>(ws.cnt);   // (80 keys; the tree reuses cnt after the sort)
+  static_assert(sizeof(ws.cnt) >= 80 * sizeof(uint64_t), "the sort keys fit cnt");
+  for (uint32_t lc = 1;; lc *= 2) {
+    uint64_t mine[2] = {~0ull, ~0ull};
+    int16_t ms[2] = {0, 0};
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+      const int a = lane + 64 * q;
+      if (a < n) {
+        const int si = ws.nz[a];
+        const uint32_t ci = h[si] > lc ? h[si] : lc;
+        mine[q] = ((uint64_t)ci << 16) | (uint32_t)(0xFFFF - si);
+        ms[q] = (int16_t)si;
+        keys[a] = mine[q];
+      }
+    }
+    wave_sync();
+    uint32_t rk[2] = {0u, 0u};
+    for (int b = 0; b < n; b++) {
+      const uint64_t kb = keys[b];
+      rk[0] += kb < mine[0] ? 1u : 0u;
+      rk[1] += kb < mine[1] ? 1u : 0u;
+    }
+    wave_sync();   // (the keys are read before the tree overwrites cnt)
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+      if (lane + 64 * q < n) ws.sorted[rk[q]] = ms[q];
+    wave_sync();
+    if (tree_depths_wave(h, ws.sorted, n, lc, limit, depth, ws.cnt, ws.val, ws.left)) return;
+    for (int i = lane; i < len; i += 64) depth[i] = 0;
+    wave_sync();
+  }
 }
 
 // Block (one wave) per (metablock, code slot): literal (block type, cluster), command (block
@@ -1988,6 +2054,89 @@ __device__ void encode_context_map(BitW &w, const uint8_t *cmap, int size, int n
   w.put(1, 1);   // IMTF
 }
 
+// encode_context_map by the wave (all 64 lanes call it; w is lane 0's writer): lane 0 forms the
+// run-length symbols, the wave counts them, builds their code (serial_depths_wave) and writes
+// them (wave_put_items) around lane 0's code header.  cnt2: two LDS ints.
+__device__ void encode_context_map_wave(BitW &w, const uint8_t *cmap, int size, int ntrees, CmapWs &ws, uint32_t *buf32,
+                                        int *cnt2) {
+  const int lane = threadIdx.x & 63;
+  if (lane == 0) put_varlen_u8(w, ntrees - 1);
+  if (ntrees <= 1) return;
+  uint8_t *v = ws.v, *sym = ws.sym, *nb = ws.nb, *depth = ws.depth;
+  uint16_t *ex = ws.ex, *code = ws.code;
+  uint32_t *hist = ws.hist;
+  int16_t *nzs = ws.nzs;
+  if (lane == 0) {
+    int maxrun = 0;
+    for (int i = 0; i < size;) {
+      int r = 0;
+      while (i + r < size && v[i + r] == 0) r++;
+      if (r > maxrun) maxrun = r;
+      i += r ? r : 1;
+    }
+    int rlemax = 0;
+    while ((2 << rlemax) <= maxrun && rlemax < 16) rlemax++;   // largest p with 2^p <= maxrun
+    int ns = 0;
+    for (int i = 0; i < size;) {
+      if (v[i] != 0) {
+        sym[ns] = (uint8_t)(v[i] + rlemax);
+        nb[ns] = 0;
+        ex[ns++] = 0;
+        i++;
+        continue;
+      }
+      int L = 0;
+      while (i + L < size && v[i + L] == 0) L++;
+      i += L;
+      while (L > 0) {
+        if (L == 1 || rlemax == 0) {
+          sym[ns] = 0;
+          nb[ns] = 0;
+          ex[ns++] = 0;
+          L--;
+          continue;
+        }
+        int p = 0;
+        while ((2 << p) <= L && p < rlemax) p++;
+        const int extra = min(L - (1 << p), (1 << p) - 1);
+        sym[ns] = (uint8_t)p;
+        nb[ns] = (uint8_t)p;
+        ex[ns++] = (uint16_t)extra;
+        L -= (1 << p) + extra;
+      }
+    }
+    cnt2[0] = ns;
+    cnt2[1] = rlemax;
+  }
+  wave_sync();
+  const int ns = cnt2[0], rlemax = cnt2[1];
+  const int asize = ntrees + rlemax;
+  for (int i = lane; i < asize; i += 64) hist[i] = 0;
+  wave_sync();
+  for (int k = lane; k < ns; k += 64) atomicAdd(&hist[sym[k]], 1u);
+  wave_sync();
+  serial_depths_wave(hist, asize, 15, depth, ws.sw);
+  if (lane == 0) {
+    w.put(1, rlemax > 0 ? 1 : 0);
+    if (rlemax) w.put(4, (uint32_t)(rlemax - 1));
+    int n = 0;
+    for (int i = 0; i < asize; i++)
+      if (hist[i]) nzs[n++] = (int16_t)i;
+    int max_bits = 0;
+    for (int c = asize - 1; c; c >>= 1) max_bits++;
+    store_code(w, n, nzs, max_bits, depth, code, asize, ws.ts, false);
+    w.flush();
+  }
+  wave_sync();
+  wave_put_items(w, buf32, ns, [&](int k, uint32_t &bits, uint32_t &val) {
+    const int c = sym[k];
+    const uint32_t d = depth[c];
+    bits = d + nb[k];
+    val = (uint32_t)code[c] | ((uint32_t)ex[k] << d);
+  });
+  if (lane == 0) w.put(1, 1);   // IMTF
+}
+
 // NBLTYPES and, for a split category, its block type and block count prefix codes and the
 // first block count (storeBlockSwitch's header part, metablock.ts:150-220)
 __device__ void put_block_split(BitW &w, int nbt, uint8_t *td, uint16_t *tc, uint8_t *cdp, uint16_t *cc, uint32_t first,
@@ -2016,7 +2165,8 @@ __device__ void put_block_split(BitW &w, int nbt, uint8_t *td, uint16_t *tc, uin
 // arrays were global / scratch memory round trips, 0.8 ms for a single metablock (a 1 MiB
 // streaming chunk, r05m) -- then copied out by the wave.
 __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs, int nmbs, uint8_t *hdr, Codes *codes) {
-  __shared__ uint8_t hb[kHdrBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t hb[kHdrBytes];   // (words for the wave writers)
+  __shared__ int sh_cm[2];
   __shared__ uint8_t map[kLitSlots];
   __shared__ int16_t nzs[26];
   __shared__ int sh_n, sh_ntrees;
@@ -2095,7 +2245,7 @@ __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs,
     wave_sync();
     if (sh_ntrees > 1) mtf_wave(map, sh_n, cws.v);
     wave_sync();
-    if (t == 0) encode_context_map(w, map, sh_n, sh_ntrees, cws);
+    encode_context_map_wave(w, map, sh_n, sh_ntrees, cws, reinterpret_cast<uint32_t *>(hb), sh_cm);
     wave_sync();
   }
   if (t == 0) {
