@@ -215,6 +215,10 @@ int decode_shard(Shard &sh, const mib_span *in, const std::vector<size_t> &idx, 
   return 0;
 }
 
+// mib_force_shards (tests): the shard path even on one device, so a one-GPU box exercises it
+int g_force_shards = 0;
+bool force_shards() { return __atomic_load_n(&g_force_shards, __ATOMIC_RELAXED) != 0; }
+
 // run fn(shard, indices) on `shards` host threads; the first error wins.  per_device: at most
 // one shard per device, a device's streams in one call (the decoder: four 256-stream shards on
 // one GPU left one shard's kernel queued behind the others' on a shared hardware queue, 298 vs
@@ -265,8 +269,9 @@ int mib_encode_batch_n(const mib_span *in, size_t k, const mib_enc_opts *o, int 
     if ((!in[i].data && in[i].size) || in[i].size >= (1ull << 31)) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
-  // (encode shards may share a device: their uploads and downloads overlap the others' kernels,
-  // 250-303 ms against one context's 268-281 on one GPU, r05v)
+  // one device (or one shard asked for): the one-context call -- shards sharing a GPU encoded in
+  // 287-316 ms what the default context does in 261 (r05final3), and varied from run to run
+  if ((n_gpus == 1 || device_count() == 1) && !force_shards()) return mib_encode_batch(in, k, o, out, status);
   const int rc = run_shards(in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) {
     return encode_shard(sh, in, idx, o, out, status);
   });
@@ -284,6 +289,7 @@ int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, i
     if (!in[i].data && in[i].size) return MIB_E_INVALID_ARG;
   }
   if (!k) return 0;
+  if ((n_gpus == 1 || device_count() == 1) && !force_shards()) return mib_decode_batch(in, k, out, status);   // (as for the encode)
   const int rc = run_shards(
       in, k, n_gpus, [&](Shard &sh, const std::vector<size_t> &idx) { return decode_shard(sh, in, idx, out, status); },
       true);
@@ -293,5 +299,7 @@ int mib_decode_batch_n(const mib_span *in, size_t k, int n_gpus, mib_buf *out, i
 }
 
 int mib_device_count(void) { return device_count(); }
+
+void mib_force_shards(int force) { __atomic_store_n(&g_force_shards, force ? 1 : 0, __ATOMIC_RELAXED); }
 
 }  // extern "C"

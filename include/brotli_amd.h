@@ -122,6 +122,10 @@ int64_t mib_selftest_lds_atomic_order(int trials);
  * items by wave ballots instead (same stream bytes, slower).  Test hook: force = 1 makes
  * every device take the ballot ranking, 0 restores the self-test's choice. */
 void mib_force_ballot_rank(int force);
+/* Diagnostic (tests): non-zero makes mib_encode_batch_n / mib_decode_batch_n shard even when one
+ * device is visible (by default a single device runs them as mib_encode_batch / mib_decode_batch,
+ * one launch sequence). */
+void mib_force_shards(int force);
 
 void mib_buf_free(mib_buf *b);
 /* The allocator behind every mib_buf the library returns (default malloc / free), in the

@@ -1,4 +1,4 @@
-# r05v: the host batch leg (decode shards capped at one per device; results freed outside the timed calls), twice; multi tests
+# r05v: the host batch leg (one device: the sharded calls run as the one-context batch), three runs; multi tests (shards forced)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

@@ -1,10 +1,13 @@
 """Batches sharded over GPUs inside the C ABI (mib_encode_batch_n / mib_decode_batch_n,
 brotli-lib_amd/csrc/multi.cpp; SURVEY.md §8(b),(e)).  Shard s runs on device s % device count,
-so on a one-GPU box two shards share device 0 and these tests exercise the real sharding:
+so on a one-GPU box two shards share device 0 and these tests exercise the real sharding
+(forced by mib_force_shards: by default one device runs the one-context calls):
 size-balanced assignment, one host thread and context per shard, results back in input
 order.  The 8-GPU node itself is the driver's; here the streams must equal the one-GPU
 batch byte for byte (each stream's encoding depends on its own bytes only) and decode to
 the inputs on the HIP decoder and the oracle."""
+import ctypes
+
 import pytest
 
 import _oracle
@@ -12,6 +15,18 @@ import brotli_amd
 from brotli_amd import datagen
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _shard_path():
+    # one device runs the sharded calls as the one-context batch; the tests force the shard
+    # machinery (threads, contexts, assignment) onto it
+    lib = brotli_amd._L()
+    lib.mib_force_shards.restype = None
+    lib.mib_force_shards.argtypes = [ctypes.c_int]
+    lib.mib_force_shards(1)
+    yield
+    lib.mib_force_shards(0)
 
 
 def _mixed():
@@ -32,6 +47,15 @@ def test_sharded_encode_equals_single(gpus):
     assert dec == bufs
     for i in (3, 10, len(bufs) - 1):
         assert _oracle.decode(many[i]) == bufs[i]
+
+
+def test_single_device_runs_the_one_context_call():
+    lib = brotli_amd._L()
+    lib.mib_force_shards(0)
+    bufs = _mixed()[:12]
+    one = brotli_amd.encode_batch(bufs, {'quality': 11})
+    assert brotli_amd.encode_batch(bufs, {'quality': 11}, gpus=4) == one
+    assert brotli_amd.decode_batch(one, gpus=4) == bufs
 
 
 def test_sharded_decode_errors_stay_in_their_slots():
