@@ -2379,7 +2379,9 @@ void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *unit
   // the rest (if any: literals of the metablocks of up to kSplitWideUnits units)
   const bool wide_short = std::max(sk.k[0], std::max(sk.k[1], sk.k[2])) > 4;
   const bool wide_long = std::max(std::min(sk.k[0], 4), std::max(sk.k[1], sk.k[2])) > 4;
-  const bool narrow = std::min(sk.k[0], std::min(sk.k[1], sk.k[2])) <= 4 || max_units > kSplitWideUnits;
+  // (FONT metablocks cap literal types at 4 whatever k[0] is: with k[0] > 4 the S = 4 launch must
+  // run for them even when no other block needs it -- ADVICE r4, an experiment-override case)
+  const bool narrow = std::min(sk.k[0], std::min(sk.k[1], sk.k[2])) <= 4 || max_units > kSplitWideUnits || sk.k[0] > 4;
   const size_t lds4 = (size_t)std::max(1, std::min(max_units, kMaxUnits)) * 4 * sizeof(float);
   const size_t lds8 = (size_t)std::max(1, std::min(wide_long ? max_units : max_short_units, kMaxUnits)) * kMaxBT * sizeof(float);
   static const bool attr = [] {   // (dynamic LDS past 64 KiB: 16 MiB metablocks)

@@ -17,6 +17,18 @@ lib = brotli_amd._L()
 prof = (ctypes.c_ulonglong * 8)()
 names = ['load', 'seed', 'histo', 'costs', 'unit_costs', 'path', 'final', 'tail']
 ctx = brotli_amd.DeviceContext(0, profiling=True)
+if os.environ.get('CADENCE'):   # the reference's cadence: one BrotliEncoder, 1 MiB update() calls
+    from brotli_amd import datagen
+    text = datagen.enwik_text(16 << 20, 3)
+    lib.mib_debug_read_split_prof(prof)
+    enc = brotli_amd.BrotliEncoder({'quality': 9, 'lgwin': 24})
+    for i in range(16):
+        enc.update(text[i << 20:(i + 1) << 20])
+    enc.finish()
+    lib.mib_debug_read_split_prof(prof)
+    nblk = 3 * 17   # (metablocks: 16 chunks + the final one; three categories)
+    print('cadence', {n: round(v / nblk) for n, v in zip(names, list(prof))}, flush=True)
+    sys.exit(0)
 for wl in os.environ.get('WLS', 'c2,c4').split(','):
     k, size, mode, _, _ = bench.WORKLOADS[wl]
     data = bench.make_inputs(wl, k, size, 0, dev)
