@@ -51,6 +51,12 @@ constexpr int kCmdSlot = kLitSlots;
 constexpr int kDistSlot = kCmdSlot + kMaxBT;
 constexpr int kTreeSlots = kDistSlot + kMaxBT * kDistCtx;
 constexpr int kBlock = 256;                   // threads of the per-segment entropy / emit blocks
+constexpr int kMaxPieceShift = 6;             // parse pieces per segment: at most 2^6 (encode.hip)
+// a segment's commands fill at most kSeg / 2 + 4 + (2 << kMaxPieceShift) slots (its cmds span,
+// encode.hip); sizes_kernel records their bits per tile of kEmitTile commands, so emit_kernel
+// can write a segment's tiles from blocks of their own
+constexpr int kEmitTile = 512;
+constexpr int kEmitTiles = (int)((kSeg / 2 + 4 + (2u << kMaxPieceShift) + kEmitTile - 1) / kEmitTile);
 
 struct Job {                // one stream (or streaming chunk) to encode
   const uint8_t *data;      // its bytes (device)
@@ -500,11 +506,11 @@ void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t
 void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
                     const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr);
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
-                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units);
+                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units, uint32_t *tile_bits);
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out);
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
-                 const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint8_t *trees, const uint8_t *hdr,
-                 uint8_t *out);
+                 const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint32_t *tile_bits,
+                 const uint8_t *trees, const uint8_t *hdr, uint8_t *out);
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out);
 struct PushSum;
 void launch_ring_scan(hipStream_t st, Job *jobs, int njobs, Seg *segs, int nsegs, const RawCmd *raw, PushSum *push);

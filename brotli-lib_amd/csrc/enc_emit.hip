@@ -199,17 +199,21 @@ __device__ __forceinline__ bool item_packed(const Codes &cd, const Mb &mb, const
   return true;
 }
 
-// Block per segment.  The segment's commands are taken kBlock at a time and expanded into
-// their items (header, literals, distance); kEmitItems items per lane per tile get their bit
-// offsets from a block scan and are ORed into an LDS window, which is then stored as whole
-// words (the tile's first and last word are ORed: neighbours share them).  A tile is at most
+// Blocks per segment: block (s, y) writes segment s's tiles of kEmitTile commands y, y +
+// gridDim.y, ...; a tile starts at the segment's bit offset plus its earlier tiles' bits
+// (sizes_kernel's tile_bits), so a call of few segments (a streaming chunk: 16) still spreads
+// its commands over many blocks.  A tile's commands are taken kBlock at a time and expanded
+// into their items (header, literals, distance); kEmitItems items per lane per pass get their
+// bit offsets from a block scan and are ORed into an LDS window, which is then stored as whole
+// words (the pass's first and last word are ORed: neighbours share them).  A pass is at most
 // kBlock * kEmitItems items of <= 180 bits, so it always fits the window.
 constexpr int kWinWords = 8192;   // 32 KiB = 262144 bits
 constexpr int kEmitItems = 4;
 static_assert(kBlock * kEmitItems * 180 <= kWinWords * 32 - 64, "emit tile must fit the LDS window");
 __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                       const uint32_t *cmd_pos, const Codes *codes, const Unit *units,
-                                                      uint8_t *out) {
+                                                      const uint32_t *tile_bits, uint8_t *out) {
+  static_assert(kEmitTile % kBlock == 0, "a tile is whole command blocks");
   typedef hipcub::BlockScan<uint32_t, kBlock> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t win[kWinWords];
@@ -217,10 +221,29 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   __shared__ Cmd sh_c[kBlock];
   __shared__ uint32_t sh_p[kBlock];
   __shared__ Unit sh_u[kSubPerSeg];
+  __shared__ uint32_t sh_tile[kEmitTiles];   // the tiles' bit offsets within the segment
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
+  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  const uint32_t ntile = (n + kEmitTile - 1) / kEmitTile;
+  if (blockIdx.y >= ntile) return;
   const int t = threadIdx.x;
+  if (t < 64) {   // exclusive prefix sum of the tile sizes (at most 65), a wave step of 64
+    const uint32_t *tb = tile_bits + (size_t)blockIdx.x * kEmitTiles;
+    uint32_t carry = 0;
+    for (uint32_t q0 = 0; q0 < ntile; q0 += 64) {
+      const uint32_t q = q0 + t, v = q < ntile ? tb[q] : 0;
+      uint32_t inc = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (t >= o) inc += y;
+      }
+      if (q < ntile) sh_tile[q] = carry + inc - v;
+      carry += __shfl(inc, 63);
+    }
+  }
   const Codes &cd = codes[sg.mb];
   const Mb &mb = mbs[sg.mb];
   __shared__ uint8_t sh_lut[512];   // per-literal lookups from LDS
@@ -232,11 +255,13 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
   uint32_t *words = reinterpret_cast<uint32_t *>(out + jb.out_off);
   const Cmd *c = cmds + sg.cmd_off;
   const uint32_t *cp = cmd_pos + sg.cmd_off;
-  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
   if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
-  uint64_t bitpos = sg.bit_off;
-  for (uint32_t base = 0; base < n; base += kBlock) {
-    const uint32_t nb = min((uint32_t)kBlock, n - base);
+  __syncthreads();
+  for (uint32_t tile = blockIdx.y; tile < ntile; tile += gridDim.y) {
+  uint64_t bitpos = sg.bit_off + sh_tile[tile];
+  const uint32_t tend = min(n, (tile + 1) * kEmitTile);
+  for (uint32_t base = tile * kEmitTile; base < tend; base += kBlock) {
+    const uint32_t nb = min((uint32_t)kBlock, tend - base);
     uint32_t cnt = 0;
     if ((uint32_t)t < nb) {
       sh_c[t] = c[base + t];
@@ -311,6 +336,7 @@ __global__ __launch_bounds__(kBlock) void emit_kernel(const Job *jobs, const Seg
       __syncthreads();
     }
   }
+  }
 }
 
 // quality 0 / n < 64 (encode.ts:105-138, storeUncompressedMetaBlock metablock.ts:821-850), the
@@ -378,10 +404,15 @@ __global__ void pack_kernel(const Job *jobs, const uint64_t *dst_off, const uint
 
 
 void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const Seg *segs, int nsegs, const Cmd *cmds,
-                 const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint8_t *trees, const uint8_t *hdr,
-                 uint8_t *out) {
+                 const uint32_t *cmd_pos, const Codes *codes, const Unit *units, const uint32_t *tile_bits,
+                 const uint8_t *trees, const uint8_t *hdr, uint8_t *out) {
   if (nmbs) hipLaunchKernelGGL(headers_kernel, dim3(nmbs), dim3(64), 0, st, jobs, mbs, nmbs, hdr, trees, out);
-  hipLaunchKernelGGL(emit_kernel, dim3(nsegs), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, out);
+  // blocks per segment: enough for ~2,048 blocks (a batch of >= 2,048 segments: one, each
+  // looping over its tiles); blocks past a segment's last tile return at once
+  static const int target = knob("MIB_EMIT_BLOCKS") ? std::max(1, atoi(knob("MIB_EMIT_BLOCKS"))) : 2048;   // (experiments)
+  const int per = std::min(kEmitTiles, std::max(1, (target + nsegs - 1) / std::max(nsegs, 1)));
+  hipLaunchKernelGGL(emit_kernel, dim3(nsegs, per), dim3(kBlock), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units,
+                     tile_bits, out);
 }
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out) {
   hipLaunchKernelGGL(uncompressed_kernel, dim3((unsigned)njobs), dim3(256), 0, st, jobs, njobs, out);

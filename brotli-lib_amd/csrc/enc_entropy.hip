@@ -1866,7 +1866,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   uint8_t *lty = reinterpret_cast<uint8_t *>(bp);
   __shared__ int sh_first[kMaxBT + 1];   // first non-empty unit of each type; [kMaxBT]: of any
   __shared__ uint8_t sh_map[kMaxBT];
-  __shared__ uint32_t sh_hcode[kMaxBT + 2], sh_hcount[26], sh_nsw;
+  __shared__ uint32_t sh_hcode[kMaxBT + 2], sh_hcount[26];
   if (t <= kMaxBT) sh_first[t] = 0x7FFFFFFF;
   if (t < kMaxBT + 2) sh_hcode[t] = 0;
   if (t < 26) sh_hcount[t] = 0;
@@ -2259,12 +2259,15 @@ __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs,
 
 // ---------------------------------------------------------------- sizes: block per segment
 // The segment's bit size: the sum of item_bits over its commands' items (the same
-// load-balanced expansion as emit_kernel, so literal-heavy segments use every lane).
+// load-balanced expansion as emit_kernel, so literal-heavy segments use every lane), kept per
+// tile of kEmitTile commands too (tile_bits[segment][tile]: emit_kernel's tile offsets).
 template <int NT>
 __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
-                                                       const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
+                                                       const uint32_t *cmd_pos, const Codes *codes, const Unit *units,
+                                                       uint32_t *tile_bits) {
+  static_assert(kEmitTile % NT == 0, "a tile is whole iterations");
   typedef hipcub::BlockScan<uint32_t, NT> Scan;
-  typedef hipcub::BlockReduce<unsigned long long, NT> Reduce;
+  typedef hipcub::BlockReduce<uint32_t, NT> Reduce;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ typename Reduce::TempStorage red_tmp;
   __shared__ ItemMap<NT> map;
@@ -2285,7 +2288,9 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
   const uint8_t *lut = sh_lut;
   const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
   if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
-  unsigned long long bits = 0;
+  uint32_t *tb = tile_bits + (size_t)blockIdx.x * kEmitTiles;
+  unsigned long long total = 0;   // (thread 0)
+  uint32_t tile = 0;              // (thread 0: the current tile's bits so far)
   for (uint32_t base = 0; base < n; base += NT) {
     const uint32_t nb = min((uint32_t)NT, n - base);
     uint32_t cnt = 0;
@@ -2299,14 +2304,23 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
     map.off[t] = off;
     if (t == 0) map.off[nb] = nitems;
     __syncthreads();
+    uint32_t bits = 0;
     for (uint32_t i = t; i < nitems; i += NT) {
       const uint32_t j = map.find(i, nb);
       const uint32_t p = sh_p[j];
       bits += item_bits(cd, mb, sh_cmap, lut, jb, sh_c[j], p, sg, sh_u, base + j, i - map.off[j]);
     }
+    const uint32_t sum = Reduce(red_tmp).Sum(bits);
+    if (t == 0) {
+      tile += sum;
+      total += sum;
+      if ((base + NT) % kEmitTile == 0 || base + NT >= n) {
+        tb[base / kEmitTile] = tile;
+        tile = 0;
+      }
+    }
     __syncthreads();
   }
-  unsigned long long total = Reduce(red_tmp).Sum(bits);
   if (t == 0) sg.bits = total;
 }
 
@@ -2452,12 +2466,13 @@ void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const ui
   hipLaunchKernelGGL(mb_header_kernel, dim3(nmbs), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
-                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units) {
+                  const uint32_t *cmd_pos, const Codes *codes, const Unit *units, uint32_t *tile_bits) {
   static const int nt = knob("MIB_SIZES_NT") ? atoi(knob("MIB_SIZES_NT")) : 512;   // (MIB_SIZES_NT overrides)
   if (nt >= 512)
-    hipLaunchKernelGGL(sizes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
+    hipLaunchKernelGGL(sizes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, tile_bits);
   else
-    hipLaunchKernelGGL(sizes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units);
+    hipLaunchKernelGGL(sizes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units,
+                       tile_bits);
 }
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
   hipLaunchKernelGGL(offsets_kernel, dim3(njobs), dim3(64), 0, st, jobs, njobs, mbs, segs, out);

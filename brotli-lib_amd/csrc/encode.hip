@@ -210,7 +210,6 @@ Params make_params(const mib_enc_opts *o) {
 // Pieces cut the parse more often (a piece's first node starts a fresh path; copies stop at
 // the piece end): C4 dp 123 -> 105 ms for +0.03 % bytes, C2 39 -> 8.5 ms.
 // MIB_DP_PIECES=0..3 overrides.
-constexpr int kMaxPieceShift = 6;
 constexpr uint64_t kSmallStream = 1ull << 20;
 // Pieces per segment (2^shift) by the stream itself, so a stream parses the same in any batch:
 // 8 KiB pieces; 2 KiB for one-shot streams below 1 MiB -- a lone small stream gets 512 DP waves
@@ -433,13 +432,13 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   need += cmd_total * (sizeof(RawCmd) + sizeof(Cmd) + 4);
   need += k * (sizeof(Job) + 1024 + 8) + ns1 * sizeof(Seg) + seg_job.size() * (4 + sizeof(SegRef)) + 256;
   need += nm1 * (sizeof(Mb) + sizeof(Codes) + kHdrBytes + kTreeSlots * kTreeBytes + 4 * (kLitSlots * 256 + kMaxBT * 704 + kMaxBT * kDistCtx * 128));
-  need += ns1 * kSubPerSeg * (sizeof(Unit) + kSubHist * 4);
+  need += ns1 * kSubPerSeg * (sizeof(Unit) + kSubHist * 4) + ns1 * kEmitTiles * 4;
   need += out_scratch + 64;
   need += ns1 * part_push_bytes();
   const bool two_pass = prm.quality >= 11 && zopfli_iterations() > 1;   // backward-references-hq.ts:562-605
   need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
   need += std::max<uint64_t>(npieces, 1) * sizeof(Seg);   // parse pieces
-  need += 40 * 256;   // alignment
+  need += 41 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*ws_slot);
   if (!ws) {
     ws = new Workspace();
@@ -473,6 +472,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   uint32_t *hc = ar.take<uint32_t>(nm1 * kMaxBT * 704);
   uint32_t *hd = ar.take<uint32_t>(nm1 * kMaxBT * kDistCtx * 128);
   Unit *units = ar.take<Unit>(ns1 * kSubPerSeg);
+  uint32_t *tile_bits = ar.take<uint32_t>(ns1 * kEmitTiles);
   uint32_t *unit_h = ar.take<uint32_t>(ns1 * kSubPerSeg * kSubHist);
   Codes *codes = ar.take<Codes>(nm1);
   uint8_t *hdr = ar.take<uint8_t>(nm1 * kHdrBytes);
@@ -568,11 +568,11 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_huffman(st, d_jobs, d_mbs, nmbs, hl, hc, hd, codes, trees, hdr);
     tm.stop();
     tm.start("sizes");
-    launch_sizes(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, codes, units);
+    launch_sizes(st, d_jobs, d_segs, d_mbs, nsegs, cmds, cmd_pos, codes, units, tile_bits);
     launch_offsets(st, d_jobs, (int)k, d_mbs, d_segs, oscr);
     tm.stop();
     tm.start("emit");
-    launch_emit(st, d_jobs, d_mbs, nmbs, d_segs, nsegs, cmds, cmd_pos, codes, units, trees, hdr, oscr);
+    launch_emit(st, d_jobs, d_mbs, nmbs, d_segs, nsegs, cmds, cmd_pos, codes, units, tile_bits, trees, hdr, oscr);
     tm.stop();
     tm.start("part_index");
     launch_part_index(st, d_jobs, (int)k, d_mbs, d_segs, nsegs, cmds, units, push, oscr);
