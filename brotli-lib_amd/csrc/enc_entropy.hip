@@ -2261,6 +2261,8 @@ __global__ __launch_bounds__(64) void mb_header_kernel(const Job *jobs, Mb *mbs,
 // The segment's bit size: the sum of item_bits over its commands' items (the same
 // load-balanced expansion as emit_kernel, so literal-heavy segments use every lane), kept per
 // tile of kEmitTile commands too (tile_bits[segment][tile]: emit_kernel's tile offsets).
+// Blocks per segment as emit_kernel's: block (s, y) sizes tiles y, y + gridDim.y, ... and adds
+// its sum into the segment's bits (zero from the host's segment table).
 template <int NT>
 __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Codes *codes, const Unit *units,
@@ -2277,6 +2279,9 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
   Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
+  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
+  const uint32_t ntile = (n + kEmitTile - 1) / kEmitTile;
+  if (blockIdx.y >= ntile) return;
   const int t = threadIdx.x;
   const Mb &mb = mbs[sg.mb];
   const Codes &cd = codes[sg.mb];
@@ -2284,15 +2289,15 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
   __shared__ uint16_t sh_cmap[kLitSlots];
   for (int i = t; i < 512; i += NT) sh_lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   for (int i = t; i < kLitSlots; i += NT) sh_cmap[i] = mb.lit_cmap[i];
+  if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
   __syncthreads();
   const uint8_t *lut = sh_lut;
-  const uint32_t n = sg.ncmd + (sg.extra_ins ? 1 : 0);
-  if (t < kSubPerSeg) sh_u[t] = units[(size_t)blockIdx.x * kSubPerSeg + t];
   uint32_t *tb = tile_bits + (size_t)blockIdx.x * kEmitTiles;
   unsigned long long total = 0;   // (thread 0)
   uint32_t tile = 0;              // (thread 0: the current tile's bits so far)
-  for (uint32_t base = 0; base < n; base += NT) {
-    const uint32_t nb = min((uint32_t)NT, n - base);
+  for (uint32_t tl = blockIdx.y; tl < ntile; tl += gridDim.y)
+  for (uint32_t base = tl * kEmitTile, tend = min(n, (tl + 1) * kEmitTile); base < tend; base += NT) {
+    const uint32_t nb = min((uint32_t)NT, tend - base);
     uint32_t cnt = 0;
     if ((uint32_t)t < nb) {
       sh_c[t] = cmds[sg.cmd_off + base + t];
@@ -2314,14 +2319,14 @@ __global__ __launch_bounds__(NT) void sizes_kernel(const Job *jobs, Seg *segs, c
     if (t == 0) {
       tile += sum;
       total += sum;
-      if ((base + NT) % kEmitTile == 0 || base + NT >= n) {
-        tb[base / kEmitTile] = tile;
+      if (base + NT >= tend) {
+        tb[tl] = tile;
         tile = 0;
       }
     }
     __syncthreads();
   }
-  if (t == 0) sg.bits = total;
+  if (t == 0) atomicAdd(reinterpret_cast<unsigned long long *>(&sg.bits), total);
 }
 
 // ---------------------------------------------------------------- offsets: wave per stream
@@ -2468,11 +2473,13 @@ void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const ui
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Codes *codes, const Unit *units, uint32_t *tile_bits) {
   static const int nt = knob("MIB_SIZES_NT") ? atoi(knob("MIB_SIZES_NT")) : 512;   // (MIB_SIZES_NT overrides)
+  // blocks per segment: enough for ~2,048 blocks, as launch_emit
+  static const int target = knob("MIB_EMIT_BLOCKS") ? std::max(1, atoi(knob("MIB_EMIT_BLOCKS"))) : 2048;
+  const dim3 grid(nsegs, std::min(kEmitTiles, std::max(1, (target + nsegs - 1) / std::max(nsegs, 1))));
   if (nt >= 512)
-    hipLaunchKernelGGL(sizes_kernel<512>, dim3(nsegs), dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, tile_bits);
+    hipLaunchKernelGGL(sizes_kernel<512>, grid, dim3(512), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, tile_bits);
   else
-    hipLaunchKernelGGL(sizes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units,
-                       tile_bits);
+    hipLaunchKernelGGL(sizes_kernel<256>, grid, dim3(256), 0, st, jobs, segs, mbs, cmds, cmd_pos, codes, units, tile_bits);
 }
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out) {
   hipLaunchKernelGGL(offsets_kernel, dim3(njobs), dim3(64), 0, st, jobs, njobs, mbs, segs, out);
