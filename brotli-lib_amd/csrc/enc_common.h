@@ -496,15 +496,17 @@ void launch_sort(hipStream_t st, const Job *jobs, const uint32_t *pos_job, int n
                  uint32_t *tmp_k, uint32_t *tmp_v, uint32_t *skeys, uint32_t *svals);
 void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const RawCmd *raw, Cmd *cmds,
                   uint32_t *cmd_pos, Unit *units, uint32_t *unit_h);
-void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes,
-                  int max_units, int max_short_units);
+// (side: a second stream the caller forks to and joins from; the launcher puts the launch
+// that is independent of the one on st there -- st itself when there is none)
+void launch_split(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, int nmbs, Unit *units,
+                  const uint32_t *unit_h, Codes *codes, int max_units, int max_short_units);
 void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd);
 void launch_dist_ring(hipStream_t st, Job *jobs, int njobs, const Seg *segs, const Cmd *cmds);
 void launch_context_mode(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs);
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd);
-void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
-                    const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr);
+void launch_huffman(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
+                    const uint32_t *hc, const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr);
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Codes *codes, const Unit *units, uint32_t *tile_bits);
 void launch_offsets(hipStream_t st, Job *jobs, int njobs, Mb *mbs, Seg *segs, uint8_t *out);

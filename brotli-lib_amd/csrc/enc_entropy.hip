@@ -2391,8 +2391,8 @@ void launch_codes(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mb
   else
     hipLaunchKernelGGL(codes_kernel<256>, dim3(nsegs), dim3(256), 0, st, jobs, segs, mbs, raw, cmds, cmd_pos, units, unit_h);
 }
-void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *units, const uint32_t *unit_h, Codes *codes,
-                  int max_units, int max_short_units) {
+void launch_split(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, int nmbs, Unit *units,
+                  const uint32_t *unit_h, Codes *codes, int max_units, int max_short_units) {
   const SplitK sk = split_k();
   // a launch per state count: S = 4 for the blocks seeding at most four types, S = kMaxBT for
   // the rest (if any: literals of the metablocks of up to kSplitWideUnits units)
@@ -2412,9 +2412,10 @@ void launch_split(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, Unit *unit
   }();
   (void)attr;
   const bool few = nmbs * 3 <= 256;
+  // (the two launches take disjoint (metablock, category) blocks: the four-type one runs on side)
   if (narrow) {
-    if (few) hipLaunchKernelGGL((split_kernel<1024, 4>), dim3(nmbs * 3), dim3(1024), lds4, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
-    else hipLaunchKernelGGL((split_kernel<256, 4>), dim3(nmbs * 3), dim3(256), lds4, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
+    if (few) hipLaunchKernelGGL((split_kernel<1024, 4>), dim3(nmbs * 3), dim3(1024), lds4, side, jobs, mbs, nmbs, units, unit_h, codes, sk);
+    else hipLaunchKernelGGL((split_kernel<256, 4>), dim3(nmbs * 3), dim3(256), lds4, side, jobs, mbs, nmbs, units, unit_h, codes, sk);
   }
   if (wide_short || wide_long) {
     if (few) hipLaunchKernelGGL((split_kernel<1024, kMaxBT>), dim3(nmbs * 3), dim3(1024), lds8, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
@@ -2457,8 +2458,8 @@ void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t
   hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * (sk.k[0] + sk.k[2])), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, lit_tree_cap(),
                      sk.k[0], sk.k[2]);
 }
-void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl, const uint32_t *hc,
-                    const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
+void launch_huffman(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
+                    const uint32_t *hc, const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
   // one launch for every slot (two launches by alphabet size, the literal one with half the LDS,
   // were measured: C4 6.0 -> 5.5 ms but C3 8.9 -> 10.2 -- the command / distance blocks, the
   // longest, then ran as a tail of their own)
@@ -2468,7 +2469,9 @@ void launch_huffman(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, const ui
   const int nl = std::max(lit_tree_cap(), sk.k[0]), nr = nl + sk.k[1] + sk.k[2] * kDistCtx;
   hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * nr), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, nl, sk.k[1],
                      nr);
-  hipLaunchKernelGGL(mb_header_kernel, dim3(nmbs), dim3(64), 0, st, jobs, mbs, nmbs, hdr, codes);
+  // the header reads the split's and the clustering's results, not the prefix codes (it writes
+  // Mb.hdr_bits and the block-split codes, huffman_kernel Mb.tree_bits and the other codes)
+  hipLaunchKernelGGL(mb_header_kernel, dim3(nmbs), dim3(64), 0, side, jobs, mbs, nmbs, hdr, codes);
 }
 void launch_sizes(hipStream_t st, const Job *jobs, Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Codes *codes, const Unit *units, uint32_t *tile_bits) {
