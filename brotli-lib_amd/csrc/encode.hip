@@ -549,7 +549,15 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     const int depth = (int)env_u32("MIB_DEPTH", (uint32_t)depth_for_quality(prm.quality), 1, 64);   // override: experiments
     // (a batch of many metablocks fills the chip with each launch: there the independent
     // launches ran side by side were slower, C4 encode -1.8 %, r05ap)
+    const DictDev *dd = any_dict ? dict_device(mib_ctx_device_of(ctx)) : nullptr;
+    if (any_dict && !dd) return MIB_E_OUT_OF_MEMORY;   // (before the fork: nothing queued on the side stream yet)
     Fork fk = nmbs * 3 <= 256 ? fork_of(ws, st) : Fork{st, st, nullptr, nullptr};
+    // every exit from here on (a failed launch check included) leaves st ordered after the side
+    // stream's work, so the next call's memsets on st cannot overtake its kernels
+    struct JoinAtExit {
+      Fork &f;
+      ~JoinAtExit() { f.join(); }
+    } join_at_exit{fk};
     // the literal histogram and the context mode read only the input: beside the match search
     // (unforked, they keep their places after the match search: C4 encode -2 % with them first)
     const bool forked = fk.side != st;
@@ -562,8 +570,6 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_sort(st, d_jobs, d_seg_job, (int)k, total, hash_bytes(prm), sort_ws, keys, vals, skeys, svals);
     tm.stop();
     tm.start("find_matches");
-    const DictDev *dd = any_dict ? dict_device(mib_ctx_device_of(ctx)) : nullptr;
-    if (any_dict && !dd) return MIB_E_OUT_OF_MEMORY;
     launch_find_matches(st, d_jobs, d_seg_job, d_seg_ref, skeys, svals, total, depth, (1u << prm.lgwin) - 16, any_hist,
                         any_parts, matches);
     if (dd) launch_dict_matches(st, d_jobs, (int)k, dict_span(), dd->tab, dd->data, matches);

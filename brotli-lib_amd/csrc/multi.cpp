@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <chrono>
 #include <thread>
@@ -31,7 +32,7 @@ extern "C" uint8_t *mib_buf_alloc(size_t n);
 extern "C" void *mib_ctx_stream_of(mib_ctx *c);
 extern "C" uint8_t *mib_ctx_stage(mib_ctx *c, int slot, uint64_t need);
 extern "C" void mib_ctx_trim(mib_ctx *c, uint64_t keep_stage, uint64_t keep_scratch);
-extern "C" void mib_ctx_set_share(mib_ctx *c, int n);
+extern "C" void mib_ctx_release_ring(mib_ctx *c);
 
 namespace {
 
@@ -40,11 +41,13 @@ constexpr int kMaxShards = 64;
 // keeps its buffers; one huge batch does not pin GiBs of host and device memory forever)
 constexpr uint64_t kKeepDevice = 4ull << 30;
 
-int device_count() {   // (counted once: a hipGetDeviceCount costs ~0.4 ms)
-  static const int n = [] {
-    int c = 0;
-    return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
-  }();
+int device_count() {   // (a hipGetDeviceCount costs ~0.4 ms: a positive count is kept, a failure is retried)
+  static std::atomic<int> known{0};
+  int n = known.load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  int c = 0;
+  n = hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+  if (n > 0) known.store(n, std::memory_order_relaxed);
   return n;
 }
 
@@ -75,14 +78,18 @@ Shard *acquire(int s, int dev) {
   return sh;
 }
 // At most kKeepIdle idle shards per index stay pooled (each holds a context with up to
-// kKeepDevice per buffer and kKeepPinned of pinned memory); a burst of concurrent sharded calls
-// destroys its extra shards as they finish instead of keeping them for the process's life.
+// kKeepDevice per buffer and its 64 MiB pinned transfer ring); a burst of concurrent sharded
+// calls destroys its extra shards as they finish instead of keeping them for the process's
+// life.  Only the first shard of each device keeps its ring while pooled: shard indices past
+// the device count (several shards on one device) give it back, so the pool pins at most one
+// ring per device however many shards a call asked for.
 constexpr size_t kKeepIdle = 1;
 void release(int s, Shard *sh) {
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
     if (g_pool[s].size() < kKeepIdle) {
       sh->trim();
+      if (s >= device_count()) mib_ctx_release_ring(sh->ctx);
       g_pool[s].push_back(sh);
       return;
     }
@@ -235,10 +242,6 @@ int run_shards(const mib_span *in, size_t k, int n_gpus, F fn, bool per_device =
   for (int s = 0; s < shards && !rc; s++)
     if (!(sh[s] = acquire(s, s % ndev))) rc = MIB_E_NO_DEVICE;
   if (!rc) {
-    // shards on one device decode at once: the decoder picks its build for all of them (its
-    // one-stream-per-CU build, chosen per call, made four 256-stream shards on one GPU take
-    // turns: 698 vs 361 ms for the one-context call, r05g)
-    for (int s = 0; s < shards; s++) mib_ctx_set_share(sh[s]->ctx, (shards + ndev - 1 - s % ndev) / ndev);
     const std::vector<std::vector<size_t>> parts = assign(in, k, shards);
     std::vector<int> rcs(shards, 0);
     std::vector<std::thread> th;

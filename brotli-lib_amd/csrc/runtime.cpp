@@ -339,9 +339,6 @@ struct mib_ctx {
   uint8_t *ring = nullptr;
   hipEvent_t ring_ev[2] = {nullptr, nullptr};
   bool ring_failed = false;
-  // contexts decoding on this device at once (multi.cpp: shards sharing a GPU): the decoder's
-  // one-stream-per-CU build is chosen only when the streams of ALL of them fit one per CU
-  int dev_share = 1;
   // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
   uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
@@ -691,31 +688,39 @@ static int bufs_from_device(size_t k, mib_buf *const *outs, const uint8_t *const
     hi = std::max(hi, d_src[i] + len[i]);
     sum += len[i];
   }
-  // large results: through the default context's pinned ring, straight into the result
-  // buffers; many small ones: one copy of the span that holds them all, then host copies (a
-  // copy call costs ~10 us)
-  if (sum >= (4u << 20) || (uint64_t)(hi - lo) > 4 * sum + (1u << 20)) {
-    mib_ctx *c = default_ctx();
-    if (!c) return MIB_E_NO_DEVICE;
-    std::vector<mib::HostPiece> ps;
-    for (size_t i = 0; i < k; i++) {
-      outs[i]->data = mib_buf_alloc(len[i]);
-      outs[i]->size = 0;
-      if (!outs[i]->data) return MIB_E_OUT_OF_MEMORY;
-      outs[i]->size = len[i];
-      if (len[i]) ps.push_back(mib::HostPiece{outs[i]->data, d_src[i], len[i]});
-    }
-    return mib::ctx_download(c, c->stream, ps.data(), ps.size());
-  }
-  std::vector<uint8_t> host(hi - lo);
-  if (hipMemcpy(host.data(), lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess) return MIB_E_NO_DEVICE;
   for (size_t i = 0; i < k; i++) {
     outs[i]->data = mib_buf_alloc(len[i]);
     outs[i]->size = 0;
     if (!outs[i]->data) return MIB_E_OUT_OF_MEMORY;
     outs[i]->size = len[i];
-    if (len[i]) memcpy(outs[i]->data, host.data() + (d_src[i] - lo), len[i]);
   }
+  const uint64_t span = (uint64_t)(hi - lo);
+  const bool sparse = span > 4 * sum + (1u << 20);
+  // Large results on average (or scattered ones): through the default context's pinned ring,
+  // straight into the result buffers, one device copy each.  Many small results in a dense
+  // span: the span as ONE device copy (through the ring when large), then host copies out of
+  // it -- a device copy call costs ~10 us, thousands of them would dominate.
+  if (sparse || sum / k >= (256u << 10)) {
+    mib_ctx *c = default_ctx();
+    if (!c) return MIB_E_NO_DEVICE;
+    std::vector<mib::HostPiece> ps;
+    for (size_t i = 0; i < k; i++)
+      if (len[i]) ps.push_back(mib::HostPiece{outs[i]->data, d_src[i], len[i]});
+    return mib::ctx_download(c, c->stream, ps.data(), ps.size());
+  }
+  std::vector<uint8_t> host(span);
+  if (span >= kParCopyMin) {
+    mib_ctx *c = default_ctx();
+    if (!c) return MIB_E_NO_DEVICE;
+    const mib::HostPiece whole{host.data(), lo, span};
+    if (mib::ctx_download(c, c->stream, &whole, 1) != 0) return MIB_E_NO_DEVICE;
+  } else if (hipMemcpy(host.data(), lo, span, hipMemcpyDeviceToHost) != hipSuccess) {
+    return MIB_E_NO_DEVICE;
+  }
+  std::vector<Piece> out;
+  for (size_t i = 0; i < k; i++)
+    if (len[i]) out.push_back(Piece{outs[i]->data, host.data() + (d_src[i] - lo), len[i]});
+  par_copy(out);
   return 0;
 }
 
@@ -907,7 +912,7 @@ static int decode_jobs(mib_ctx *c, std::vector<mib::DecJob> &jobs, hipStream_t s
     hipEventCreate(&e1);
     hipEventRecord(e0, stream);
   }
-  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, waves_per_cu(c->device, (size_t)grid * (size_t)c->dev_share),
+  HIP_OK(mib_decode_launch(c->d_jobs, (int)k, c->d_scratch, per_block, ring_bytes, grid, waves_per_cu(c->device, (size_t)grid),
                            stream));
   if (c->profiling) hipEventRecord(e1, stream);
   HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * k, hipMemcpyDeviceToHost, stream));
@@ -1010,7 +1015,7 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
     hipEventRecord(e0, stream);
   }
   HIP_OK(mib_decode_parts_launch(c->d_jobs, (int)nj, c->d_scratch, per_block, d_ticket, grid,
-                                 waves_per_cu(c->device, (size_t)grid * (size_t)c->dev_share), stream));
+                                 waves_per_cu(c->device, (size_t)grid), stream));
   if (c->profiling) hipEventRecord(e1, stream);
   HIP_OK(hipMemcpyAsync(jobs.data(), c->d_jobs, sizeof(mib::DecJob) * nj, hipMemcpyDeviceToHost, stream));
   HIP_OK(hipStreamSynchronize(stream));
@@ -1265,5 +1270,17 @@ int mib_decode_batch(const mib_span *in, size_t k, mib_buf *out, int *status) {
 }  // extern "C"
 
 extern "C" void mib_force_ballot_rank(int force) { __atomic_store_n(&g_force_ballot, force ? 1 : 0, __ATOMIC_RELAXED); }
-// internal (multi.cpp): how many contexts decode on this context's device at once
-extern "C" void mib_ctx_set_share(mib_ctx *c, int n) { c->dev_share = n > 1 ? n : 1; }
+// internal (multi.cpp): give back the context's pinned transfer ring (allocated again on the
+// next large transfer)
+extern "C" void mib_ctx_release_ring(mib_ctx *c) {
+  if (!c || !c->ring) return;
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  hipHostFree(c->ring);
+  c->ring = nullptr;
+  for (int h = 0; h < 2; h++)
+    if (c->ring_ev[h]) {
+      hipEventDestroy(c->ring_ev[h]);
+      c->ring_ev[h] = nullptr;
+    }
+}
