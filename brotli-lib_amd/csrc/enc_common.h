@@ -17,8 +17,16 @@ namespace enc {
 
 constexpr uint32_t kSegBits = 16;
 constexpr uint32_t kSeg = 1u << kSegBits;     // 64 KiB parse segments
-constexpr int kMaxMatches = 4;                // staircase entries kept per position (the longest ones)
-constexpr int kMatchRec = 4;                  // u32 per position record: 4 matches, 0 = none (16 B)
+// staircase entries kept per position (the longest ones).  4 by measurement (6 and 8
+// change C4 / C3 by < 0.05 % for more record traffic and a slower parse; the reference's own
+// q11 parse, restated by the oracle, gains nothing from more than 4 either); MIB_MAX_MATCHES=6|8
+// builds the wider records for that A/B.
+#ifndef MIB_MAX_MATCHES
+#define MIB_MAX_MATCHES 4
+#endif
+constexpr int kMaxMatches = MIB_MAX_MATCHES;
+static_assert(kMaxMatches == 4 || kMaxMatches == 6 || kMaxMatches == 8, "records of 4, 6 or 8 entries");
+constexpr int kMatchRec = kMaxMatches;        // u32 per position record: the matches, 0 = none (16 B at 4)
 constexpr uint32_t kMatchLenSat = 255;        // a match is (length:8 | distance:24); 255 = "255 or more"
 constexpr int kLongCopy = 200;                // copies longer than this are taken outright (the
                                               // reference's MAX_ZOPFLI_LEN is 325 at q11, 150 at q10,
@@ -96,6 +104,8 @@ struct Job {                // one stream (or streaming chunk) to encode
   uint32_t cdict_tail4;     // its last four bytes (little endian)
   uint32_t font;            // FONT mode (last-distance copies pass, 4-byte keys)
   uint32_t hq;              // quality >= 10 (context mode rule)
+  uint32_t binary;          // set by context_mode_kernel: some metablock's literals are not UTF-8
+                            // text (the parse's distance-cache candidates run there)
 };
 
 // Per 64 KiB of global positions: where its stream's bytes are, so the match finder's gather
@@ -281,6 +291,33 @@ __device__ __forceinline__ uint32_t short_code(uint32_t d, const uint32_t *r) {
   if (a >= -3 && a <= 3 && a != 0) return a < 0 ? (uint32_t)(4 + 2 * (-a - 1)) : (uint32_t)(5 + 2 * (a - 1));
   if (b >= -3 && b <= 3 && b != 0) return b < 0 ? (uint32_t)(10 + 2 * (-b - 1)) : (uint32_t)(11 + 2 * (b - 1));
   return d + 15;
+}
+
+// a position's record as kMaxMatches words (16-byte or 8-byte vector accesses)
+__device__ __forceinline__ void rec_load(const uint32_t *p, uint32_t (&v)[kMaxMatches]) {
+  if constexpr (kMaxMatches % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < kMaxMatches / 4; q++) {
+      const uint4 a = reinterpret_cast<const uint4 *>(p)[q];
+      v[4 * q] = a.x; v[4 * q + 1] = a.y; v[4 * q + 2] = a.z; v[4 * q + 3] = a.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kMaxMatches / 2; q++) {
+      const uint2 a = reinterpret_cast<const uint2 *>(p)[q];
+      v[2 * q] = a.x; v[2 * q + 1] = a.y;
+    }
+  }
+}
+__device__ __forceinline__ void rec_store(uint32_t *p, const uint32_t (&v)[kMaxMatches]) {
+  if constexpr (kMaxMatches % 4 == 0) {
+#pragma unroll
+    for (int q = 0; q < kMaxMatches / 4; q++)
+      reinterpret_cast<uint4 *>(p)[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < kMaxMatches / 2; q++) reinterpret_cast<uint2 *>(p)[q] = make_uint2(v[2 * q], v[2 * q + 1]);
+  }
 }
 
 __device__ __forceinline__ uint32_t pack_match(uint32_t dist, uint32_t len) {
@@ -485,7 +522,10 @@ size_t cost_model_hist_bytes(int njobs);
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,
                        uint32_t *hist, CostModel *model);
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
-               const uint32_t *matches, uint64_t *choice, bool cdict, bool font);
+               const uint32_t *matches, uint64_t *choice, bool cdict, bool font, const uint32_t *words, uint32_t *ring_hist,
+               const Mb *mbs);
+size_t dp_ring_hist_bytes(int nsegs);
+void launch_words(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref, uint32_t total, uint32_t *words);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);
 void launch_derive_segs(hipStream_t st, const Seg *segs, int nsegs, uint32_t sample, Seg *d_sample, Seg *pieces);

@@ -141,6 +141,7 @@ __global__ __launch_bounds__(64) void context_mode_kernel(const Job *jobs, Mb *m
   }
   const int mode = !jb.hq || 4 * valid > 3 * len ? 2 : 3;
   mb.ctx_mode = (uint32_t)(force >= 0 ? force : mode);
+  if (mb.ctx_mode != 2u) atomicOr(const_cast<uint32_t *>(&jb.binary), 1u);
 }
 
 // ---------------------------------------------------------------- codes + unit histograms
@@ -446,7 +447,16 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     return;
   }
   const int nh = kind == 0 ? kLitCtx : kDistCtx;
-  const int cap = kind == 0 ? max(1, lit_cap / nbt) : kDistCtx;
+  // The decoder keeps a metablock's prefix codes in its LDS table area (decode.hip kLdsTab,
+  // 12,224 entries, at least 257 a code) only when they all fit.  The literal cap is sized for
+  // four command and four distance types; each type past four takes room from the literal codes:
+  // a command code (704 symbols, ~400 entries with its second-level tables) two literal codes'
+  // worth, a distance type (up to four codes) four.  (Past the area a stream still decodes, with
+  // every symbol lookup an HBM load: C4 decode 140 -> 299 ms with eight command and distance
+  // types and no such budget, r04af.)
+  const int extra = 2 * max(0, (int)mb.nbt[1] - 4) + 4 * max(0, (int)mb.nbt[2] - 4);
+  const int mb_lit_cap = max((int)mb.nbt[0], lit_cap - extra);
+  const int cap = kind == 0 ? max(1, mb_lit_cap / nbt) : kDistCtx;
   const int A = kind == 0 ? 256 : 16 + (int)jb.ndirect + (48 << jb.npostfix);
   const int stride = kind == 0 ? 256 : 128;
   uint32_t *src = kind == 0 ? hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256
@@ -1627,11 +1637,12 @@ __device__ void split_path(int t, int nu, const uint32_t *ns, const float *ucost
 // with 8 their prefix codes overflow the decoder's LDS table area (§7) and C4 decode goes from
 // 140 to 299 ms for 0.05 % of bytes.  (A/B: MIB_SPLIT_BT = "l,c,d", each 1..kMaxBT.)
 constexpr int kSplitBtLit = 8;
+constexpr float kExtraTypeBits = 400.f;   // a literal code's worth (C4: 24 -> 16 literal codes, +0.1 % bytes, r06d)
 __device__ __forceinline__ int nu_of(const Mb &mb) { return (int)mb.nseg * kSubPerSeg; }
 struct SplitK { int k[3]; };
 SplitK split_k() {
   static const SplitK sk = [] {
-    SplitK k{{kSplitBtLit, 4, 4}};
+    SplitK k{{kSplitBtLit, kMaxBT, kMaxBT}};
     if (const char *e = knob("MIB_SPLIT_BT")) sscanf(e, "%d,%d,%d", &k.k[0], &k.k[1], &k.k[2]);
     for (int c = 0; c < 3; c++) k.k[c] = std::min(kMaxBT, std::max(1, k.k[c]));
     return k;
@@ -1833,6 +1844,76 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
     return sh_keep;
   };
   if (K > 1 && ne >= 2 * K) keep = refine();
+  if constexpr (S > 4) {
+    // Command / distance types past four (the reference allows 256) take room from
+    // the literal codes in the decoder's LDS table area (cluster_kernel's budget: two literal
+    // codes a command type, four a distance type).  So past four types, the two types whose
+    // merge costs the fewest bits merge while that is less than what the extra type displaces
+    // (kExtraTypeBits): homogeneous data (C4's text) keeps four or fewer, a metablock whose
+    // units differ in kind keeps more.
+    if (keep && cat > 0) {
+      __shared__ float pair_d[kMaxBT * (kMaxBT - 1) / 2];
+      __shared__ int sh_merge;
+      const float penalty = cat == 1 ? kExtraTypeBits * 2.f : kExtraTypeBits * 4.f;
+      for (;;) {
+        int used = 0;
+        for (int q = 0; q < S; q++) used += tot[q] ? 1 : 0;
+        if (used <= 4) break;
+        // thread per type pair: the bits the merge adds (entropy, 3.5 bits a used symbol, one
+        // code header of 40 bits fewer)
+        if (t < S * (S - 1) / 2) {
+          int a = 0, r = t;
+          while (r >= S - 1 - a) {
+            r -= S - 1 - a;
+            a++;
+          }
+          const int b = a + 1 + r;
+          float d = 1e30f;
+          if (tot[a] && tot[b]) {
+            const float la = __log2f((float)tot[a]), lb = __log2f((float)tot[b]), lab = __log2f((float)(tot[a] + tot[b]));
+            float e = -40.f;
+            for (int x = 0; x < A; x++) {
+              const uint32_t ca = th[a][x], cb = th[b][x];
+              if (!(ca | cb)) continue;
+              const float cab = (float)(ca + cb);
+              e += cab * (lab - __log2f(cab)) + 3.5f;
+              if (ca) e -= (float)ca * (la - __log2f((float)ca)) + 3.5f;
+              if (cb) e -= (float)cb * (lb - __log2f((float)cb)) + 3.5f;
+            }
+            d = e;
+          }
+          pair_d[t] = d;
+        }
+        __syncthreads();
+        if (t == 0) {
+          int bi = 0;
+          for (int k2 = 1; k2 < S * (S - 1) / 2; k2++)
+            if (pair_d[k2] < pair_d[bi]) bi = k2;
+          sh_merge = pair_d[bi] < penalty ? bi : -1;
+        }
+        __syncthreads();
+        if (sh_merge < 0) break;
+        int a = 0, r = sh_merge;
+        while (r >= S - 1 - a) {
+          r -= S - 1 - a;
+          a++;
+        }
+        const int b = a + 1 + r;
+        for (int i = t; i < nu; i += kSplitT)
+          if (asg[i] == b) asg[i] = (uint8_t)a;
+        for (int x = t; x < A; x += kSplitT) {
+          th[a][x] += th[b][x];
+          th[b][x] = 0;
+        }
+        __syncthreads();
+        if (t == 0) {
+          tot[a] += tot[b];
+          tot[b] = 0;
+        }
+        __syncthreads();
+      }
+    }
+  }
 #ifdef MIB_PROF
   const uint64_t tail0 = __builtin_amdgcn_s_memtime();
 #endif

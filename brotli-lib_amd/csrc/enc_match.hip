@@ -132,7 +132,7 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
     const uint32_t pA = (kHist || kParts) ? jb.abs_base + p : 0u, pbits = kParts ? jb.part_bits : 16u,
                    plag = kParts ? jb.part_lag : 0u;
     uint32_t best = 3;
-    uint32_t local[kMaxMatches] = {0u, 0u, 0u, 0u};
+    uint32_t local[kMaxMatches] = {};
     if constexpr (!kHist) {
       const uint64_t mine0 = spre[0][me];
       const int dmax = min(depth, kBack), nwalk = min(dmax, nrun);
@@ -308,10 +308,11 @@ __global__ __launch_bounds__(kTile) void find_matches_kernel(const Job *jobs, co
 #undef TAKE
     }
     // a match word is never 0 (length >= 4): the unused tail entries mark the count
-    *reinterpret_cast<uint4 *>(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec) = make_uint4(local[0], local[1], local[2], local[3]);
+    rec_store(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec, local);
     return;
   }
-  *reinterpret_cast<uint4 *>(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec) = make_uint4(0u, 0u, 0u, 0u);   // no candidates
+  const uint32_t none[kMaxMatches] = {};
+  rec_store(matches + (uint64_t)(sorted_store ? r : g) * kMatchRec, none);   // no candidates
 }
 
 // ---------------------------------------------------------------- near matches (short scan)
@@ -422,8 +423,8 @@ __global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, c
     uint32_t *rec = matches + (uint64_t)g * kMatchRec;
     // (thread kStep, and a position past the block: the m2 of the position before it only)
     const bool emit = here && m2 && t < kStep && g < gb + kNearSpan;
-    uint4 r = make_uint4(0u, 0u, 0u, 0u);
-    if (emit) r = *reinterpret_cast<const uint4 *>(rec);
+    uint32_t old[kMaxMatches] = {};
+    if (emit) rec_load(rec, old);
     __syncthreads();
     if (!emit) continue;
     // a 3-byte copy from d = the pairs at p and at p + 1 both match d back
@@ -462,9 +463,8 @@ __global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, c
       }
     }
     if (!f0) continue;
-    if (r.x && (match_dist(r.x) == kCDictMark || (jb.dict && is_dict(match_dist(r.x))))) continue;   // a dictionary copy: the only entry
+    if (old[0] && (match_dist(old[0]) == kCDictMark || (jb.dict && is_dict(match_dist(old[0]))))) continue;   // a dictionary copy: the only entry
     // the near entries, then the tree's longer ones; a full record keeps its longest
-    const uint32_t old[kMaxMatches] = {r.x, r.y, r.z, r.w};
     uint32_t w[2 + kMaxMatches];
     int m = 0;
     w[m++] = f0;
@@ -473,11 +473,11 @@ __global__ __launch_bounds__(kNearT) void near_matches_kernel(const Job *jobs, c
     for (int q = 0; q < kMaxMatches; q++)
       if (old[q] && match_length(old[q]) > best) w[m++] = old[q];
     const int sk = m > kMaxMatches ? m - kMaxMatches : 0;
-    uint32_t o4[kMaxMatches] = {0u, 0u, 0u, 0u};
+    uint32_t o4[kMaxMatches] = {};
 #pragma unroll
     for (int q = 0; q < kMaxMatches; q++)
       if (q + sk < m) o4[q] = w[q + sk];
-    *reinterpret_cast<uint4 *>(rec) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    rec_store(rec, o4);
   }
 }
 

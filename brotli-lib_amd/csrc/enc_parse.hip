@@ -116,19 +116,27 @@ struct Staged {   // one position's parse inputs as loaded
   uint32_t m[kMaxMatches];
   uint32_t nm;
   uint32_t lit;
+  uint32_t w0, w1;   // (KC) the position's first 8 bytes: words[g], words[g + 4]
 };
-__device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches, const uint8_t *data, uint32_t g, uint32_t p) {
+template <bool KC>
+__device__ __forceinline__ void load_staged(Staged &st, const uint32_t *matches, const uint8_t *data, const uint32_t *words,
+                                            uint32_t g, uint32_t p) {
   st.lit = data[p];
-  const uint4 a = *reinterpret_cast<const uint4 *>(matches + (uint64_t)g * kMatchRec);   // 0 = no entry
-  st.m[0] = a.x; st.m[1] = a.y; st.m[2] = a.z; st.m[3] = a.w;
-  st.nm = (a.x != 0u) + (a.y != 0u) + (a.z != 0u) + (a.w != 0u);
+  rec_load(matches + (uint64_t)g * kMatchRec, st.m);   // 0 = no entry
+  st.nm = 0;
+#pragma unroll
+  for (int q = 0; q < kMaxMatches; q++) st.nm += st.m[q] != 0u;
+  if (KC) {
+    st.w0 = words[g];
+    st.w1 = words[g + 4];
+  }
 }
 struct alignas(16) StageEnt {   // one position's parse inputs in LDS (48 B: two b128 reads and a b64)
   uint32_t m[kMaxMatches];   // (clipped length << 24) | distance, 0 = none
   uint32_t mc[kMaxMatches];  // distance | distance-cost code << 24 (quarter bits)
   uint32_t info;             // nm | maxlen << 8 | shortest usable length << 16
   float lc;                  // literal cost
-  uint32_t pad[2];
+  uint32_t w[2];             // (KC) the position's first 8 bytes, for its distance-cache candidates
 };
 __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (distance << 32) | length, 0 = literal
   const uint32_t cl = (m >> 16) ? 0u : m & 0xFFFF;   // (a literal edge: insert length << 16 | its codes)
@@ -137,22 +145,55 @@ __device__ __forceinline__ uint64_t choice_of(uint32_t d, uint32_t m) {   // (di
 __device__ __forceinline__ uint32_t bperm(uint32_t lane_src, uint32_t v) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lane_src << 2), (int)v);
 }
+// quad permutes (DPP, no LDS): the distance ring lives in the lanes of each quad, entry q in
+// lane q of the quad
+__device__ __forceinline__ uint32_t quad_entry0(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false); }
+__device__ __forceinline__ uint32_t quad_entry1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x55, 0xF, 0xF, false); }
+__device__ __forceinline__ uint32_t quad_shift1(uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x90, 0xF, 0xF, false); }
+
+// ---------------------------------------------------------------- distance-cache candidates
+// (KC; SURVEY a6, backward-references-hq.ts:309-345, computeDistanceCache :213-234).  Every
+// node's path has a decoder distance ring (the last four distances its copies pushed, RFC 7932
+// section 4); short code j (1..15) names ring entry kIdx[j] plus kOff[j].  The pending nodes
+// cannot carry four distances each in registers, so the ring is kept per POSITION of the path
+// already decided: when node x is final (it has become the current node), its ring follows
+// from its edge -- a literal keeps node x-1's ring, a copy pushes its distance on its
+// predecessor's ring (unless it repeats entry 0; a dictionary word pushes nothing) -- and is
+// stored in a 256-position history per lane group (global memory, L1/L2 resident); a copy
+// node's predecessor is at most kLongCopy back.  Pipelined so that no step waits on memory:
+//   step of node i:  fetch node i, load its predecessor's ring from the history (copy edge);
+//                    ring of node i-1 from the load issued one step ago, stored;
+//                    node i-1's 15 candidate distances (a lane each), their source words
+//                    loaded (words[]: each position's 4 bytes, one aligned load per word);
+//                    node i-2's candidates (loaded one step ago) measured over 8 bytes and
+//                    relaxed out of node i-2 for lengths 4..R (the reference's minimum: >= 4),
+//                    priced with the short code's distance symbol.
+// Code 0 (entry 0, no offset) is KR's last-distance copy when that is built, else lane 0 here.
+// The ring at a segment / piece start is unknown: entries 0 offer nothing until the path's
+// own copies fill them.  codes_kernel assigns the real short codes afterwards from the decoder's
+// exact ring (ring_scan_kernel), so a candidate the parse priced is coded as priced except near
+// a piece start.
+constexpr uint32_t kHistPos = 256;      // ring history per lane group (> kLongCopy)
+static_assert(kHistPos > (uint32_t)kLongCopy, "a copy's predecessor must still be in the ring history");
 
 // KM: the second iteration (prices from the stream's CostModel; a separate build, so
 // profiles tell the two passes apart).  KD: some stream has a custom dictionary (records with
 // kCDictMark; a separate build, so the common case pays nothing for it).  KR: the parse relaxes
 // last-distance copies (rp_d below; FONT mode: C3 -1 % bytes, text -0.1 %, a separate build so
 // text pays nothing for it)
-template <int KS, bool KM, bool KD, bool KR>
-__global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
+template <int KS, bool KM, bool KD, bool KR, bool KC>
+__global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS == 2) ? 3 : kDpWavesPerSimd) void dp_kernel(const Job *jobs, const Seg *segs, int nsegs,
                                                            const uint32_t *lit_histo, const CostModel *model,
                                                            const uint32_t *matches,
-                                                           uint64_t *choice /* per position+1 */, float cmd_pen, int use_rep) {
+                                                           uint64_t *choice /* per position+1 */, float cmd_pen, int use_rep,
+                                                           const uint32_t *pwords, uint32_t *ring_hist, const Mb *mbs,
+                                                           int kc_split) {
   constexpr int kS = KS;                // segments per wave
   constexpr int kL = 64 / kS;           // lanes per segment
   constexpr int kC = (kL - 1 + kLongCopy) / kL + 1;   // chunks: batch offset (< kL) + longest relaxed length
   static_assert(kL - 1 + kLongCopy < kL * kC, "every relaxed length must land in a chunk");
   static_assert(kRepLen <= kL, "a last-distance copy is measured by one lane per byte");
+  static_assert(!KC || kL >= 16, "a lane per distance-cache candidate");
   constexpr uint64_t kLaneMask = kL == 64 ? ~0ull : ((1ull << kL) - 1);
   __shared__ uint32_t ptab_all[kDpWaves * kS][24 * kPtabW];   // per segment: (insert code, copy code) -> fp16 (explicit distance) | fp16 (short code 0) << 16
   __shared__ uint8_t cctab[kLenTab];                       // length -> copy code
@@ -200,6 +241,10 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     words = jb.dict != 0;
     cdl = jb.cdict ? jb.cdict_len : 0u;
   }
+  // kc_split: the candidates' build takes the segments whose metablock's literals are not UTF-8
+  // text (context_mode_kernel), the other build the rest (text: the candidates changed C4 by
+  // +0.01 % bytes, r06b)
+  if (kc_split && a < b && (mbs[segs[sgi].mb].ctx_mode == 2u) == KC) a = b;
   if (__ballot(a < b) == 0) return;
   // prices: iteration 0 from zopfli-cost-model.ts's initial model, iteration 1 from the
   // stream's CostModel (per segment tables: a wave's segments may be different streams)
@@ -244,7 +289,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
   if (hl == 0) wc[0] = 0.f;   // node a
   Staged pf;
   uint32_t pf_at = a;
-  if (a + hl < b) load_staged(pf, matches, data, gbase + a + hl, a + hl);
+  if (a + hl < b) load_staged<KC>(pf, matches, data, pwords, gbase + a + hl, a + hl);
   uint32_t chd = 0, chm = 0;   // choices of the batch
   // the pending last-distance candidate (a6): node j reached by a literal, with last distance
   // rp_d, loads the bytes at j + hl and j - rp_d + hl in its step; the step of node j + 1 (the
@@ -252,6 +297,30 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
   // of j, priced with short code 0 (rp_base / rp_ic: node j's cost + insert extra, insert code)
   uint32_t rp_d = 0, rp_ic = 0, rp_cb = 0, rp_sb = 1;
   float rp_base = 0.f;
+  // distance-cache candidates (KC, see above): this lane's short code (lanes 0..15 of the group);
+  // the ring entry q = lane % 4 of each quad.  State packed to keep the build's registers down.
+  const uint32_t cj = hl & 15u, rq = hl & 3u;
+  const bool clane = KC && hl < 16u && (!KR || cj != 0u);
+  const float ccost = KC ? dist_price(cj, cm) : 0.f;   // its distance symbol (short codes carry no extra bits)
+  const uint32_t hoff = (uint32_t)sgi * (kHistPos * 4);   // this lane group's ring history: 256 positions x 4 distances
+  // kf: bits 0-1 node i-1's edge (0 none, 1 literal, 2 copy); bit 2 the next node ends a long
+  // copy (its ring is rg); bit 3 node i-2's candidates are in flight; bits 8-15 node i-1's insert
+  // code, bits 16-23 node i-2's
+  uint32_t kf = 0;
+  uint32_t kp_ld = 0, kp_h = 0;   // node i-1's distance, its predecessor's ring entry rq (copy edge)
+  float kp_base = 0.f;            // node i-1's cost + insert extra
+  uint32_t rg = 0;                // ring entry rq of node i-2 (after the ring step: of node i-1)
+  // node i-2's candidates: distance (0: none), source words, own words, cap | full length << 8
+  uint32_t cq_d = 0, cq_w0 = 0, cq_w1 = 0, cq_c0 = 0, cq_c1 = 0, cq_lim = 0;
+  float cq_base = 0.f;
+  auto words_on_ring = [&](uint32_t dd) { return words && is_dict(dd); };
+  auto ring_step = [&](uint32_t kind, uint32_t dd, uint32_t h, uint32_t prev) -> uint32_t {
+    const uint32_t v = kind == 2u ? h : prev;
+    const uint32_t v0 = quad_entry0(v), vm = quad_shift1(v);
+    const bool word = words_on_ring(dd);
+    const bool push = kind == 2u && dd != v0 && !word;
+    return push ? (rq == 0u ? dd : vm) : (kind == 2u && word && rq == 0u) ? dd : v;
+  };
   uint32_t i = a, i0 = a;
   bool done = a >= b;
 #ifdef MIB_PROF
@@ -263,13 +332,14 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     Staged cur;
     cur.nm = 0;
     cur.lit = 0;
+    cur.w0 = cur.w1 = 0;
     if (pf_at == i0) {
       cur = pf;
     } else if (i0 + hl < b) {   // the parse jumped past the prefetched batch
-      load_staged(cur, matches, data, gbase + i0 + hl, i0 + hl);
+      load_staged<KC>(cur, matches, data, pwords, gbase + i0 + hl, i0 + hl);
     }
     const uint32_t nx = i0 + kL;
-    if (nx + hl < b) load_staged(pf, matches, data, gbase + nx + hl, nx + hl);
+    if (nx + hl < b) load_staged<KC>(pf, matches, data, pwords, gbase + nx + hl, nx + hl);
     pf_at = nx;
     const uint32_t p = i0 + hl;
     const uint32_t nm = p < b ? cur.nm : 0u;
@@ -302,9 +372,9 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
       }
     }
     e.info = (maxlen ? nm : 0u) | (maxlen << 8) | ((word ? maxlen : 2u) << 16);   // | the shortest usable length
-    e.pad[0] = e.pad[1] = 0;
+    e.w[0] = KC ? cur.w0 : 0u;
+    e.w[1] = KC ? cur.w1 : 0u;
     stg[lane + (lane >> kPadSh)] = e;
-    DPCOUNT(6, 1);
   };
   if (!done) stage();
   wave_sync();
@@ -395,6 +465,16 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
           const uint32_t p = i0 + hl;
           if (p <= i && p != a) choice[gbase + p] = choice_of(chd, chm);
         }
+        if (KC) {
+          // the ring after the copy (waits for its loads: long copies are rare): node i-1's ring,
+          // node i's (its predecessor's, loaded now), fd pushed on it
+          const uint32_t r1 = (kf & 3u) ? ring_step(kf & 3u, kp_ld, kp_h, rg) : rg;
+          const bool ccopy = !(kf & 4u) && mm >= 2u && (mm >> 16) == 0u;
+          const uint32_t hv = ccopy ? ring_hist[hoff + ((i - mm) & (kHistPos - 1)) * 4 + rq] : 0u;
+          const uint32_t ri = ring_step(ccopy ? 2u : 1u, ld, hv, r1);
+          rg = ring_step(2u, fd, ri, ri);
+          kf = 4u;   // (no node i-1, nothing in flight)
+        }
         i += fl;
         i0 = i;
         rp_d = 0;
@@ -406,7 +486,6 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
           wm[0] = fl;
         }
         stage();
-        DPCOUNT(7, 1);
       }
       wave_sync();
       DPMARK(2);
@@ -414,11 +493,20 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
     }
     // the match staircase of i: lengths (clipped) and the packed (distance | cost code) words
     // (both read unconditionally: a masked load would be a branch and a wait per entry)
-    const uint4 em = *reinterpret_cast<const uint4 *>(e.m), emc = *reinterpret_cast<const uint4 *>(e.mc);
     const uint32_t actm = 0u - (uint32_t)act;
-    const uint32_t mL[kMaxMatches] = {match_length(em.x) & actm, match_length(em.y) & actm, match_length(em.z) & actm,
-                                      match_length(em.w) & actm};   // 0 past nm
-    const uint32_t vpk[kMaxMatches] = {emc.x, emc.y, emc.z, emc.w};
+    uint32_t mL[kMaxMatches], vpk[kMaxMatches];
+    if constexpr (kMaxMatches == 4) {
+      const uint4 em = *reinterpret_cast<const uint4 *>(e.m), emc = *reinterpret_cast<const uint4 *>(e.mc);
+      mL[0] = match_length(em.x) & actm; mL[1] = match_length(em.y) & actm;   // 0 past nm
+      mL[2] = match_length(em.z) & actm; mL[3] = match_length(em.w) & actm;
+      vpk[0] = emc.x; vpk[1] = emc.y; vpk[2] = emc.z; vpk[3] = emc.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < kMaxMatches; q++) {
+        mL[q] = match_length(e.m[q]) & actm;
+        vpk[q] = e.mc[q];
+      }
+    }
     // the last-distance copy out of node i - 1 (see rp_d): its length R from the loaded bytes
     uint32_t R = 0;
     if (KR) {
@@ -436,7 +524,6 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
 #pragma unroll
     for (int c = 0; c < kC; c++) {
       if (c > 0 && __ballot(act && (uint32_t)(kL * c) <= off + maxrel) == 0) break;
-      DPCOUNT(5, 1);
       const uint32_t l = (uint32_t)(kL * c) + hl - off;   // wraps (huge) for consumed nodes
       float cand = kInf;
       uint32_t nd = ld, nmeta = (ins1 << 16) | nx;
@@ -481,6 +568,106 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : kDpWavesP
         }
       }
     }
+    DPMARK(3);
+    if (KC) {
+      // (1) node i-2's candidates (loaded one step ago): the match length over 8 bytes (all 8:
+      // the full length where node i-2's staircase holds the same distance -- a cheap 8-byte
+      // piece of a longer copy would split it in two commands), and the copies of lengths 4..R
+      // relaxed out of node i-2 (lane j of chunk c: length kL c + j + 2 - off)
+      const uint32_t x0 = cq_w0 ^ cq_c0, x1 = cq_w1 ^ cq_c1;
+      uint32_t R = x0 ? 0u : x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : max(8u, cq_lim >> 8);
+      R = min(R, cq_lim & 0xFFu);
+      const bool pass = act && (kf & 8u) && cq_d != 0u && R >= 4u;
+      uint64_t pm = __ballot(pass);
+      if (pm) {
+        // the lengths' copy prices out of node i-2 (its insert code's row), both halves, for the
+        // chunks the longest passing candidate reaches: read once, before the candidates' loop
+        const uint32_t *crow = ptab + ((kf >> 16) & 0xFFu) * kPtabW;
+        // (the wave's longest reach, bit by bit from ballots: no cross-lane latency chain)
+        uint32_t rmax = 0;
+#pragma unroll
+        for (int bit = 7; bit >= 0; bit--) {
+          const uint32_t trial = rmax | (1u << bit);
+          if (__ballot(pass && R >= trial)) rmax = trial;
+        }
+        uint32_t ctv[kC];
+#pragma unroll
+        for (int c = 0; c < kC; c++) {
+          const uint32_t lr = (uint32_t)(kL * c) + hl + 2u - off;   // wraps (huge) below node i-2
+          ctv[c] = (lr >= 4u && lr <= rmax) ? crow[cctab[lr]] : 0u;
+        }
+        // every passing candidate in turn (the lowest short code first), each relaxing lengths
+        // 4..R at its own price (the farthest-reaching one alone lost the cheaper short codes of
+        // the shorter lengths: records +1.0 % bytes, r06e)
+        do {
+          const uint32_t mine = (uint32_t)((pm >> hbase) & 0xFFFFull);
+          const uint32_t k = mine ? (uint32_t)__builtin_ctz(mine) : 0u;
+          const uint32_t src = hbase + k;
+          const uint32_t Rk = mine ? bperm(src, R) : 0u, dk = bperm(src, cq_d);
+          const float ck = __uint_as_float(bperm(src, __float_as_uint(ccost)));   // short code k's distance symbol
+#pragma unroll
+          for (int c = 0; c < kC; c++) {
+            if (c > 1 && __ballot((uint32_t)(kL * c) + 2u <= off + Rk) == 0) break;
+            const uint32_t lr = (uint32_t)(kL * c) + hl + 2u - off;
+            if (lr >= 4u && lr <= Rk) {
+              const float cr = cq_base + (k ? (float)__builtin_bit_cast(_Float16, (uint16_t)(ctv[c] & 0xFFFF)) + ck
+                                            : (float)__builtin_bit_cast(_Float16, (uint16_t)(ctv[c] >> 16)));
+              if (cr < wc[c]) {
+                wc[c] = cr;
+                wd[c] = dk;
+                wm[c] = lr;
+              }
+            }
+          }
+          pm &= ~__ballot(mine != 0u && hl == k);
+        } while (pm);
+      }
+      DPMARK(6);   // (KC: measuring and relaxing node i-2's candidates)
+      // (2) the ring of node i-1, from its edge and the predecessor ring loaded one step ago; kept
+      // in the history
+      const uint32_t pk = kf & 3u;
+      if (pk) {
+        rg = ring_step(pk, kp_ld, kp_h, rg);
+        ring_hist[hoff + ((i - 1u) & (kHistPos - 1)) * 4 + rq] = rg;
+      }
+      // (3) node i-1's candidates: a lane per short code, its distance from the ring, its first 8
+      // source bytes and node i-1's own loaded now (measured next step)
+      {
+        const uint32_t e0 = quad_entry0(rg), e1 = quad_entry1(rg);
+        const uint32_t cb = cj < 4u ? rg : cj < 10u ? e0 : e1;
+        const int coff = cj < 4u ? 0 : (int)(((cj - 4u) % 6u) / 2u + 1u) * (((cj - 4u) & 1u) ? 1 : -1);
+        const uint32_t cd = cb + (uint32_t)coff;
+        const uint32_t x = i - 1u;
+        const bool cv = clane && pk != 0u && cb != 0u && !words_on_ring(cb) && cd - 1u < min(x, maxback);
+        cq_d = cv ? cd : 0u;
+        if (cv) {
+          cq_w0 = pwords[gbase + x - cd];
+          cq_w1 = pwords[gbase + x - cd + 4u];
+          cq_c0 = pwords[gbase + x];
+          cq_c1 = pwords[gbase + x + 4u];
+        }
+        // node i-1's staircase (its stage entry, while this batch holds it): the full length of
+        // a staircase match at the candidate's distance
+        uint32_t full = 0;
+        if (off != 0u) {
+          const uint32_t ps = src - 1u;
+          const StageEnt &pe = stg[ps + (ps >> kPadSh)];
+#pragma unroll
+          for (int q = 0; q < kMaxMatches; q++) full = match_dist(pe.m[q]) == cd ? max(full, match_length(pe.m[q])) : full;
+        }
+        uint32_t cap = b - x;
+        if (parts && cv) cap = min(cap, part_cap(abs0 + x, cd, pbits, plag));
+        cq_lim = min(cap, (uint32_t)kLongCopy) | (min(full, (uint32_t)kLongCopy) << 8);
+        cq_base = kp_base;
+      }
+      // (4) node i for the next step: its edge, its predecessor's ring (copy edge)
+      const bool ccopy = !(kf & 4u) && mm >= 2u && (mm >> 16) == 0u;
+      if (act && ccopy) kp_h = ring_hist[hoff + ((i - mm) & (kHistPos - 1)) * 4 + rq];
+      kf = (act ? (ccopy ? 2u : 1u) : 0u) | (pk ? 8u : 0u) | ((uint32_t)ic << 8) | (((kf >> 8) & 0xFFu) << 16);
+      kp_ld = ld;
+      kp_base = base;
+    }
+    DPMARK(5);   // (KC: the candidates' cycles)
     // node i's own last-distance candidate: loads now, measured in the next step (a window
     // distance only: not a dictionary word's or a custom-dictionary copy's)
     if (KR) {
@@ -722,9 +909,27 @@ void launch_merge_pieces(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, 
 // A stream's model depends on its own bytes only, so a batch encodes each stream exactly as
 // a call of its own does.
 constexpr int kHistLen = 256 + 704 + 128;   // literals | commands | distances
+// The distance code of a copy at distance d (not a repeat of the last) under a ring r that may
+// have unknown (0) entries -- a segment's parse starts without the ring before it: a short code
+// 1-15 (as short_code) when d is a known entry or within 3 of entry 0 or 1, else 0.
+__device__ __forceinline__ uint32_t known_short_code(uint32_t d, const uint32_t *r) {
+  if (r[1] && d == r[1]) return 1;
+  if (r[2] && d == r[2]) return 2;
+  if (r[3] && d == r[3]) return 3;
+  const int64_t a = (int64_t)d - (int64_t)r[0], b = (int64_t)d - (int64_t)r[1];
+  if (r[0] && a >= -3 && a <= 3 && a != 0) return a < 0 ? (uint32_t)(4 + 2 * (-a - 1)) : (uint32_t)(5 + 2 * (a - 1));
+  if (r[1] && b >= -3 && b <= 3 && b != 0) return b < 0 ? (uint32_t)(10 + 2 * (-b - 1)) : (uint32_t)(11 + 2 * (b - 1));
+  return 0;
+}
 __global__ __launch_bounds__(256) void cmd_stats_kernel(const Job *jobs, const Seg *segs, const RawCmd *raw,
                                                         uint32_t *hist /* kHistLen per job */) {
   __shared__ uint32_t hs[kHistLen], scan[256];
+  // the chunk's distances, then their distance codes: the first parse's copies take short codes
+  // 1-15 from the distance cache (dp_kernel KC), so the model must see them (setFromCommands
+  // counts each command's distance prefix code, zopfli-cost-model.ts:96-110); one thread walks
+  // the segment's ring (a sampled first parse: ~200 commands a segment)
+  __shared__ uint32_t cdist[256];
+  uint32_t ring[4] = {0, 0, 0, 0}, prev_d = 0;
   uint32_t *hl = hs, *hc = hs + 256, *hd = hs + 256 + 704;
   const uint32_t t = threadIdx.x;
   for (uint32_t i = t; i < kHistLen; i += 256) hs[i] = 0;
@@ -752,17 +957,35 @@ __global__ __launch_bounds__(256) void cmd_stats_kernel(const Job *jobs, const S
       __syncthreads();
     }
     const uint32_t pos = base + scan[t] - span, tot = scan[255];
+    cdist[t] = c.dist;
+    __syncthreads();
+    if (t == 0) {
+      const uint32_t m = min(256u, n - q0);
+      for (uint32_t j = 0; j < m; j++) {
+        const uint32_t d = cdist[j];
+        const bool word = is_word(jb, d), last = !word && d == prev_d;
+        uint32_t code = 0;
+        if (!last) {
+          const uint32_t sc = word ? 0u : known_short_code(d, ring);
+          uint32_t extra;
+          code = sc ? sc : dist_prefix((word ? d & ~kDictFlag : d) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra) & 0x3FFu;
+          if (!word) {   // every distance code but 0 pushes (a dictionary word: none)
+            ring[3] = ring[2];
+            ring[2] = ring[1];
+            ring[1] = ring[0];
+            ring[0] = d;
+          }
+        }
+        prev_d = d;
+        cdist[j] = code;
+      }
+    }
     __syncthreads();
     if (q < n) {
       const bool last = !is_word(jb, c.dist) && c.dist == prevd;
       const int cmd = combine_codes(ins_code(c.ins), copy_code(c.len), last);
       atomicAdd(&hc[cmd], 1u);
-      if (cmd >= 128) {
-        uint32_t extra;
-        const uint32_t code =
-            last ? 0u : (dist_prefix((is_word(jb, c.dist) ? c.dist & ~kDictFlag : c.dist) + 15, (int)jb.ndirect, (int)jb.npostfix, &extra) & 0x3FFu);
-        atomicAdd(&hd[min(code, 127u)], 1u);
-      }
+      if (cmd >= 128) atomicAdd(&hd[min(cdist[t], 127u)], 1u);
       for (uint32_t j = 0; j < c.ins; j++) atomicAdd(&hl[jb.data[pos + j]], 1u);
     }
     base += tot;
@@ -976,9 +1199,10 @@ static int dp_ks(int nsegs, bool font) {
   if (v == 1 || v == 2 || v == 4) return v;
   return !font && nsegs >= kKs4Segs ? 4 : nsegs < 2048 ? 1 : 2;
 }
-template <bool KD>
+template <bool KD, bool KC>
 static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,
-                        const CostModel *model, const uint32_t *matches, uint64_t *choice, bool font) {
+                        const CostModel *model, const uint32_t *matches, uint64_t *choice, bool font,
+                        const uint32_t *words, uint32_t *ring_hist, const Mb *mbs, int kc_split) {
   const int ks = dp_ks(nsegs, font), spw = kDpWaves * ks;
   const dim3 g((nsegs + spw - 1) / spw), b(64 * kDpWaves);
   // MIB_CMD_PENALTY (bits, experiment): added to every copy's price, fewer and longer commands
@@ -986,7 +1210,8 @@ static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int ns
   // last-distance candidates in the parse: FONT mode (MIB_DP_REP, experiments: 0 off, 2 every mode)
   static const int rep_knob = knob("MIB_DP_REP") ? atoi(knob("MIB_DP_REP")) : 1;
   const bool rep = rep_knob == 2 || (rep_knob == 1 && font);
-#define MIB_DP(K, M, R) hipLaunchKernelGGL((dp_kernel<K, M, KD, R>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen, 1)
+#define MIB_DP(K, M, R) \
+  hipLaunchKernelGGL((dp_kernel<K, M, KD, R, KC>), g, b, 0, st, jobs, segs, nsegs, lit_h, model, matches, choice, cmd_pen, 1, words, ring_hist, mbs, kc_split)
 #define MIB_DP_KS(K)                \
   do {                              \
     if (model && rep) MIB_DP(K, true, true);   \
@@ -1000,10 +1225,37 @@ static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int ns
 #undef MIB_DP_KS
 #undef MIB_DP
 }
+// (words, ring_hist: the distance-cache candidates' inputs, dp_ring_hist_bytes; null: none).
+// With them, two launches: the candidates' build for the segments whose metablock's literals
+// are not UTF-8 text, the plain build for the rest (mbs[].ctx_mode must be set).
 void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h, const CostModel *model,
-               const uint32_t *matches, uint64_t *choice, bool cdict, bool font) {
-  if (cdict) launch_dp_t<true>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font);
-  else launch_dp_t<false>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font);
+               const uint32_t *matches, uint64_t *choice, bool cdict, bool font, const uint32_t *words, uint32_t *ring_hist,
+               const Mb *mbs) {
+  const bool kc = words && ring_hist && mbs;
+  if (cdict) {
+    if (kc) launch_dp_t<true, true>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font, words, ring_hist, mbs, 1);
+    launch_dp_t<true, false>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font, words, ring_hist, mbs, kc ? 1 : 0);
+  } else {
+    if (kc) launch_dp_t<false, true>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font, words, ring_hist, mbs, 1);
+    launch_dp_t<false, false>(st, jobs, segs, nsegs, lit_h, model, matches, choice, font, words, ring_hist, mbs, kc ? 1 : 0);
+  }
+}
+size_t dp_ring_hist_bytes(int nsegs) { return (size_t)std::max(nsegs, 1) * kHistPos * 16; }
+// words[g] = the four stream bytes at global position g (0 past the stream's end): the
+// distance-cache candidates compare 8 bytes with two aligned loads.  Thread per position.
+// (only the streams with a metablock the candidates run in: Job.binary)
+__global__ void words_kernel(const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref, uint32_t total, uint32_t *words) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= total || !jobs[pos_job[g >> kSegBits]].binary) return;
+  const SegRef r = seg_ref[g >> kSegBits];
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; k++)
+    if (g + k < r.end) v |= (uint32_t)r.base[g + k] << (8 * k);
+  words[g] = v;
+}
+void launch_words(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref, uint32_t total, uint32_t *words) {
+  if (total) hipLaunchKernelGGL(words_kernel, dim3((total + 255) / 256), dim3(256), 0, st, jobs, pos_job, seg_ref, total, words);
 }
 size_t cost_model_hist_bytes(int njobs) { return (size_t)njobs * kHistLen * 4; }
 void launch_cost_model(hipStream_t st, const Job *jobs, int njobs, const Seg *segs, int nsegs, const RawCmd *raw,

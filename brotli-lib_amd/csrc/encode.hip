@@ -273,6 +273,13 @@ bool near_scan(const Params &p) {
   static const int v = knob("MIB_NEAR") ? atoi(knob("MIB_NEAR")) : 1;
   return p.quality >= 10 && (v == 2 || (v == 1 && !p.font));
 }
+// distance-cache candidates in the parse (dp_kernel KC) at q10+, every mode
+// (MIB_DP_CACHE=0 turns them off: experiment builds)
+int g_no_dp_cache = 0;   // mib_force_no_dp_cache (tests)
+bool dp_cache(const Params &p) {
+  static const int v = knob("MIB_DP_CACHE") ? atoi(knob("MIB_DP_CACHE")) : 1;
+  return p.quality >= 10 && v != 0 && !__atomic_load_n(&g_no_dp_cache, __ATOMIC_RELAXED);
+}
 int hash_bytes(const Params &p) {
   static const int v = knob("MIB_HASH_BYTES") ? std::min(6, std::max(4, atoi(knob("MIB_HASH_BYTES")))) : -1;
   return v > 0 ? v : p.font ? 4 : kHashBytes;
@@ -474,6 +481,8 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   const bool two_pass = prm.quality >= 11 && zopfli_iterations() > 1;   // backward-references-hq.ts:562-605
   need += two_pass ? k * sizeof(CostModel) + cost_model_hist_bytes((int)k) : 0;
   need += std::max<uint64_t>(npieces, 1) * sizeof(Seg);   // parse pieces
+  const bool cache = dp_cache(prm);
+  need += cache ? dp_ring_hist_bytes((int)std::max<uint64_t>(npieces, (uint64_t)nsegs)) : 0;
   need += 41 * 256;   // alignment
   Workspace *ws = reinterpret_cast<Workspace *>(*ws_slot);
   if (!ws) {
@@ -525,6 +534,11 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   // the final parse on pieces of the segments (merge_pieces_kernel)
   const bool ps = npieces > (uint64_t)nsegs;
   Seg *d_pieces = ps ? ar.take<Seg>(std::max<uint64_t>(npieces, 1)) : nullptr;
+  // the candidates' ring history (per DP lane group) and position words (in the sort's first
+  // key buffer, free once the sort is done)
+  uint32_t *ring_hist =
+      cache ? reinterpret_cast<uint32_t *>(ar.take<uint8_t>(dp_ring_hist_bytes((int)std::max<uint64_t>(npieces, (uint64_t)nsegs)))) : nullptr;
+  uint32_t *pos_words = cache ? keys : nullptr;
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
   Timer tm{ctx, st, mib_ctx_profiling(ctx) != 0, {}};
@@ -579,15 +593,19 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
       if (any_hist) launch_hist_update(st, d_jobs, d_seg_job, skeys, svals, total);
       launch_lit_histo(st, d_jobs, d_segs, nsegs, lit_h);
     }
+    // (the parse's candidates go by the metablocks' context modes)
+    if (!forked) launch_context_mode(st, d_jobs, d_mbs, nmbs);
     tm.stop();
     fk.join();
+    // (after the join: the words go by Job.binary, which the context modes set)
+    if (pos_words) launch_words(st, d_jobs, d_seg_job, d_seg_ref, total, pos_words);
     // the history table's update (read by the next call's match search): beside the parse
     fk.fork();
     if (forked && any_hist) launch_hist_update(fk.side, d_jobs, d_seg_job, skeys, svals, total);
     tm.start(two_pass ? "dp_sample" : "dp_parse");
     Seg *s1 = sampled ? d_sample : two_pass ? d_segs : d_fin;
     const int n1 = s1 == d_fin ? nfin : nsegs;
-    launch_dp(st, d_jobs, s1, n1, lit_h, nullptr, matches, choice, any_cdict, prm.font);
+    launch_dp(st, d_jobs, s1, n1, lit_h, nullptr, matches, choice, any_cdict, prm.font, pos_words, ring_hist, d_mbs);
     tm.stop();
     tm.start("backtrack");
     launch_backtrack(st, d_jobs, s1, n1, choice, raw);
@@ -597,7 +615,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
       launch_cost_model(st, d_jobs, (int)k, s1, nsegs, raw, model_h, model);
       tm.stop();
       tm.start("dp_parse");
-      launch_dp(st, d_jobs, d_fin, nfin, lit_h, model, matches, choice, any_cdict, prm.font);
+      launch_dp(st, d_jobs, d_fin, nfin, lit_h, model, matches, choice, any_cdict, prm.font, pos_words, ring_hist, d_mbs);
       tm.stop();
       tm.start("backtrack");
       launch_backtrack(st, d_jobs, d_fin, nfin, choice, raw);
@@ -608,7 +626,6 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
     launch_carry(st, d_jobs, (int)k, d_segs, d_mbs);
     if (two_pass && rep_pass(prm)) launch_rep(st, d_jobs, d_segs, nsegs, model, raw, cmd_pos);   // (cmd_pos: scratch until codes)
     launch_ring_scan(st, d_jobs, (int)k, d_segs, nsegs, raw, push);
-    if (!forked) launch_context_mode(st, d_jobs, d_mbs, nmbs);
     launch_codes(st, d_jobs, d_segs, d_mbs, nsegs, raw, cmds, cmd_pos, units, unit_h);
     launch_dist_ring(st, d_jobs, (int)k, d_segs, cmds);
     tm.stop();
@@ -895,6 +912,8 @@ struct mib_encoder {
   uint64_t staged = 0;            // ... these many bytes, still to go behind the pending input
 };
 extern "C" {
+
+void mib_force_no_dp_cache(int off) { __atomic_store_n(&g_no_dp_cache, off ? 1 : 0, __ATOMIC_RELAXED); }
 
 void mib_encode_ws_free(void *p) {
   Workspace *ws = reinterpret_cast<Workspace *>(p);

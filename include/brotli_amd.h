@@ -126,6 +126,11 @@ void mib_force_ballot_rank(int force);
  * device is visible (by default a single device runs them as mib_encode_batch / mib_decode_batch,
  * one launch sequence). */
 void mib_force_shards(int force);
+/* Diagnostic (tests): non-zero turns the q10+ parse's distance-cache candidates off (the
+ * parse then prices only last-distance copies, short codes 1-15 arise only where codes_kernel
+ * finds a chosen distance in the ring), so a test can show what the candidates change; 0
+ * restores them. */
+void mib_force_no_dp_cache(int off);
 
 void mib_buf_free(mib_buf *b);
 /* The allocator behind every mib_buf the library returns (default malloc / free), in the

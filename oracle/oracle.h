@@ -28,6 +28,7 @@ uint64_t oracle_compound_refs(void);
 /* out[4]: the copies decoded on this thread since the last call, by distance code: implicit
  * (command code < 128), explicit code 0, short codes 1-15, explicit distances (>= 16) */
 void oracle_dist_code_counts(uint64_t *out);
+void oracle_max_block_types(int *out);   /* largest (literal, command, distance) block type counts decoded (clears) */
 
 /* encode.ts:50 brotliEncode (bugs A,B fixed = the survey's "ref-fixed"; C,E fixed too).
  * quality 0..11, lgwin 10..24, mode 0 GENERIC / 1 TEXT / 2 FONT. */

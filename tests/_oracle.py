@@ -111,3 +111,11 @@ def probe(data, positions):
     if rc:
         raise RuntimeError('oracle_decode_probe rc=%d' % rc)
     return out
+
+
+def max_block_types():
+    """the largest (literal, command, distance) block type counts of any metablock the oracle
+    decoder has decoded on this thread since the last call"""
+    out = (ctypes.c_int * 3)()
+    lib().oracle_max_block_types(out)
+    return list(out)

@@ -50,3 +50,36 @@ def test_record_stride_parse_uses_the_distance_cache(mode):
     ref = _oracle.encode(data[:60000], 11, 22, 2 if mode == brotli_amd.EncoderMode.FONT else 0)
     ours = brotli_amd.brotliEncode(data[:60000], {'quality': 11, 'mode': mode})
     assert len(ours) < len(ref)
+
+
+def _dp_cache(on):
+    import ctypes
+    lib = brotli_amd._L()
+    lib.mib_force_no_dp_cache.restype = None
+    lib.mib_force_no_dp_cache.argtypes = [ctypes.c_int]
+    lib.mib_force_no_dp_cache(0 if on else 1)
+
+
+@pytest.mark.parametrize('mode', [brotli_amd.EncoderMode.GENERIC, brotli_amd.EncoderMode.TEXT, brotli_amd.EncoderMode.FONT])
+def test_short_codes_come_from_the_parse(mode):
+    """The parse's distance-cache candidates (dp_kernel KC: the path's ring, 15 short codes per
+    node, backward-references-hq.ts:309-345) in every mode: with them the stream takes many more
+    short codes 1-15 than the same parse without them (where short codes arise only when
+    codes_kernel finds a chosen distance in the decoder's ring) and gets smaller."""
+    data = records(200000, 11)
+    try:
+        _dp_cache(False)
+        off = brotli_amd.brotliEncode(data, {'quality': 11, 'mode': mode})
+    finally:
+        _dp_cache(True)
+    on = brotli_amd.brotliEncode(data, {'quality': 11, 'mode': mode})
+    counts = {}
+    for name, enc in (('off', off), ('on', on)):
+        _oracle.dist_code_counts()
+        assert _oracle.decode(enc) == data
+        assert brotli_amd.brotliDecode(enc) == data
+        counts[name] = _oracle.dist_code_counts()
+    print('mode %d: without candidates %s, %d bytes; with %s, %d bytes' % (mode, counts['off'], len(off), counts['on'], len(on)))
+    short_off, short_on = counts['off'][2], counts['on'][2]
+    assert short_on > short_off + 100
+    assert len(on) < len(off)
