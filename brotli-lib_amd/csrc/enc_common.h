@@ -166,6 +166,7 @@ struct Mb {                   // one metablock: block types per category, litera
   uint32_t hdr_bits;          // header bits before the prefix codes (incl. context maps)
   uint32_t ctx_mode;          // literal context mode (chooseContextMode, context.ts:180-227)
   uint32_t nbt[3];            // block types: literal, command, distance
+  float split_gain[3];        // the four-type split's saving, a share of the one-type cost (0: no split)
   uint32_t first_count[3];    // symbols in the first block of each category
   uint32_t nlit_t[kMaxBT], ndist_t[kMaxBT];   // prefix codes (clusters) per literal / distance block type
   uint16_t lit_cmap[kLitSlots];            // (type, context) -> literal code slot (type * 64 + cluster)
@@ -525,6 +526,7 @@ void launch_dp(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, cons
                const uint32_t *matches, uint64_t *choice, bool cdict, bool font, const uint32_t *words, uint32_t *ring_hist,
                const Mb *mbs);
 size_t dp_ring_hist_bytes(int nsegs);
+void launch_any_binary(hipStream_t st, const Job *jobs, int njobs, uint32_t *flag);
 void launch_words(hipStream_t st, const Job *jobs, const uint32_t *pos_job, const SegRef *seg_ref, uint32_t total, uint32_t *words);
 void launch_backtrack(hipStream_t st, const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice, RawCmd *raw);
 void launch_carry(hipStream_t st, Job *jobs, int njobs, Seg *segs, const Mb *mbs);

@@ -419,8 +419,11 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
   __shared__ float red_v[kCluT / 64];
   __shared__ int red_i[kCluT / 64];
   __shared__ int sh_best, sh_alive;
-  // block per (metablock, literal type < kl | distance type < kd)
-  const int nr = kl + kd, m = blockIdx.x / nr, r = blockIdx.x % nr, kind = r < kl ? 0 : 1, ty = kind == 0 ? r : r - kl;
+  __shared__ int rep_id[kMaxH];
+  // block per (metablock, literal type < kl | distance type < 4); distance types 4 .. kd - 1 (the
+  // split's widening pass, rarely present) as a second item of the first blocks, so that the
+  // launch has no block per absent type (4 more per metablock: +2.7 ms a C4 launch, r06o)
+  const int nb = kl + 4, m = blockIdx.x / nb, r0 = blockIdx.x % nb;
   Mb &mb = mbs[m];
   const Job &jb = jobs[mb.job];
   if (jb.uncompressed) return;
@@ -438,6 +441,7 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
 #else
 #define CLMARK(k) do {} while (0)
 #endif
+  auto item = [&](const int kind, const int ty) {
   const int nbt = (int)(kind == 0 ? mb.nbt[0] : mb.nbt[2]);
   if (ty >= nbt) {
     if (t == 0) {
@@ -490,6 +494,28 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     sh_alive = na;
   }
   CLMARK(0);
+  if (cap == 1 && sh_alive > 1) {
+    // one code for the type (the decoder budget left no more, cluster_kernel's caller): every
+    // used context merged into the first, no pair search
+    __shared__ int sh_a0;
+    if (t == 0) {
+      int a0 = 0;
+      while (!alive[a0]) a0++;
+      sh_a0 = a0;
+    }
+    __syncthreads();
+    const int a0 = sh_a0;
+    for (int x = t; x < A; x += kCluT) {
+      uint32_t v = 0;
+      for (int a = 0; a < nh; a++) v += alive[a] ? h[a][x] : 0u;
+      h[a0][x] = v;
+    }
+    __syncthreads();
+    if (t < nh && alive[t]) label[t] = a0;
+    if (t < nh && t != a0) alive[t] = 0;
+    if (t == 0) sh_alive = 1;
+    __syncthreads();
+  }
   // savings of every pair
   auto pair_saving = [&](int a, int b) -> float {
     float sum = 0.f, ent = 0.f;
@@ -618,7 +644,6 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
   }
   CLMARK(3);
   // number the clusters by first use; unused contexts go to cluster 0
-  __shared__ int rep_id[kMaxH];
   if (t == 0) {
     for (int a = 0; a < nh; a++) rep_id[a] = -1;
     int k = 0;
@@ -641,6 +666,12 @@ __global__ __launch_bounds__(kCluT) void cluster_kernel(const Job *jobs, Mb *mbs
     const int a = i / 256, x = i % 256;
     const int c = alive[a] ? rep_id[a] : -1;
     if (c >= 0 && x < A) src[c * stride + x] = h[a][x];
+  }
+  };
+  item(r0 < kl ? 0 : 1, r0 < kl ? r0 : r0 - kl);
+  if (r0 < kd - 4) {
+    __syncthreads();
+    item(1, 4 + r0);
   }
 #ifdef MIB_PROF
   CLMARK(4);
@@ -1237,6 +1268,9 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   __shared__ __attribute__((aligned(16))) uint8_t buf[kTreeBytes];   // (words for store_complex_wave)
   __shared__ int sh_nr;
   __shared__ TreeScratch ts;
+  // nr blocks per metablock: nl literal codes, four command and sixteen distance slots (types
+  // 0..3); the slots of command / distance types 4..7 (the split's widening pass, rarely
+  // present) are second items of the first blocks, so the launch has no block per absent type
   const int m = blockIdx.x / nr, r = (int)(blockIdx.x % nr);
   const int lane = threadIdx.x;
   Mb &mb = mbs[m];
@@ -1254,18 +1288,21 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
       if (!slot_used(q)) mb.tree_bits[q] = 0;
   // block r builds the r-th used code: literal codes first (at most kMaxLitTrees of them,
   // numbered per block type), then the command codes, then the distance codes
-  int t = -1;
+  int t0 = -1, t1 = -1;
   if (r < nl) {
     int acc = 0;
-    for (int ty = 0; ty < (int)mb.nbt[0] && t < 0; ty++) {
-      if (r < acc + (int)mb.nlit_t[ty]) t = ty * kLitCtx + (r - acc);
+    for (int ty = 0; ty < (int)mb.nbt[0] && t0 < 0; ty++) {
+      if (r < acc + (int)mb.nlit_t[ty]) t0 = ty * kLitCtx + (r - acc);
       acc += (int)mb.nlit_t[ty];
     }
-  } else if (r < nl + kc) {
-    t = kCmdSlot + (r - nl);
+  } else if (r < nl + 4) {
+    t0 = kCmdSlot + (r - nl);
   } else {
-    t = kDistSlot + (r - nl - kc);
+    t0 = kDistSlot + (r - nl - 4);
   }
+  if (r < kc - 4) t1 = kCmdSlot + 4 + r;
+  else if (r < kc - 4 + 4 * kDistCtx) t1 = kDistSlot + 4 * kDistCtx + (r - (kc - 4));
+  auto item = [&](const int t) {
   if (t < 0 || !slot_used(t)) return;
   const bool lit = t < kCmdSlot, dist = t >= kDistSlot;
   const int cl = lit ? t : dist ? t - kDistSlot : t - kCmdSlot;   // slot within its alphabet
@@ -1417,6 +1454,12 @@ __global__ __launch_bounds__(64) void huffman_kernel(const Job *jobs, Mb *mbs, i
   for (int i = lane; i < asize; i += 64) {
     dd[i] = depth[i];
     cc[i] = code[i];
+  }
+  };
+  item(t0);
+  if (t1 >= 0) {
+    wave_sync();
+    item(t1);
   }
 }
 
@@ -1637,13 +1680,19 @@ __device__ void split_path(int t, int nu, const uint32_t *ns, const float *ucost
 // with 8 their prefix codes overflow the decoder's LDS table area (§7) and C4 decode goes from
 // 140 to 299 ms for 0.05 % of bytes.  (A/B: MIB_SPLIT_BT = "l,c,d", each 1..kMaxBT.)
 constexpr int kSplitBtLit = 8;
-constexpr float kExtraTypeBits = 400.f;   // a literal code's worth (C4: 24 -> 16 literal codes, +0.1 % bytes, r06d)
+constexpr float kExtraTypeBits = 400.f;
+// a four-type command / distance split that saved at least this share of the one-type cost is
+// tried again with eight seeds (the heterogeneous input of test_more_than_four_command_and_
+// distance_block_types: 0.217 for commands; C4's text ~0.010 / 0.035, C3's glyphs 0.05-0.09,
+// r06k): past four types the data must differ in kind
+constexpr float kWidenGain = 0.15f;   // a literal code's worth (C4: 24 -> 16 literal codes, +0.1 % bytes, r06d)
 __device__ __forceinline__ int nu_of(const Mb &mb) { return (int)mb.nseg * kSubPerSeg; }
-struct SplitK { int k[3]; };
+struct SplitK { int k[3]; int dbg; int widen; };
 SplitK split_k() {
   static const SplitK sk = [] {
-    SplitK k{{kSplitBtLit, kMaxBT, kMaxBT}};
+    SplitK k{{kSplitBtLit, 4, 4}, 0, 0};
     if (const char *e = knob("MIB_SPLIT_BT")) sscanf(e, "%d,%d,%d", &k.k[0], &k.k[1], &k.k[2]);
+    k.dbg = knob("MIB_SPLIT_PRINT") ? atoi(knob("MIB_SPLIT_PRINT")) : 0;   // (experiments: the first n metablocks' split costs)
     for (int c = 0; c < 3; c++) k.k[c] = std::min(kMaxBT, std::max(1, k.k[c]));
     return k;
   }();
@@ -1673,8 +1722,16 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   // (literals: the metablock's 24 codes -- the decoder's LDS budget -- serve more block types
   // in a short metablock, more contexts per type in a long one; FONT mode keeps 4: C3 0.45579
   // -> 0.45569 for 2 % of its MB/s, r04am)
-  const int K = cat == 0 && (nu_of(mbs[m]) > kSplitWideUnits || jobs[mbs[m].job].font) ? min(sk.k[0], 4) : sk.k[cat];
-  if ((K <= 4) != (S == 4)) return;   // (the other launch's block)
+  int K = cat == 0 && (nu_of(mbs[m]) > kSplitWideUnits || jobs[mbs[m].job].font) ? min(sk.k[0], 4) : sk.k[cat];
+  if (sk.widen) {
+    // the widening pass (launch_split): command / distance categories whose four-type split
+    // saved at least kWidenGain of the one-type cost are split again with kMaxBT seeds
+    if constexpr (S == 4) return;
+    if (cat == 0 || K > 4 || !(mb.split_gain[cat] >= kWidenGain)) return;
+    K = kMaxBT;
+  } else if ((K <= 4) != (S == 4)) {
+    return;   // (the other launch's block)
+  }
 #ifdef MIB_PROF
   uint64_t sp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sp0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1838,12 +1895,16 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       for (int q = 0; q < S; q++) used += tot[q] ? 1 : 0;
       const float split_cost = red[0] + 40.f * (float)used + sw_cost * (float)nsw + 60.f;
       sh_keep = (used > 1 && split_cost < base_cost) ? 1 : 0;
+      if (!sk.widen) mb.split_gain[cat] = sh_keep ? (base_cost - split_cost) / base_cost : 0.f;
+      if (m < sk.dbg) printf("[split] mb %d cat %d K %d used %d units %d base %.0f split %.0f gain %.4f\n", m, cat, K, used, ne,
+                             base_cost, split_cost, (base_cost - split_cost) / base_cost);
     }
     __syncthreads();
     SPMARK(6);
     return sh_keep;
   };
   if (K > 1 && ne >= 2 * K) keep = refine();
+  else if (t == 0 && !sk.widen) mb.split_gain[cat] = 0.f;
   if constexpr (S > 4) {
     // Command / distance types past four (the reference allows 256) take room from
     // the literal codes in the decoder's LDS table area (cluster_kernel's budget: two literal
@@ -2502,6 +2563,17 @@ void launch_split(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, in
     if (few) hipLaunchKernelGGL((split_kernel<1024, kMaxBT>), dim3(nmbs * 3), dim3(1024), lds8, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
     else hipLaunchKernelGGL((split_kernel<256, kMaxBT>), dim3(nmbs * 3), dim3(256), lds8, st, jobs, mbs, nmbs, units, unit_h, codes, sk);
   }
+  // the widening pass: after the four-type split of the command and distance
+  // categories (on side), those whose split saved the most are split again with eight seeds,
+  // and keep more than four types where that pays (the merge pass in split_kernel)
+  static const bool widen = !knob("MIB_SPLIT_WIDEN") || atoi(knob("MIB_SPLIT_WIDEN")) != 0;   // (experiments: 0 off)
+  if (widen && narrow && std::max(sk.k[1], sk.k[2]) <= 4) {
+    SplitK wk = sk;
+    wk.widen = 1;
+    const size_t ldsw = (size_t)std::max(1, std::min(max_units, kMaxUnits)) * kMaxBT * sizeof(float);
+    if (few) hipLaunchKernelGGL((split_kernel<1024, kMaxBT>), dim3(nmbs * 3), dim3(1024), ldsw, side, jobs, mbs, nmbs, units, unit_h, codes, wk);
+    else hipLaunchKernelGGL((split_kernel<256, kMaxBT>), dim3(nmbs * 3), dim3(256), ldsw, side, jobs, mbs, nmbs, units, unit_h, codes, wk);
+  }
 }
 void launch_histo(hipStream_t st, const Job *jobs, const Seg *segs, const Mb *mbs, int nsegs, const Cmd *cmds,
                   const uint32_t *cmd_pos, const Unit *units, uint32_t *hl, uint32_t *hc, uint32_t *hd) {
@@ -2536,8 +2608,9 @@ int lit_tree_cap() {
 }
 void launch_cluster(hipStream_t st, const Job *jobs, Mb *mbs, int nmbs, uint32_t *hl, uint32_t *hd) {
   const SplitK sk = split_k();
-  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * (sk.k[0] + sk.k[2])), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, lit_tree_cap(),
-                     sk.k[0], sk.k[2]);
+  static const int kd = knob("MIB_TYPE_SIZING") ? sk.k[2] : kMaxBT;   // (the widening pass may leave more than sk.k[2] distance types)
+  hipLaunchKernelGGL(cluster_kernel, dim3(nmbs * (sk.k[0] + 4)), dim3(kCluT), 0, st, jobs, mbs, nmbs, hl, hd, lit_tree_cap(),
+                     sk.k[0], kd);
 }
 void launch_huffman(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, int nmbs, const uint32_t *hl,
                     const uint32_t *hc, const uint32_t *hd, Codes *codes, uint8_t *trees, uint8_t *hdr) {
@@ -2547,9 +2620,11 @@ void launch_huffman(hipStream_t st, hipStream_t side, const Job *jobs, Mb *mbs, 
   // blocks per metablock: the literal codes (at most the cap, or one per literal type), one per
   // command type, the distance (type, cluster) slots
   const SplitK sk = split_k();
-  const int nl = std::max(lit_tree_cap(), sk.k[0]), nr = nl + sk.k[1] + sk.k[2] * kDistCtx;
-  hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * nr), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, nl, sk.k[1],
-                     nr);
+  // (command / distance: kMaxBT types, the widening pass may leave more than sk.k[1], sk.k[2])
+  static const int kc = knob("MIB_TYPE_SIZING") ? sk.k[1] : kMaxBT, kdt = knob("MIB_TYPE_SIZING") ? sk.k[2] : kMaxBT;   // (experiments)
+  (void)kdt;
+  const int nl = std::max(lit_tree_cap(), sk.k[0]), nr = nl + 4 + 4 * kDistCtx;   // (types 4..kc-1: second items)
+  hipLaunchKernelGGL(huffman_kernel<704>, dim3(nmbs * nr), dim3(64), 0, st, jobs, mbs, nmbs, hl, hc, hd, codes, trees, nl, kc, nr);
   // the header reads the split's and the clustering's results, not the prefix codes (it writes
   // Mb.hdr_bits and the block-split codes, huffman_kernel Mb.tree_bits and the other codes)
   hipLaunchKernelGGL(mb_header_kernel, dim3(nmbs), dim3(64), 0, side, jobs, mbs, nmbs, hdr, codes);
