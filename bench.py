@@ -326,7 +326,7 @@ def run_stream(args, rank, world, local):
             'kernel_ms_per_step': {n: round(v[0] / args.steps, 3) for n, v in sorted(times.items())},
             'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 3), 'peak': PEAK_HBM_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 6),
-                         'traffic': load_traffic(dom_name, 'c5'),
+                         'traffic': load_traffic(dom_name, 'c5' if args.stream_chunk else 'c5cad'),
                          'algorithmic_bytes_per_launch': launch_bytes, 'avg_launch_ms': round(avg_ms, 3)},
             'cpu_baseline': cpu}), flush=True)
     if world > 1:

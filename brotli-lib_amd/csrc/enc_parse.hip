@@ -309,6 +309,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
   uint32_t kf = 0;
   uint32_t kp_ld = 0, kp_h = 0;   // node i-1's distance, its predecessor's ring entry rq (copy edge)
   float kp_base = 0.f;            // node i-1's cost + insert extra
+  uint32_t kp_m[kMaxMatches] = {};   // node i-1's staircase entries
   uint32_t rg = 0;                // ring entry rq of node i-2 (after the ring step: of node i-1)
   // node i-2's candidates: distance (0: none), source words, own words, cap | full length << 8
   uint32_t cq_d = 0, cq_w0 = 0, cq_w1 = 0, cq_c0 = 0, cq_c1 = 0, cq_lim = 0;
@@ -646,15 +647,13 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
           cq_c0 = pwords[gbase + x];
           cq_c1 = pwords[gbase + x + 4u];
         }
-        // node i-1's staircase (its stage entry, while this batch holds it): the full length of
-        // a staircase match at the candidate's distance
+        // node i-1's staircase (its entries, kept from its step): the full length of a staircase
+        // match at the candidate's distance.  (Read from its stage entry while the batch held it,
+        // the result depended on where the batches fall, i.e. on the lanes per segment -- and a
+        // stream must parse the same in any batch.)
         uint32_t full = 0;
-        if (off != 0u) {
-          const uint32_t ps = src - 1u;
-          const StageEnt &pe = stg[ps + (ps >> kPadSh)];
 #pragma unroll
-          for (int q = 0; q < kMaxMatches; q++) full = match_dist(pe.m[q]) == cd ? max(full, match_length(pe.m[q])) : full;
-        }
+        for (int q = 0; q < kMaxMatches; q++) full = match_dist(kp_m[q]) == cd ? max(full, match_length(kp_m[q])) : full;
         uint32_t cap = b - x;
         if (parts && cv) cap = min(cap, part_cap(abs0 + x, cd, pbits, plag));
         cq_lim = min(cap, (uint32_t)kLongCopy) | (min(full, (uint32_t)kLongCopy) << 8);
@@ -666,6 +665,8 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
       kf = (act ? (ccopy ? 2u : 1u) : 0u) | (pk ? 8u : 0u) | ((uint32_t)ic << 8) | (((kf >> 8) & 0xFFu) << 16);
       kp_ld = ld;
       kp_base = base;
+#pragma unroll
+      for (int q = 0; q < kMaxMatches; q++) kp_m[q] = e.m[q];
     }
     DPMARK(5);   // (KC: the candidates' cycles)
     // node i's own last-distance candidate: loads now, measured in the next step (a window

@@ -83,3 +83,18 @@ def test_short_codes_come_from_the_parse(mode):
     short_off, short_on = counts['off'][2], counts['on'][2]
     assert short_on > short_off + 100
     assert len(on) < len(off)
+
+
+@pytest.mark.parametrize('mode', [brotli_amd.EncoderMode.GENERIC, brotli_amd.EncoderMode.FONT])
+def test_candidates_parse_the_same_in_any_batch(mode):
+    """A stream's parse must not depend on its batch: 24 x 1 MiB of records run the DP with two
+    segments a wave (3,072 parse pieces), one of them alone with one (128 pieces); the
+    candidates' pipeline (the ring history, the staircase lengths it reuses) must give the same
+    bytes either way."""
+    bufs = [records(1 << 20, 100 + i, rec=40 + 8 * (i % 5)) for i in range(24)]
+    outs = brotli_amd.encode_batch(bufs, {'quality': 11, 'mode': mode})
+    for i in (0, 7, 23):
+        single = brotli_amd.brotliEncode(bufs[i], {'quality': 11, 'mode': mode})
+        assert single == outs[i], i
+    assert _oracle.decode(outs[7]) == bufs[7]
+    assert brotli_amd.decode_batch(outs) == bufs
