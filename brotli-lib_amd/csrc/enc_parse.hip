@@ -569,6 +569,20 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
         }
       }
     }
+    // node i's own last-distance candidate: loads now, measured in the next step (a window
+    // distance only: not a dictionary word's or a custom-dictionary copy's)
+    if (KR) {
+      const bool rv = act && use_rep && ins > 0 && ld != 0u && !(words && is_dict(ld)) && ld <= min(wabs + i, maxback);
+      rp_d = rv ? ld : 0u;
+      rp_base = base;
+      rp_ic = (uint32_t)ic;
+      rp_cb = 0;
+      rp_sb = 1;
+      if (rv && hl < (uint32_t)kRepLen && i + hl < b) {
+        rp_cb = ((GCU8 *)data)[i + hl];
+        rp_sb = ((GCU8 *)data)[(int64_t)(i + hl) - (int64_t)ld];
+      }
+    }
     DPMARK(3);
     if (KC) {
       // (1) node i-2's candidates (loaded one step ago): the match length over 8 bytes (all 8:
@@ -580,22 +594,20 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
       R = min(R, cq_lim & 0xFFu);
       const bool pass = act && (kf & 8u) && cq_d != 0u && R >= 4u;
       uint64_t pm = __ballot(pass);
+      DPCOUNT(2, pm ? 1 : 0);   // (MIB_PROF: steps with a passing candidate; slot 7: the loop's iterations)
       if (pm) {
         // the lengths' copy prices out of node i-2 (its insert code's row), both halves, for the
         // chunks the longest passing candidate reaches: read once, before the candidates' loop
         const uint32_t *crow = ptab + ((kf >> 16) & 0xFFu) * kPtabW;
-        // (the wave's longest reach, bit by bit from ballots: no cross-lane latency chain)
-        uint32_t rmax = 0;
-#pragma unroll
-        for (int bit = 7; bit >= 0; bit--) {
-          const uint32_t trial = rmax | (1u << bit);
-          if (__ballot(pass && R >= trial)) rmax = trial;
-        }
+        // (only the chunks some passing candidate reaches: one ballot a chunk; all kC chunks'
+        // lookups unconditionally were 88 of the section's instructions, r06 ISA listing)
         uint32_t ctv[kC];
 #pragma unroll
         for (int c = 0; c < kC; c++) {
+          ctv[c] = 0u;
+          if (c > 1 && __ballot(pass && (uint32_t)(kL * c) + 2u <= off + R) == 0) break;
           const uint32_t lr = (uint32_t)(kL * c) + hl + 2u - off;   // wraps (huge) below node i-2
-          ctv[c] = (lr >= 4u && lr <= rmax) ? crow[cctab[lr]] : 0u;
+          if (lr >= 4u && lr <= (uint32_t)kLongCopy) ctv[c] = crow[cctab[lr]];
         }
         // every passing candidate in turn (the lowest short code first), each relaxing lengths
         // 4..R at its own price (the farthest-reaching one alone lost the cheaper short codes of
@@ -621,6 +633,7 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
             }
           }
           pm &= ~__ballot(mine != 0u && hl == k);
+          DPCOUNT(7, 1);
         } while (pm);
       }
       DPMARK(6);   // (KC: measuring and relaxing node i-2's candidates)
@@ -632,21 +645,18 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
         ring_hist[hoff + ((i - 1u) & (kHistPos - 1)) * 4 + rq] = rg;
       }
       // (3) node i-1's candidates: a lane per short code, its distance from the ring, its first 8
-      // source bytes and node i-1's own loaded now (measured next step)
+      // source bytes and node i-1's own loaded below (measured next step)
+      bool cv;
+      uint32_t cx;
       {
         const uint32_t e0 = quad_entry0(rg), e1 = quad_entry1(rg);
         const uint32_t cb = cj < 4u ? rg : cj < 10u ? e0 : e1;
         const int coff = cj < 4u ? 0 : (int)(((cj - 4u) % 6u) / 2u + 1u) * (((cj - 4u) & 1u) ? 1 : -1);
         const uint32_t cd = cb + (uint32_t)coff;
         const uint32_t x = i - 1u;
-        const bool cv = clane && pk != 0u && cb != 0u && !words_on_ring(cb) && cd - 1u < min(x, maxback);
+        cv = clane && pk != 0u && cb != 0u && !words_on_ring(cb) && cd - 1u < min(x, maxback);
         cq_d = cv ? cd : 0u;
-        if (cv) {
-          cq_w0 = pwords[gbase + x - cd];
-          cq_w1 = pwords[gbase + x - cd + 4u];
-          cq_c0 = pwords[gbase + x];
-          cq_c1 = pwords[gbase + x + 4u];
-        }
+        cx = gbase + x;
         // node i-1's staircase (its entries, kept from its step): the full length of a staircase
         // match at the candidate's distance.  (Read from its stage entry while the batch held it,
         // the result depended on where the batches fall, i.e. on the lanes per segment -- and a
@@ -667,22 +677,18 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
       kp_base = base;
 #pragma unroll
       for (int q = 0; q < kMaxMatches; q++) kp_m[q] = e.m[q];
-    }
-    DPMARK(5);   // (KC: the candidates' cycles)
-    // node i's own last-distance candidate: loads now, measured in the next step (a window
-    // distance only: not a dictionary word's or a custom-dictionary copy's)
-    if (KR) {
-      const bool rv = act && use_rep && ins > 0 && ld != 0u && !(words && is_dict(ld)) && ld <= min(wabs + i, maxback);
-      rp_d = rv ? ld : 0u;
-      rp_base = base;
-      rp_ic = (uint32_t)ic;
-      rp_cb = 0;
-      rp_sb = 1;
-      if (rv && hl < (uint32_t)kRepLen && i + hl < b) {
-        rp_cb = ((GCU8 *)data)[i + hl];
-        rp_sb = ((GCU8 *)data)[(int64_t)(i + hl) - (int64_t)ld];
+      // the candidates' loads last: vmcnt counts loads (and stores) in issue order, so a wait for
+      // an older load -- the ring above, KR's bytes -- never waits for these far-back sources
+      // (issued before them, KR's measure and the ring step waited out their HBM latency:
+      // candidates 1,160 cycles a step, r06r)
+      if (cv) {
+        cq_w0 = pwords[cx - cq_d];
+        cq_w1 = pwords[cx - cq_d + 4u];
+        cq_c0 = pwords[cx];
+        cq_c1 = pwords[cx + 4u];
       }
     }
+    DPMARK(5);   // (KC: the candidates' cycles)
     if (act) i++;
     const bool bend = act && i - i0 == (uint32_t)kL;
     if (__ballot(bend)) {

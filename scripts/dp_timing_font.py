@@ -20,7 +20,7 @@ cap = k * size + k * 8192
 comp = torch.empty(cap, dtype=torch.uint8, device=dev)
 lib = brotli_amd._L()
 prof = (ctypes.c_ulonglong * 8)()
-names = ['stage_cyc', 'node_cyc', 'long_cyc', 'relax_cyc', 'steps', 'kc_cyc', 'kc1_cyc', 'unused']
+names = ['stage_cyc', 'node_cyc', 'long_cyc', 'relax_cyc', 'steps', 'kc_cyc', 'kc1_cyc', 'kc_iters']
 nseg = k * size // 65536
 lib.mib_force_no_dp_cache.argtypes = [ctypes.c_int]
 for it in range(4):
@@ -34,3 +34,5 @@ for it in range(4):
     st = max(1.0, d['steps'])
     print('per step: node %.1f relax %.1f kc measure+relax %.1f kc ring+issue %.1f stage %.1f long %.1f cycles' % (
         d['node_cyc'] / st, d['relax_cyc'] / st, d['kc1_cyc'] / st, d['kc_cyc'] / st, d['stage_cyc'] / st, d['long_cyc'] / st), flush=True)
+    print('candidate loop: iterations per step %.3f (the long-copy slot counts steps with a passing candidate: %.3f)' % (
+        d['kc_iters'] / st, d['long_cyc'] / st), flush=True)
