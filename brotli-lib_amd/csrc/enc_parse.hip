@@ -309,10 +309,12 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
   uint32_t kf = 0;
   uint32_t kp_ld = 0, kp_h = 0;   // node i-1's distance, its predecessor's ring entry rq (copy edge)
   float kp_base = 0.f;            // node i-1's cost + insert extra
-  uint32_t kp_m[kMaxMatches] = {};   // node i-1's staircase entries
   uint32_t rg = 0;                // ring entry rq of node i-2 (after the ring step: of node i-1)
-  // node i-2's candidates: distance (0: none), source words, own words, cap | full length << 8
+  // node i-2's candidates: distance (0: none), source words, own words, length cap, its match
+  // record (the staircase: a match's full length at the candidate's distance)
   uint32_t cq_d = 0, cq_w0 = 0, cq_w1 = 0, cq_c0 = 0, cq_c1 = 0, cq_lim = 0;
+  uint32_t cq_m[kMaxMatches] = {};
+  const int coff = cj < 4u ? 0 : (int)(((cj - 4u) % 6u) / 2u + 1u) * (((cj - 4u) & 1u) ? 1 : -1);   // short code cj's offset
   float cq_base = 0.f;
   auto words_on_ring = [&](uint32_t dd) { return words && is_dict(dd); };
   auto ring_step = [&](uint32_t kind, uint32_t dd, uint32_t h, uint32_t prev) -> uint32_t {
@@ -590,8 +592,14 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
       // piece of a longer copy would split it in two commands), and the copies of lengths 4..R
       // relaxed out of node i-2 (lane j of chunk c: length kL c + j + 2 - off)
       const uint32_t x0 = cq_w0 ^ cq_c0, x1 = cq_w1 ^ cq_c1;
-      uint32_t R = x0 ? 0u : x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : max(8u, cq_lim >> 8);
-      R = min(R, cq_lim & 0xFFu);
+      uint32_t R = x0 ? 0u : x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : 8u;
+      if (__ballot(R == 8u && cq_d != 0u)) {   // (rare: the record is read only then)
+        uint32_t full = 0;
+#pragma unroll
+        for (int q = 0; q < kMaxMatches; q++) full = match_dist(cq_m[q]) == cq_d ? max(full, match_length(cq_m[q])) : full;
+        R = R == 8u ? max(R, full) : R;
+      }
+      R = min(R, cq_lim);
       const bool pass = act && (kf & 8u) && cq_d != 0u && R >= 4u;
       uint64_t pm = __ballot(pass);
       DPCOUNT(2, pm ? 1 : 0);   // (MIB_PROF: steps with a passing candidate; slot 7: the loop's iterations)
@@ -651,22 +659,14 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
       {
         const uint32_t e0 = quad_entry0(rg), e1 = quad_entry1(rg);
         const uint32_t cb = cj < 4u ? rg : cj < 10u ? e0 : e1;
-        const int coff = cj < 4u ? 0 : (int)(((cj - 4u) % 6u) / 2u + 1u) * (((cj - 4u) & 1u) ? 1 : -1);
         const uint32_t cd = cb + (uint32_t)coff;
         const uint32_t x = i - 1u;
         cv = clane && pk != 0u && cb != 0u && !words_on_ring(cb) && cd - 1u < min(x, maxback);
         cq_d = cv ? cd : 0u;
         cx = gbase + x;
-        // node i-1's staircase (its entries, kept from its step): the full length of a staircase
-        // match at the candidate's distance.  (Read from its stage entry while the batch held it,
-        // the result depended on where the batches fall, i.e. on the lanes per segment -- and a
-        // stream must parse the same in any batch.)
-        uint32_t full = 0;
-#pragma unroll
-        for (int q = 0; q < kMaxMatches; q++) full = match_dist(kp_m[q]) == cd ? max(full, match_length(kp_m[q])) : full;
         uint32_t cap = b - x;
         if (parts && cv) cap = min(cap, part_cap(abs0 + x, cd, pbits, plag));
-        cq_lim = min(cap, (uint32_t)kLongCopy) | (min(full, (uint32_t)kLongCopy) << 8);
+        cq_lim = min(cap, (uint32_t)kLongCopy);
         cq_base = kp_base;
       }
       // (4) node i for the next step: its edge, its predecessor's ring (copy edge)
@@ -675,8 +675,6 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
       kf = (act ? (ccopy ? 2u : 1u) : 0u) | (pk ? 8u : 0u) | ((uint32_t)ic << 8) | (((kf >> 8) & 0xFFu) << 16);
       kp_ld = ld;
       kp_base = base;
-#pragma unroll
-      for (int q = 0; q < kMaxMatches; q++) kp_m[q] = e.m[q];
       // the candidates' loads last: vmcnt counts loads (and stores) in issue order, so a wait for
       // an older load -- the ring above, KR's bytes -- never waits for these far-back sources
       // (issued before them, KR's measure and the ring step waited out their HBM latency:
@@ -686,6 +684,11 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
         cq_w1 = pwords[cx - cq_d + 4u];
         cq_c0 = pwords[cx];
         cq_c1 = pwords[cx + 4u];
+        // node i-1's match record (its staircase, as the match finder stored it): the full
+        // length of a staircase match at the candidate's distance.  (From its stage entry, while
+        // the batch held it, the result depended on where the batches fall -- on the lanes per
+        // segment -- and a stream must parse the same in any batch.)
+        rec_load(matches + (uint64_t)cx * kMatchRec, cq_m);
       }
     }
     DPMARK(5);   // (KC: the candidates' cycles)
