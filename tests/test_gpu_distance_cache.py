@@ -98,3 +98,36 @@ def test_candidates_parse_the_same_in_any_batch(mode):
         assert single == outs[i], i
     assert _oracle.decode(outs[7]) == bufs[7]
     assert brotli_amd.decode_batch(outs) == bufs
+
+
+def test_candidates_in_every_stream_shape():
+    """Binary (non-UTF-8) data takes the candidates in every encoder shape: streaming chunks
+    (their candidates stay inside the chunk), part-indexed streams of >= 2 MiB (a candidate
+    copy from an earlier part obeys the part lag), small windows (a candidate never reaches past
+    the window), static-dictionary words and a custom dictionary on the ring (never candidate
+    bases); every stream decodes with the oracle and with the HIP decoder."""
+    data = records(3 << 20, 21, rec=56)
+    # part-indexed one-shot stream (>= 2 MiB): HIP decodes it part-parallel
+    enc = brotli_amd.brotliEncode(data, {'quality': 11})
+    assert _oracle.decode(enc) == data
+    assert brotli_amd.brotliDecode(enc) == data
+    # streaming in 1 MiB update() chunks, and small chunks
+    for step in (1 << 20, 300000):
+        e = brotli_amd.BrotliEncoder({'quality': 11})
+        out = b''.join([e.update(data[p:p + step]) for p in range(0, len(data), step)] + [e.finish()])
+        assert brotli_amd.brotliDecode(out) == data
+        assert _oracle.decode(out) == data
+    small = data[:200000]
+    for lg in (10, 12, 16):
+        enc = brotli_amd.brotliEncode(small, {'quality': 11, 'lgwin': lg})
+        assert _oracle.decode(enc) == small, lg
+        assert brotli_amd.brotliDecode(enc) == small, lg
+    # a custom dictionary (its tail copies push on the ring) and static-dictionary words
+    cdict = records(20000, 5, rec=56)
+    mixed = cdict[-3000:] + small[:100000] + b' the world of the people ' * 40
+    enc = brotli_amd.brotliEncode(mixed, {'quality': 11, 'customDictionary': cdict})
+    assert brotli_amd.brotliDecode(enc, {'customDictionary': cdict}) == mixed
+    assert _oracle.decode(enc, dictionary=cdict) == mixed
+    enc = brotli_amd.brotliEncode(mixed, {'quality': 11})
+    assert _oracle.decode(enc) == mixed
+    assert brotli_amd.brotliDecode(enc) == mixed
