@@ -126,6 +126,9 @@ struct Dec {
   // part mode: [part_start, part_end) of the output, progress publishing, the stream's
   // progress words (part_end = INT_MAX: whole-stream mode)
   int part, part_start, part_end, pub_next, pidx, cover_lo;
+#ifdef MIB_PROF
+  int pidx_g;
+#endif
   int pctx;              // part mode: the two output bytes before part_start (p1 | p2 << 8, from the entry)
   uint64_t *prog;
   const int64_t *ppos;   // the stream's part start positions (+ its total at [nparts])
@@ -175,6 +178,21 @@ constexpr bool kSpecLit = MIB_SPECLIT;
 
 #ifdef MIB_PROF   // timing experiment: cycles in command / literal / distance / copy, literal and command counts
 __device__ unsigned long long g_prof[16];   // + metablocks with LDS / HBM tables
+// per part (decode_parts_kernel): start / end clock, cycles in part_wait, part_wait calls, spins,
+// header done clock, commands (unused), the wave's hardware id
+constexpr int kPartProfMax = 8192;
+__device__ unsigned long long g_part_prof[kPartProfMax * 8];
+// metablock headers: cycles in partitions + modes, context maps, literal / command / distance
+// groups, the LDS copy; headers, literal trees, read_code_lengths cycles, build_table cycles
+__device__ unsigned long long g_hdr_prof[16];
+#define HMARK(k)                                        \
+  do {                                                  \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    if (LANE == 0) atomicAdd(&g_hdr_prof[k], t_ - ht0); \
+    ht0 = t_;                                           \
+  } while (0)
+#else
+#define HMARK(k) do {} while (0)
 #endif
 
 // A block is one wave: a wave's LDS and global accesses are performed in order, so the
@@ -358,6 +376,9 @@ __device__ __noinline__ int part_wait(int a, int b) {
   const int64_t *ppos = s.ppos;
   const int lo = g_lds.part_lo[lane], hi = g_lds.part_hi[lane];
   const int cover_lo = s.cover_lo;
+#ifdef MIB_PROF
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
   for (uint32_t spin = 0;; spin++) {
     const int w = pidx - 1 - lane;
     const uint64_t v = w >= 0 ? __hip_atomic_load(s.prog + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
@@ -386,6 +407,14 @@ __device__ __noinline__ int part_wait(int a, int b) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU's L1 drops what it held
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       wave_sync();
+#ifdef MIB_PROF
+      if (lane == 0 && s.pidx_g < kPartProfMax) {
+        unsigned long long *q = g_part_prof + 8 * s.pidx_g;
+        q[2] += __builtin_amdgcn_s_memtime() - t0;
+        q[3] += 1;
+        q[4] += spin;
+      }
+#endif
       return 0;
     }
     if (spin > (1u << 24)) return kPartFail;   // (bounded: a part never waits on a later one)
@@ -454,13 +483,40 @@ __device__ int build_table(DecS &s, int32_t *group, int cap, int idx, int root, 
     wave_sync();
     return total;
   }
-  int key = 0, sym = 0, step = 1;
-  for (int l = 1; l <= root; l++) {
-    step <<= 1;
-    for (; count[l] > 0; count[l]--) {
-      replicate(s, group, cap, toff + key, step, tsize, (l << 16) | sorted[sym++]);
-      key = next_key(key, l);
+  // Root-level entries, a symbol per lane: the canonical code of the i-th symbol in sorted
+  // order is first[l] + (i - start[l]) (first[l + 1] = (first[l] + count[l]) << 1), and its
+  // table key is that code reversed in l bits -- the key the reference's serial nextKey walk
+  // (engine.ts:1677-1762) reaches at it.  (Serially: one dependent step per symbol.)
+  uint32_t first_l = 0, start_l = 0;   // lane l: first[l], start[l]
+  int nroot = 0;
+  {
+    uint32_t code = 0, start = 0;
+    for (int l = 1; l < 16; l++) {
+      const uint32_t c = (uint32_t)__shfl((int)cnt, l);
+      first_l = LANE == l ? code : first_l;
+      start_l = LANE == l ? start : start_l;
+      code = (code + c) << 1;
+      start += c;
+      if (l == root) nroot = (int)start;
     }
+  }
+  auto key_of = [&](int i, int l) -> int {   // (every lane calls it: the shuffles need all)
+    const uint32_t f = (uint32_t)__shfl((int)first_l, l), st = (uint32_t)__shfl((int)start_l, l);
+    return l ? (int)(__builtin_bitreverse32(f + (uint32_t)i - st) >> (32 - l)) : 0;
+  };
+  for (int c0 = 0; c0 < nroot; c0 += 64) {
+    const int i = c0 + LANE;
+    const int sy = i < nroot ? (int)sorted[i] : 0;
+    const int l = i < nroot ? (int)lens[sy] : 0;
+    const int k0 = key_of(i, l);
+    if (i < nroot)
+      for (int k = k0; k < tsize; k += 1 << l)
+        if (toff + k < cap) group[toff + k] = (l << 16) | sy;
+  }
+  int key = 0, sym = nroot, step = 1 << root;
+  if (nroot < nonzero) {   // the walk of the longer codes starts at the first of them
+    const int l = (int)lens[sorted[nroot]];
+    key = __builtin_amdgcn_readfirstlane(key_of(nroot, l));
   }
   wave_sync();
   int mask = total - 1, low = -1, cur = toff;
@@ -515,12 +571,39 @@ __device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, uint8_t 
   if (LANE == 0) table[32] = 0;
   wave_sync();
   build_table(s, table, kNoCap, 32, 5, cl_lens, 18);
+  // The reader's (acc, bo, ho) in registers and the 32-entry table in lanes (lane p: entry p):
+  // a symbol is a register shift and a readlane, not a chain of LDS round trips through the
+  // state (a metablock header of 24 literal and 4 command codes: 2.5 M cycles in here before).
+  const int tab = table[LANE & 31];
+  uint32_t acc = s.acc;
+  int bo = s.bo, ho = s.ho;
+  const uint8_t *win = s.l->win;
+  auto fill = [&]() {
+    if (bo >= 16) {
+      const uint32_t h = (ho >= 0 && ho < 2080) ? ((uint32_t)win[2 * ho] | ((uint32_t)win[2 * ho + 1] << 8)) : 0u;
+      ho++;
+      acc = (h << 16) | (acc >> 16);
+      bo -= 16;
+    }
+  };
+  int rc = 0;
   while (sym < nsym && space > 0) {
-    MAYBE_REFILL(s);
-    fill16(s);
-    int p = (int)(peek(s) & 31);
-    s.bo += table[p] >> 16;
-    int len = table[p] & 0xFFFF;
+    if (ho > 2030) {   // MAYBE_REFILL with the state written back around it
+      s.acc = acc;
+      s.bo = bo;
+      s.ho = ho;
+      wave_sync();
+      rc = read_more_input(s);
+      if (rc < 0) return rc;
+      acc = s.acc;
+      bo = s.bo;
+      ho = s.ho;
+    }
+    fill();
+    const int p = (int)((acc >> (bo & 31)) & 31);
+    const int e = __builtin_amdgcn_readlane(tab, p);
+    bo += e >> 16;
+    const int len = e & 0xFFFF;
     if (len < 16) {
       repeat = 0;
       if (LANE == 0) lens[sym] = (uint8_t)len;
@@ -530,26 +613,34 @@ __device__ int read_code_lengths(DecS &s, const int *cl_lens, int nsym, uint8_t 
         space -= 32768 >> len;
       }
     } else {
-      int eb = len - 14, new_len = len == 16 ? prev : 0;
+      const int eb = len - 14, new_len = len == 16 ? prev : 0;
       if (repeat_len != new_len) {
         repeat = 0;
         repeat_len = new_len;
       }
-      int old = repeat;
+      const int old = repeat;
       if (repeat > 0) {
         repeat -= 2;
         repeat <<= eb;
       }
-      fill16(s);
-      repeat += bits(s, eb) + 3;
-      int delta = repeat - old;
-      if (sym + delta > nsym) return ERR(s, -2);
+      fill();
+      repeat += (int)((acc >> (bo & 31)) & ((1u << eb) - 1u)) + 3;
+      bo += eb;
+      const int delta = repeat - old;
+      if (sym + delta > nsym) {
+        rc = ERR(s, -2);
+        break;
+      }
       for (int k = LANE; k < delta; k += 64) lens[sym + k] = (uint8_t)repeat_len;
       sym += delta;
       if (repeat_len) space -= delta << (15 - repeat_len);
     }
-    wave_sync();
   }
+  s.acc = acc;
+  s.bo = bo;
+  s.ho = ho;
+  wave_sync();
+  if (rc < 0) return rc;
   if (space != 0) return ERR(s, -18);
   for (int k = sym + LANE; k < nsym; k += 64) lens[k] = 0;
   wave_sync();
@@ -609,9 +700,15 @@ __device__ int read_huffman_code(DecS &s, int amax, int alimit, int32_t *group, 
     }
   }
   if (space != 0 && ncodes != 1) return ERR(s, -4);
+#ifdef MIB_PROF
+  unsigned long long ht0 = __builtin_amdgcn_s_memtime();
+#endif
   int r = read_code_lengths(s, cl, alimit, lens);
   if (r < 0) return r;
-  return build_table(s, group, cap, idx, 8, lens, alimit);
+  HMARK(7);
+  r = build_table(s, group, cap, idx, 8, lens, alimit);
+  HMARK(8);
+  return r;
 }
 
 __device__ int decode_var_len_byte(DecS &s) {
@@ -855,6 +952,9 @@ __device__ int decode_tree_group(DecS &s, int amax, int alimit, int n, int32_t *
 
 __device__ int read_codes_and_maps(DecS &s, int8_t *dist_extra, int32_t *dist_offset, int32_t *ctxmap_table) {
   int r;
+#ifdef MIB_PROF
+  unsigned long long ht0 = __builtin_amdgcn_s_memtime();
+#endif
   s.n_lit_types = decode_var_len_byte(s) + 1;
   if ((r = read_partition(s, 0, s.n_lit_types)) < 0) return r;
   s.lit_blen = r;
@@ -880,6 +980,7 @@ __device__ int read_codes_and_maps(DecS &s, int8_t *dist_extra, int32_t *dist_of
     MAYBE_REFILL(s);
   }
   int cml = s.n_lit_types << 6;
+  HMARK(0);
   if ((r = decode_context_map(s, cml, s.ctx_map, ctxmap_table)) < 0) return r;
   int nlit_trees = r;
   int nontrivial = 0;
@@ -888,16 +989,26 @@ __device__ int read_codes_and_maps(DecS &s, int8_t *dist_extra, int32_t *dist_of
   s.trivial_lit_ctx = __any(nontrivial) ? 0 : 1;
   if ((r = decode_context_map(s, s.n_dist_types << 2, s.dist_ctx_map, ctxmap_table)) < 0) return r;
   int ndist_trees = r;
+  HMARK(1);
   // groups live back to back: literal, command, distance.  A metablock with few prefix
   // codes (the common case: one tree per alphabet) gets them in LDS, so every symbol
   // lookup is an LDS read instead of a dependent HBM load.
   s.lit_group = s.tab_hbm;
   if ((r = decode_tree_group(s, 256, 256, nlit_trees, s.lit_group)) < 0) return r;
+  HMARK(2);
+#ifdef MIB_PROF
+  if (LANE == 0) {
+    atomicAdd(&g_hdr_prof[5], 1ull);
+    atomicAdd(&g_hdr_prof[6], (unsigned long long)nlit_trees);
+  }
+#endif
   s.cmd_group = s.lit_group + r;
   if ((r = decode_tree_group(s, 704, 704, s.n_cmd_types, s.cmd_group)) < 0) return r;
+  HMARK(3);
   s.dist_group = s.cmd_group + r;
   int dmax = 16 + s.ndirect + 2 * (24 << s.npostfix);
   if ((r = decode_tree_group(s, dmax, dmax, ndist_trees, s.dist_group)) < 0) return r;
+  HMARK(4);
   // tables that fit go to LDS as 16-bit entries, roots made absolute
   const int cmd_base = (int)(s.cmd_group - s.lit_group), dist_base = (int)(s.dist_group - s.lit_group);
   const int total = dist_base + r;
@@ -948,6 +1059,7 @@ __device__ int read_codes_and_maps(DecS &s, int8_t *dist_extra, int32_t *dist_of
   s.lit_tree_idx = 0;
   s.cmd_tree_idx = 0;
   s.rings[4] = 1; s.rings[5] = 0; s.rings[6] = 1; s.rings[7] = 0; s.rings[8] = 1; s.rings[9] = 0;
+  HMARK(9);
   return 0;
 }
 
@@ -1719,6 +1831,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   constexpr bool part = kPart;
   const int pstart = kPart ? U(s.part_start) : 0, cover_lo = kPart ? U(s.cover_lo) : 0;
   int pub_next = kPart ? U(s.pub_next) : 0x7FFFFFFF;
+  uint64_t *const prog_me = kPart ? s.prog + U(s.pidx) : nullptr;
   int plo = 0, phi = 0, pseen = 0;
   if (part) {
     plo = g_lds.part_lo[LANE];
@@ -1868,9 +1981,13 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     // ---- command boundary: a block switch or refill goes to the general loop
     if (mbl <= 0 || cmd_blen == 0 || ho_now() > 2030 - 8) break;
     if (part && pos >= pub_next) {   // every output byte below pos is stored: publish
+      // (inline: a call in this loop makes the compiler park SGPRs in VGPR lanes across it,
+      // part mode's commands ran 40 % slower than the serial decoder's on the same stream)
       finish_copy();
-      part_publish(pos);
-      pub_next = U(s.pub_next);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(prog_me, (uint64_t)pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pub_next = pos + (int)kPartPublish;
     }
     const int P0 = P, F0 = F;
     F = P;
@@ -2176,9 +2293,12 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
     if (part && src < pstart) {   // the source reaches into earlier parts: wait until they wrote it
       const int b = U(min(min(src + copy_len, pos), pstart));
       if (!part_ready_near(src, b, plo, phi, pseen, cover_lo)) {
-        finish_copy();
-        if (part_wait(src, b) < 0) return kPartFail;
-        pseen = g_lds.part_seen[lane];
+        // not yet known to be written: the general loop redoes the distance and waits (no
+        // call in this loop, above)
+        P = dP;
+        F = dF;
+        max_dist = dmax;
+        break;
       }
     }
     mbl -= insert_len;
@@ -2279,6 +2399,7 @@ __device__ __noinline__ int fast_loop(int fence_in, int rmask_in) {
   s.insert_len = insert_len; s.copy_len = copy_len; s.dist_code = dist_code; s.j = j;
   s.guard += 3ull * ncmd;
   s.running = phase;
+  if (kPart) s.pub_next = pub_next;
 #ifdef MIB_PROF
   if (lane == 0) {
     atomicAdd(&g_prof[14], (unsigned long long)ncmd);
@@ -2635,6 +2756,9 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
   // the literal context: the two bytes before the part, from the entry (ctx_byte); the
   // previous part's output is never written here, and it checks those bytes itself
   s.pctx = (int)e.p1 | ((int)e.p2 << 8);
+#ifdef MIB_PROF
+  if (lane == 0 && s.pidx_g < kPartProfMax) g_part_prof[8 * s.pidx_g + 5] = __builtin_amdgcn_s_memtime();
+#endif
   r = decompress(s, dist_extra, dist_offset, ctxmap_table);
   if (last) return (r == 1 && s.pos == (int)job.total) ? 0 : kPartFail;
   if (r != 3) return kPartFail;
@@ -2671,6 +2795,15 @@ __device__ int part_run(DecS &s, const DecJob &job, int8_t *dist_extra, int32_t 
 
 // Parts are taken in order from a ticket counter, so every part a wave may wait on has
 // already been taken by a running wave: a part only waits on earlier parts of its stream.
+// (Chunks of consecutive parts per XCD group were measured: C2 unchanged, C5 179 -> 679 ms,
+// profiles/r06/r06y3.)
+__device__ __forceinline__ int next_part(unsigned *ticket, int njobs) {
+  int jb = 0;
+  if (LANE == 0) jb = (int)atomicAdd(ticket, 1u);
+  jb = __shfl(jb, 0);
+  return jb < njobs ? jb : -1;
+}
+
 template <bool BIG>
 __global__ __launch_bounds__(64) void decode_parts_kernel(DecJob *jobs, int njobs, uint8_t *scratch, uint64_t per_block,
                                                           unsigned *ticket) {
@@ -2686,14 +2819,31 @@ __global__ __launch_bounds__(64) void decode_parts_kernel(DecJob *jobs, int njob
   int32_t *block_trees = BIG ? bt_lds : ctxmap_table + 1100;
   const int lane = threadIdx.x;
   for (;;) {
-    int jb = 0;
-    if (lane == 0) jb = (int)atomicAdd(ticket, 1u);
-    jb = __shfl(jb, 0);
-    if (jb >= njobs) break;
+    const int jb = next_part(ticket, njobs);
+    if (jb < 0) break;
     const DecJob job = jobs[jb];
     DecS &s = *(DecS *)&g_dec;
+#ifdef MIB_PROF
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
     dec_init(s, job, job.out, tables, ctx, block_trees, tab, tab_cap);
+#ifdef MIB_PROF
+    s.pidx_g = jb;
+    if (lane == 0 && jb < kPartProfMax) {
+      unsigned long long *q = g_part_prof + 8 * jb;
+      q[0] = t_start;
+      q[2] = q[3] = q[4] = 0;
+      unsigned hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      q[7] = hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(hw));
+      q[6] = (hw & 0xF) | ((unsigned long long)blockIdx.x << 8);
+    }
+#endif
     int rc = part_run(s, job, dist_extra, dist_offset, ctxmap_table);
+#ifdef MIB_PROF
+    if (lane == 0 && jb < kPartProfMax) g_part_prof[8 * jb + 1] = __builtin_amdgcn_s_memtime();
+#endif
     if (rc == 0) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!job.next_entry) part_publish(0x7FFFFFFF);
@@ -2756,6 +2906,16 @@ extern "C" hipError_t mib_decode_peek_heads(const uint8_t *d_in, const uint64_t 
 }
 
 #ifdef MIB_PROF
+extern "C" int mib_debug_read_hdr_prof(unsigned long long *out) {
+  hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_hdr_prof), sizeof(unsigned long long) * 16);
+  unsigned long long z[16] = {0};
+  hipMemcpyToSymbol(HIP_SYMBOL(mib::g_hdr_prof), z, sizeof(z));
+  return 0;
+}
+extern "C" int mib_debug_read_part_prof(unsigned long long *out, int n) {
+  if (n > mib::kPartProfMax) n = mib::kPartProfMax;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_part_prof), sizeof(unsigned long long) * 8 * n);
+}
 extern "C" int mib_debug_read_prof(unsigned long long *out) {
   hipMemcpyFromSymbol(out, HIP_SYMBOL(mib::g_prof), sizeof(unsigned long long) * 16);
   unsigned long long z[16] = {0};

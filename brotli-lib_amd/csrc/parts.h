@@ -29,7 +29,10 @@ constexpr uint32_t kPartMagic = 0x3170424Du;     // "MBp1"
 constexpr uint32_t kPartBits = 18;               // part size: 256 KiB (a multiple of the encoder's 64 KiB parse segment)
 constexpr uint32_t kPartLag = 4096;              // an external copy source ends this far behind
                                                  // the destination's offset in its segment
-constexpr uint32_t kPartPublish = 2048;          // a part publishes its progress this often (bytes)
+#ifndef MIB_PART_PUBLISH
+#define MIB_PART_PUBLISH 2048
+#endif
+constexpr uint32_t kPartPublish = MIB_PART_PUBLISH;   // a part publishes its progress this often (bytes)
 constexpr uint64_t kPartMinStream = 2ull << 20;  // streams at least this long get a part index
 
 constexpr uint32_t kPartValid = 1u;              // entry flags

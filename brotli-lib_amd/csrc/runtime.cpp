@@ -994,7 +994,8 @@ static int decode_parts(mib_ctx *c, const std::vector<PartStream> &ps, std::vect
   }
   uint64_t per_block = mib::kDecodeTableInts * 4 + mib::kDecodeCtxBytes + 1152 + 1152 * 4 + 1100 * 4 + 3092 * 4;
   per_block = (per_block + 255) & ~(uint64_t)255;
-  const int grid = (int)std::min<size_t>(nj, 2048);
+  static const size_t grid_cap = mib::knob("MIB_PART_GRID") ? (size_t)std::max(1, atoi(mib::knob("MIB_PART_GRID"))) : 2048;
+  const int grid = (int)std::min<size_t>(nj, grid_cap);
   c->scratch_trim.need = std::max(c->scratch_trim.need, per_block * (uint64_t)grid);
   if ((rc = grow((void **)&c->d_scratch, &c->scratch_bytes, per_block * (uint64_t)grid)) != 0) return rc;
   if (nj > c->jobs_cap) {
