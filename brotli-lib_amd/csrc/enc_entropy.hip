@@ -285,20 +285,22 @@ __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *s
 
 // ---------------------------------------------------------------- histograms by block type
 // Block per segment, after the split: literal histograms per (block type, context), command
-// histograms per block type, distance-code histograms per (block type, distance context),
-// accumulated in LDS (literals one block type at a time) and added to the metablock's with
-// one global atomic per non-zero bin (the histogram pass of storeMetaBlock, metablock.ts:580-640).
+// histograms per block type, distance-code histograms per (block type, distance context):
+// accumulated in LDS (literals: the segment's major block type; the others by global
+// atomics) and added to the metablock's with one global atomic per non-zero bin (the
+// histogram pass of storeMetaBlock, metablock.ts:580-640).
 template <int NT>
 __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Unit *units, uint32_t *hl,
                                                        uint32_t *hc, uint32_t *hd) {
-  typedef hipcub::BlockScan<uint32_t, NT> Scan;
-  __shared__ typename Scan::TempStorage scan_tmp;
-  __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
+  __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then the major literal type's
   __shared__ uint8_t ut[kSubPerSeg][3];
-  __shared__ ItemMap<NT> map;
-  __shared__ uint32_t sh_pos[NT], sh_ins[NT];
+  __shared__ int sh_major;
   uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
+  struct LitRows {
+    uint32_t off[64], pos[64];
+  };
+  __shared__ LitRows lit_rows[NT / 64];
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
@@ -308,6 +310,21 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
   for (int i = t; i < 512; i += NT) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
+  if (t == 64) {   // the literal block type with the most literals in this segment (its histogram in LDS)
+    uint32_t best = 0;
+    int major = 0;
+#pragma unroll
+    for (int ty = 0; ty < kMaxBT; ty++) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int u = 0; u < kSubPerSeg; u++) c += un[u].type[0] == ty ? un[u].nsym[0] : 0u;
+      if (c > best) {
+        best = c;
+        major = ty;
+      }
+    }
+    sh_major = major;
+  }
   for (int i = t; i < (int)mb.nbt[1] * 704; i += NT) sh_c[i] = 0;
   for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT) sh_d[i] = 0;
   __syncthreads();
@@ -326,59 +343,55 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
     if (sh_c[i]) atomicAdd(&hc[(size_t)m * kMaxBT * 704 + i], sh_c[i]);
   for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT)
     if (sh_d[i]) atomicAdd(&hd[(size_t)m * kMaxBT * kDistCtx * 128 + i], sh_d[i]);
+  // The literals, every one once whatever its block type: a wave per 64 commands (no block
+  // barrier), the inserts' offsets by a wave prefix sum in the wave's LDS rows, each lane's
+  // literal found by a six-step search over them.  The segment's major type (most literals)
+  // counts in the LDS histogram, flushed once; a literal of another type goes to the
+  // metablock's histogram by a global atomic.  (It was a pass over all commands per block type
+  // present, with block scans, and the LDS histogram zeroed and flushed per type; every literal
+  // by a global atomic instead slowed the other encode lane's kernels: C4 encode -2.3 %.)
   __syncthreads();
-  uint32_t present = 0;   // literal block types used by this segment
-  for (int u = 0; u < kSubPerSeg; u++) present |= 1u << ut[u][0];
-  for (int ty = 0; ty < kMaxBT; ty++) {
-    if (!(present >> ty & 1)) continue;
-    for (int i = t; i < kLitCtx * 256; i += NT) sh_l[i] = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < n; base += NT) {   // the literals of this type, spread over the lanes
-      const uint32_t q = base + t, nb = min((uint32_t)NT, n - base);
-      uint32_t cnt = 0;
-      if (q < n && c[q].ins) {   // the command's literals that lie in units of this type
-        const uint32_t pos = cp[q], ins = c[q].ins;
-        sh_pos[t] = pos;
-        sh_ins[t] = ins;
-        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
-        for (uint32_t v = ulo; v <= uhi; v++)
-          if (ut[v][0] == ty) {
-            const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
-            const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
-            cnt += s1 - s0;
-          }
-      }
-      uint32_t off, nlits;
-      Scan(scan_tmp).ExclusiveSum(cnt, off, nlits);
-      map.off[t] = off;
-      if (t == 0) map.off[nb] = nlits;
-      __syncthreads();
-      for (uint32_t i = t; i < nlits; i += NT) {
-        const uint32_t j = map.find(i, nb);
-        // the (i - off)-th of command j's literals in type-ty units (an insert spans few units)
-        const uint32_t pos = sh_pos[j], ins = sh_ins[j];
-        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
-        uint32_t k = i - map.off[j], lp = pos;
-        for (uint32_t v = ulo; v <= uhi; v++) {
-          if (ut[v][0] != ty) continue;
-          const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
-          const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
-          if (k < s1 - s0) {
-            lp = s0 + k;
-            break;
-          }
-          k -= s1 - s0;
-        }
-        const uint32_t p12 = prev2(jb, lp);
-        atomicAdd(&sh_l[(lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp]], 1u);
-      }
-      __syncthreads();
+  for (int i = t; i < kLitCtx * 256; i += NT) sh_l[i] = 0;
+  __syncthreads();
+  const int major = sh_major;
+  uint32_t *hm = hl + (size_t)m * kLitSlots * 256;
+  const int w = t >> 6, ln = t & 63;
+  LitRows &rw = lit_rows[w];
+  for (uint32_t base = (uint32_t)w * 64; base < n; base += NT) {
+    const uint32_t q = base + ln;
+    uint32_t ins = 0, pos = 0;
+    if (q < n) {
+      ins = c[q].ins;
+      pos = cp[q];
     }
-    uint32_t *dst = hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256;
-    for (int i = t; i < kLitCtx * 256; i += NT)
-      if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
-    __syncthreads();
+    uint32_t x = ins;   // inclusive prefix sum over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 64);
+      if (ln >= o) x += y;
+    }
+    const uint32_t nl = __shfl(x, 63, 64);
+    rw.off[ln] = x - ins;
+    rw.pos[ln] = pos;
+    wave_sync();
+    for (uint32_t i = ln; i < nl; i += 64) {
+      uint32_t j = 0;   // the last command whose offset is <= i (the one owning literal i)
+#pragma unroll
+      for (int s = 32; s; s >>= 1)
+        if (rw.off[j + s] <= i) j += s;
+      const uint32_t lp = rw.pos[j] + i - rw.off[j];
+      const uint32_t p12 = prev2(jb, lp);
+      const int ty = ut[unit_of(sg, lp)][0];
+      const uint32_t bin = (lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp];
+      if (ty == major) atomicAdd(&sh_l[bin], 1u);
+      else atomicAdd(&hm[ty * kLitCtx * 256 + bin], 1u);
+    }
+    wave_sync();   // (the rows are rewritten by the next batch)
   }
+  __syncthreads();
+  uint32_t *dst = hm + major * kLitCtx * 256;
+  for (int i = t; i < kLitCtx * 256; i += NT)
+    if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
 }
 
 // ---------------------------------------------------------------- clustering

@@ -726,9 +726,14 @@ __global__ __launch_bounds__(64 * kDpWaves, KS == 4 ? MIB_DP_OCC_KS4 : (KC && KS
 // ---------------------------------------------------------------- 4. backtrack, wave per segment
 // computeShortestPathFromNodes / createCommandsFromPath (backward-references-hq.ts:384-406,
 // 610-673) without the distance ring: that is stitched per segment in enc_entropy.hip.
-// The path is walked from the segment end in windows of 64 positions: one coalesced load
-// of the window's choices, a ballot of its copy nodes, then a scalar walk that skips each
-// literal run with a bit scan and each copy with its length.
+// The path is walked from the segment end in windows of 64 positions: a ballot of the
+// window's copy nodes, then a scalar walk that skips each literal run with a bit scan and each
+// copy with its length.  The windows are aligned to the segment end and loaded four at a time
+// (a chunk of 256 positions), the next chunk in flight while this one is walked; the commands
+// gather in lanes (lane k: the k-th of a batch) and are stored 64 at a time.  (A load per
+// window issued when the walk reached it, and a store per command from lane 0, left the wave
+// waiting on every window: C4 backtrack 2.7 ms a launch.)
+constexpr int kBtWin = 4;   // windows per chunk
 __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *segs, int nsegs, const uint64_t *choice,
                                                        RawCmd *raw) {
   const int s = blockIdx.x;
@@ -743,58 +748,97 @@ __global__ __launch_bounds__(64) void backtrack_kernel(const Job *jobs, Seg *seg
   uint32_t cur = sg.end, lits = 0, tail = 0;
   bool seen_copy = false;
   uint32_t pend_len = 0, pend_dist = 0, last_dist = 0;
+  // the batch of commands in lanes: lane k holds the k-th, stored at w - 1 - k
+  uint32_t bi = 0, bl = 0, bd = 0;
+  int nb = 0;
+  auto put = [&](uint32_t ins, uint32_t len, uint32_t dist) {
+    bi = lane == nb ? ins : bi;
+    bl = lane == nb ? len : bl;
+    bd = lane == nb ? dist : bd;
+    if (++nb == 64) {
+      RawCmd &o = out[w - 1 - lane];
+      o.ins = bi;
+      o.len = bl;
+      o.dist = bd;
+      w -= 64;
+      nb = 0;
+    }
+  };
+  auto load_chunk = [&](uint32_t top, uint64_t (&v)[kBtWin]) {   // windows top, top - 64, ...
+#pragma unroll
+    for (int j = 0; j < kBtWin; j++) {
+      const uint32_t p = top - 64u * j - lane;
+      v[j] = (top > 64u * j + lane && p > a) ? c[p] : 0ull;
+    }
+  };
+  uint32_t hi = sg.end;   // the chunk's top
+  uint64_t va[kBtWin], vb[kBtWin];
+  load_chunk(hi, va);
+  load_chunk(hi - min(hi, 64u * kBtWin), vb);
   while (cur > a) {
-    const uint32_t nvalid = min(64u, cur - a);
-    const uint32_t p = cur - lane;
-    uint64_t v = 0;
-    if ((uint32_t)lane < nvalid) v = c[p];
-    uint32_t len = (uint32_t)v;
-    if ((uint32_t)lane >= nvalid || len > p - a) len = 0;   // a literal is always a valid edge
-    const uint32_t dist = (uint32_t)(v >> 32);
-    const uint64_t copies = __ballot(len != 0);
-    uint32_t x = 0;
-    for (;;) {
-      const uint64_t rest = x < 64 ? (copies >> x) : 0ull;
-      const uint32_t y = rest ? x + (uint32_t)(__ffsll((unsigned long long)rest) - 1) : nvalid;
-      if (y >= nvalid) {   // literals to the window's end
-        lits += nvalid - x;
-        cur -= nvalid;
-        break;
-      }
-      lits += y - x;
-      const uint32_t L = __builtin_amdgcn_readlane(len, y);
-      const uint32_t D = __builtin_amdgcn_readlane(dist, y);
-      if (!seen_copy) {
-        tail = lits;
-        seen_copy = true;
-        last_dist = D;
-      } else {
-        w--;
-        if (lane == 0) {
-          out[w].ins = lits;
-          out[w].len = pend_len;
-          out[w].dist = pend_dist;
+#pragma unroll
+    for (int j = 0; j < kBtWin; j++) {
+      const uint32_t wtop = hi - 64u * j;
+      // (the walk may have jumped past this window, or reached the segment start)
+      if (cur > a && cur + 64u > wtop) {
+        const uint32_t nvalid = min(64u, wtop - a);
+        const uint32_t p = wtop - lane;
+        const uint64_t v = va[j];
+        uint32_t len = (uint32_t)v;
+        if ((uint32_t)lane >= nvalid || len > p - a) len = 0;   // a literal is always a valid edge
+        const uint32_t dist = (uint32_t)(v >> 32);
+        const uint64_t copies = __ballot(len != 0);
+        uint32_t x = wtop - cur;
+        for (;;) {
+          const uint64_t rest = x < 64 ? (copies >> x) : 0ull;
+          const uint32_t y = rest ? x + (uint32_t)(__ffsll((unsigned long long)rest) - 1) : nvalid;
+          if (y >= nvalid) {   // literals to the window's end
+            lits += nvalid - x;
+            cur = wtop - nvalid;
+            break;
+          }
+          lits += y - x;
+          const uint32_t L = __builtin_amdgcn_readlane(len, y);
+          const uint32_t D = __builtin_amdgcn_readlane(dist, y);
+          if (!seen_copy) {
+            tail = lits;
+            seen_copy = true;
+            last_dist = D;
+          } else {
+            put(lits, pend_len, pend_dist);
+          }
+          lits = 0;
+          pend_len = L;
+          pend_dist = D;
+          x = y + L;
+          if (x >= nvalid) {
+            cur = wtop - x;
+            break;
+          }
         }
       }
-      lits = 0;
-      pend_len = L;
-      pend_dist = D;
-      x = y + L;
-      if (x >= nvalid) {
-        cur -= x;
-        break;
-      }
     }
+    if (cur <= a) break;
+    hi -= 64u * kBtWin;
+    if (cur + 64u * kBtWin <= hi) {   // a long copy jumped past the next chunk: reload at cur
+      hi = sg.end - ((sg.end - cur) / (64u * kBtWin)) * (64u * kBtWin);
+      load_chunk(hi, va);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kBtWin; j++) va[j] = vb[j];
+    }
+    load_chunk(hi - min(hi, 64u * kBtWin), vb);
   }
-  if (seen_copy) {
-    if (lane == 0) {
-      out[w - 1].ins = lits;
-      out[w - 1].len = pend_len;
-      out[w - 1].dist = pend_dist;
+  if (seen_copy) put(lits, pend_len, pend_dist);
+  else tail = lits;
+  if (nb) {   // the last, partial batch
+    if (lane < nb) {
+      RawCmd &o = out[w - 1 - lane];
+      o.ins = bi;
+      o.len = bl;
+      o.dist = bd;
     }
-    w--;
-  } else {
-    tail = lits;
+    w -= nb;
   }
   const uint32_t n = cap - w;
   wave_sync();
