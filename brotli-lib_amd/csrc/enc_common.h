@@ -59,7 +59,7 @@ constexpr int kCmdSlot = kLitSlots;
 constexpr int kDistSlot = kCmdSlot + kMaxBT;
 constexpr int kTreeSlots = kDistSlot + kMaxBT * kDistCtx;
 constexpr int kBlock = 256;                   // threads of the per-segment entropy / emit blocks
-constexpr int kMaxPieceShift = 6;             // parse pieces per segment: at most 2^6 (encode.hip)
+constexpr int kMaxPieceShift = 7;             // parse pieces per segment: at most 2^7 (encode.hip)
 // a segment's commands fill at most kSeg / 2 + 4 + (2 << kMaxPieceShift) slots (its cmds span,
 // encode.hip); sizes_kernel records their bits per tile of kEmitTile commands, so emit_kernel
 // can write a segment's tiles from blocks of their own

@@ -286,16 +286,15 @@ __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *s
 // ---------------------------------------------------------------- histograms by block type
 // Block per segment, after the split: literal histograms per (block type, context), command
 // histograms per block type, distance-code histograms per (block type, distance context):
-// accumulated in LDS (literals: the segment's major block type; the others by global
-// atomics) and added to the metablock's with one global atomic per non-zero bin (the
-// histogram pass of storeMetaBlock, metablock.ts:580-640).
+// accumulated in LDS (literals one block type at a time) and added to the metablock's with
+// one global atomic per non-zero bin (the histogram pass of storeMetaBlock, metablock.ts:580-640).
 template <int NT>
 __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Unit *units, uint32_t *hl,
                                                        uint32_t *hc, uint32_t *hd) {
-  __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then the major literal type's
+  __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
   __shared__ uint8_t ut[kSubPerSeg][3];
-  __shared__ int sh_major;
+  __shared__ uint32_t sh_present;
   uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
   struct LitRows {
     uint32_t off[64], pos[64];
@@ -310,20 +309,11 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
   for (int i = t; i < 512; i += NT) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
-  if (t == 64) {   // the literal block type with the most literals in this segment (its histogram in LDS)
-    uint32_t best = 0;
-    int major = 0;
+  if (t == 64) {   // the literal block types this segment's literals fall in
+    uint32_t present = 0;
 #pragma unroll
-    for (int ty = 0; ty < kMaxBT; ty++) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int u = 0; u < kSubPerSeg; u++) c += un[u].type[0] == ty ? un[u].nsym[0] : 0u;
-      if (c > best) {
-        best = c;
-        major = ty;
-      }
-    }
-    sh_major = major;
+    for (int u = 0; u < kSubPerSeg; u++) present |= un[u].nsym[0] ? 1u << un[u].type[0] : 0u;
+    sh_present = present;
   }
   for (int i = t; i < (int)mb.nbt[1] * 704; i += NT) sh_c[i] = 0;
   for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT) sh_d[i] = 0;
@@ -343,55 +333,57 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
     if (sh_c[i]) atomicAdd(&hc[(size_t)m * kMaxBT * 704 + i], sh_c[i]);
   for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT)
     if (sh_d[i]) atomicAdd(&hd[(size_t)m * kMaxBT * kDistCtx * 128 + i], sh_d[i]);
-  // The literals, every one once whatever its block type: a wave per 64 commands (no block
-  // barrier), the inserts' offsets by a wave prefix sum in the wave's LDS rows, each lane's
-  // literal found by a six-step search over them.  The segment's major type (most literals)
-  // counts in the LDS histogram, flushed once; a literal of another type goes to the
-  // metablock's histogram by a global atomic.  (It was a pass over all commands per block type
-  // present, with block scans, and the LDS histogram zeroed and flushed per type; every literal
-  // by a global atomic instead slowed the other encode lane's kernels: C4 encode -2.3 %.)
-  __syncthreads();
-  for (int i = t; i < kLitCtx * 256; i += NT) sh_l[i] = 0;
-  __syncthreads();
-  const int major = sh_major;
+  // The literals, a pass per block type present (its histogram in LDS, flushed with one global
+  // atomic per non-zero bin): a wave per 64 commands (no block barrier), the inserts' offsets by
+  // a wave prefix sum in the wave's LDS rows, each lane's literal found by a six-step search
+  // over them and counted when its unit is of the pass's type.  (The passes used block scans
+  // before, a barrier per 1,024 commands.  Every literal by a global atomic instead slowed the
+  // other encode lane's kernels, C4 encode -2.3 %, and serialised on 16 MiB metablocks' hot
+  // bins, C2 type_histo 0.24 -> 0.70 ms.)
   uint32_t *hm = hl + (size_t)m * kLitSlots * 256;
   const int w = t >> 6, ln = t & 63;
   LitRows &rw = lit_rows[w];
-  for (uint32_t base = (uint32_t)w * 64; base < n; base += NT) {
-    const uint32_t q = base + ln;
-    uint32_t ins = 0, pos = 0;
-    if (q < n) {
-      ins = c[q].ins;
-      pos = cp[q];
-    }
-    uint32_t x = ins;   // inclusive prefix sum over the wave
+  const uint32_t present = sh_present;
+  for (int ty = 0; ty < kMaxBT; ty++) {
+    if (!(present >> ty & 1)) continue;
+    __syncthreads();
+    for (int i = t; i < kLitCtx * 256; i += NT) sh_l[i] = 0;
+    __syncthreads();
+    for (uint32_t base = (uint32_t)w * 64; base < n; base += NT) {
+      const uint32_t q = base + ln;
+      uint32_t ins = 0, pos = 0;
+      if (q < n) {
+        ins = c[q].ins;
+        pos = cp[q];
+      }
+      uint32_t x = ins;   // inclusive prefix sum over the wave
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if (ln >= o) x += y;
-    }
-    const uint32_t nl = __shfl(x, 63, 64);
-    rw.off[ln] = x - ins;
-    rw.pos[ln] = pos;
-    wave_sync();
-    for (uint32_t i = ln; i < nl; i += 64) {
-      uint32_t j = 0;   // the last command whose offset is <= i (the one owning literal i)
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (ln >= o) x += y;
+      }
+      const uint32_t nl = __shfl(x, 63, 64);
+      rw.off[ln] = x - ins;
+      rw.pos[ln] = pos;
+      wave_sync();
+      for (uint32_t i = ln; i < nl; i += 64) {
+        uint32_t j = 0;   // the last command whose offset is <= i (the one owning literal i)
 #pragma unroll
-      for (int s = 32; s; s >>= 1)
-        if (rw.off[j + s] <= i) j += s;
-      const uint32_t lp = rw.pos[j] + i - rw.off[j];
-      const uint32_t p12 = prev2(jb, lp);
-      const int ty = ut[unit_of(sg, lp)][0];
-      const uint32_t bin = (lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp];
-      if (ty == major) atomicAdd(&sh_l[bin], 1u);
-      else atomicAdd(&hm[ty * kLitCtx * 256 + bin], 1u);
+        for (int s = 32; s; s >>= 1)
+          if (rw.off[j + s] <= i) j += s;
+        const uint32_t lp = rw.pos[j] + i - rw.off[j];
+        if (ut[unit_of(sg, lp)][0] == ty) {
+          const uint32_t p12 = prev2(jb, lp);
+          atomicAdd(&sh_l[(lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp]], 1u);
+        }
+      }
+      wave_sync();   // (the rows are rewritten by the next batch)
     }
-    wave_sync();   // (the rows are rewritten by the next batch)
+    __syncthreads();
+    uint32_t *dst = hm + ty * kLitCtx * 256;
+    for (int i = t; i < kLitCtx * 256; i += NT)
+      if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
   }
-  __syncthreads();
-  uint32_t *dst = hm + major * kLitCtx * 256;
-  for (int i = t; i < kLitCtx * 256; i += NT)
-    if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
 }
 
 // ---------------------------------------------------------------- clustering
@@ -1774,6 +1766,13 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
   // the refinement: S-wide loops and unit-cost rows
   auto refine = [&]() -> int {
     float base_cost = 0.f;
+    constexpr int kRowK = (704 + 63) / 64;
+    const int lx = t & 63;
+    auto load_row = [&](int i, uint32_t (&v)[kRowK]) {
+      const uint32_t *h = H + (size_t)i * kSubHist;
+#pragma unroll
+      for (int k = 0; k < kRowK; k++) v[k] = (i < nu && ns[i] && lx + 64 * k < A) ? h[lx + 64 * k] : 0u;
+    };
     for (int it = 0; it <= kSplitIters; it++) {
       // type histograms (it == kSplitIters: of the final assignment); one type = all units.
       // NT / 256 unit ranges in parallel (256 symbols each), summed with LDS atomics
@@ -1781,34 +1780,55 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
         for (int q = 0; q < S; q++) th[q][x] = 0;
       __syncthreads();
       {
-        const int qd = t >> 8, i0 = (nu * qd) / (kSplitT / 256), i1 = (nu * (qd + 1)) / (kSplitT / 256);
-        for (int x = t & 255; x < A; x += 256) {
-          uint32_t s[S];
+        // a thread per (unit range, four symbols): 16-byte row loads, eight rows a batch issued
+        // together (a load-use pair per row left one HBM/L2 round trip per row in flight; 4-byte
+        // loads kept the block's few waves waiting on the latency: C2's 16 MiB metablocks read
+        // each 704-wide command row 2,048 times an iteration)
+        constexpr int kV = S <= 4 ? 4 : 2;   // symbols a thread (registers: kV x S sums)
+        typedef typename std::conditional<kV == 4, uint4, uint2>::type VT;
+        auto vget = [](const VT &v, int k) -> uint32_t {
+          if constexpr (kV == 4) return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+          else return k == 0 ? v.x : v.y;
+        };
+        const int ng = (A + kV - 1) / kV, nr = max(1, kSplitT / ng);
+        const int qd = t / ng, g = t % ng;
+        if (qd < nr) {
+          const int i0 = (nu * qd) / nr, i1 = (nu * (qd + 1)) / nr;
+          uint32_t s[kV][S];
 #pragma unroll
-          for (int q = 0; q < S; q++) s[q] = 0;
-          // eight unit rows a batch: the loads issued together, then summed (a load-use pair per
-          // row left one HBM/L2 round trip per row in flight)
+          for (int k = 0; k < kV; k++)
+#pragma unroll
+            for (int q = 0; q < S; q++) s[k][q] = 0;
+          const VT *hrow = reinterpret_cast<const VT *>(H + kV * g);   // (rows and the category's offset are 16-byte aligned)
+          constexpr uint32_t kRowV = kSubHist / kV;
           int i = i0;
           for (; i + 8 <= i1; i += 8) {
-            uint32_t v[8];
+            VT v[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) v[j] = H[(size_t)(i + j) * kSubHist + x];
+            for (int j = 0; j < 8; j++) v[j] = hrow[(size_t)(i + j) * kRowV];
 #pragma unroll
             for (int j = 0; j < 8; j++) {
               const int a = asg[i + j];
 #pragma unroll
-              for (int q = 0; q < S; q++) s[q] += a == q ? v[j] : 0u;
+              for (int k = 0; k < kV; k++)
+#pragma unroll
+                for (int q = 0; q < S; q++) s[k][q] += a == q ? vget(v[j], k) : 0u;
             }
           }
           for (; i < i1; i++) {
-            const uint32_t v = H[(size_t)i * kSubHist + x];
+            const VT v = hrow[(size_t)i * kRowV];
             const int a = asg[i];
 #pragma unroll
-            for (int q = 0; q < S; q++) s[q] += a == q ? v : 0u;
+            for (int k = 0; k < kV; k++)
+#pragma unroll
+              for (int q = 0; q < S; q++) s[k][q] += a == q ? vget(v, k) : 0u;
           }
 #pragma unroll
-          for (int q = 0; q < S; q++)
-            if (s[q]) atomicAdd(&th[q][x], s[q]);
+          for (int k = 0; k < kV; k++)
+            if (kV * g + k < A)
+#pragma unroll
+              for (int q = 0; q < S; q++)
+                if (s[k][q]) atomicAdd(&th[q][kV * g + k], s[k][q]);
         }
       }
       __syncthreads();
@@ -1848,24 +1868,33 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       SPMARK(3);
       if (it == kSplitIters) break;
       // every unit's bits under every type: a wave per unit, lanes over the symbols
+      // (the unit's row is loaded whole, one unit ahead -- up to 22 loads a lane in flight; the
+      // sums in the same order as ever)
+      uint32_t rv[kRowK], rn[kRowK];
+      load_row(t >> 6, rv);
       for (int i = t >> 6; i < nu; i += kSplitT / 64) {
+        load_row(i + kSplitT / 64, rn);   // the wave's next unit, in flight while this one is summed
         float c[S];
 #pragma unroll
         for (int q = 0; q < S; q++) c[q] = 0.f;
         if (ns[i]) {
-          const uint32_t *h = H + (size_t)i * kSubHist;
-#pragma unroll 4
-          for (int x = t & 63; x < A; x += 64) {
-            const float v = (float)h[x];
 #pragma unroll
-            for (int q = 0; q < S; q++) c[q] += v * bc[q][x];
+          for (int k = 0; k < kRowK; k++) {
+            const int x = lx + 64 * k;
+            if (x < A) {
+              const float v = (float)rv[k];
+#pragma unroll
+              for (int q = 0; q < S; q++) c[q] += v * bc[q][x];
+            }
           }
 #pragma unroll
           for (int q = 0; q < S; q++)
             for (int o = 32; o; o >>= 1) c[q] += __shfl_xor(c[q], o);
         }
-        if ((t & 63) == 0)
+        if (lx == 0)
           for (int q = 0; q < S; q++) ucost[i * S + q] = q < K ? c[q] : 1e30f;   // (types past K: empty)
+#pragma unroll
+        for (int k = 0; k < kRowK; k++) rv[k] = rn[k];
       }
       __syncthreads();
       SPMARK(4);
@@ -1884,11 +1913,20 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
     }
     // the split's cost: unit bits under the final histograms, switches, one code header per type
     float part = 0.f;   // (the first 256 threads, in the same grouping as ever: identical sums)
-    for (int i = t >> 6; t < 256 && i < nu; i += 4) {
-      if (!ns[i]) continue;
-      const uint32_t *h = H + (size_t)i * kSubHist;
-      const int q = asg[i];
-      for (int x = t & 63; x < A; x += 64) part += (float)h[x] * bc[q][x];
+    if (t < 256) {
+      uint32_t fv[kRowK], fn[kRowK];
+      load_row(t >> 6, fv);
+      for (int i = t >> 6; i < nu; i += 4) {
+        load_row(i + 4, fn);
+        if (ns[i]) {
+          const int q = asg[i];
+#pragma unroll
+          for (int k = 0; k < kRowK; k++)
+            if (lx + 64 * k < A) part += (float)fv[k] * bc[q][lx + 64 * k];
+        }
+#pragma unroll
+        for (int k = 0; k < kRowK; k++) fv[k] = fn[k];
+      }
     }
     for (int x = t; t < 256 && x < A; x += 256)
       for (int q = 0; q < S; q++) part += th[q][x] ? 3.5f : 0.f;

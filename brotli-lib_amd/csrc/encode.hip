@@ -249,16 +249,17 @@ Params make_params(const mib_enc_opts *o) {
 constexpr uint64_t kSmallStream = 1ull << 20;
 // Pieces per segment (2^shift) by the stream itself, so a stream parses the same in any batch:
 // 8 KiB pieces; 2 KiB for one-shot streams below 1 MiB -- a lone small stream gets 512 DP waves
-// per MiB instead of 128 --, 1 KiB for one-shot streams of one segment and for streaming chunks
-// of up to 4 MiB (a reference-cadence
+// per MiB instead of 128 --, 1 KiB for one-shot streams of one segment, 512 B for streaming
+// chunks of up to 4 MiB (a reference-cadence
 // update()'s 1 MiB chunk: its parse was 4.7 of the 9.2 ms an update took with 8 KiB pieces,
-// r05m, 1.2 ms with 2 KiB, r05n; 1 KiB: 205 -> 227 MB/s for 0.38309 -> 0.38317, r05ad).  C4's
+// r05m, 1.2 ms with 2 KiB, r05n; 1 KiB: 205 -> 227 MB/s for 0.38309 -> 0.38317, r05ad; 512 B:
+// 330 -> 353 MB/s for 0.38326 -> 0.38341, r06 kn_pieces: two DP waves a SIMD).  C4's
 // 1 MiB buffers keep 8 KiB pieces (2 KiB: 0.36296 vs 0.36281, r05n).  (MIB_DP_PIECES, experiment
 // builds: one shift for every stream.)
 int dp_piece_shift(uint64_t n, bool streaming) {
   static const int v = knob("MIB_DP_PIECES") ? std::min(kMaxPieceShift, std::max(0, atoi(knob("MIB_DP_PIECES")))) : -1;
   if (v >= 0) return v;
-  if (streaming) return n <= 4 * kSmallStream ? 6 : 3;
+  if (streaming) return n <= 4 * kSmallStream ? 7 : 3;
   return n <= kSeg ? 6 : n < kSmallStream ? 5 : 3;   // (one segment: C1's 45,000 B, 3.65 -> 3.14 ms for +0.06 %, r05af)
 }
 bool rep_pass(const Params &p) {
