@@ -561,7 +561,8 @@ void launch_ring_scan(hipStream_t st, Job *jobs, int njobs, Seg *segs, int nsegs
 void launch_part_index(hipStream_t st, const Job *jobs, int njobs, const Mb *mbs, const Seg *segs, int nsegs,
                        const Cmd *cmds, const Unit *units, PushSum *push, uint8_t *out);
 size_t part_push_bytes();
-void launch_pack(hipStream_t st, const Job *jobs, int njobs, const uint64_t *dst_off, const uint8_t *src, uint8_t *dst);
+void launch_pack(hipStream_t st, const Job *jobs, int njobs, uint64_t out_pos, uint64_t out_cap, uint64_t *dst_off,
+                 const uint8_t *src, uint8_t *dst);
 
 }  // namespace enc
 }  // namespace mib

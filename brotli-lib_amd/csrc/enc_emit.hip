@@ -394,7 +394,40 @@ __global__ void uncompressed_kernel(Job *jobs, int njobs, uint8_t *out) {
 }
 
 // pack the per-job output slices back to back
-__global__ void pack_kernel(const Job *jobs, const uint64_t *dst_off, const uint8_t *src, uint8_t *dst) {
+// Each stream's place in the packed output (dst_off[0..k]: out_pos, then its sizes summed) and
+// the call's status in dst_off[k + 1]: 0, or a stream's bytes past its scratch slot / the packed
+// output past out_cap (then nothing is packed).  One block; the host reads it all back with
+// the jobs after the pack (it used to read the jobs, sum on the host and upload the offsets
+// before the pack: a host round trip per call, ~50 us of a cadence update()).
+__global__ __launch_bounds__(1024) void dst_off_kernel(const Job *jobs, int k, uint64_t out_pos, uint64_t out_cap,
+                                                        uint64_t *dst_off) {
+  typedef hipcub::BlockScan<uint64_t, 1024> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  __shared__ int bad;
+  const int t = threadIdx.x, per = (k + 1023) / 1024, lo = min(k, t * per), hi = min(k, lo + per);
+  if (t == 0) bad = 0;
+  __syncthreads();
+  uint64_t sum = 0;
+  for (int j = lo; j < hi; j++) {
+    const uint64_t nb = (jobs[j].total_bits + 7) >> 3;
+    if (nb > jobs[j].out_cap) atomicOr(&bad, 1);
+    sum += nb;
+  }
+  uint64_t x, total;
+  Scan(tmp).ExclusiveSum(sum, x, total);
+  x += out_pos;
+  for (int j = lo; j < hi; j++) {
+    dst_off[j] = x;
+    x += (jobs[j].total_bits + 7) >> 3;
+  }
+  __syncthreads();
+  if (t == 0) {
+    dst_off[k] = out_pos + total;
+    dst_off[k + 1] = bad ? (uint64_t)1 : (out_pos + total > out_cap ? (uint64_t)2 : (uint64_t)0);
+  }
+}
+__global__ void pack_kernel(const Job *jobs, const uint64_t *dst_off, int k, const uint8_t *src, uint8_t *dst) {
+  if (dst_off[k + 1]) return;   // (dst_off_kernel's status: nothing to pack)
   const Job &jb = jobs[blockIdx.y];
   uint64_t n = (jb.total_bits + 7) >> 3;
   const uint8_t *s = src + jb.out_off;
@@ -417,8 +450,10 @@ void launch_emit(hipStream_t st, const Job *jobs, const Mb *mbs, int nmbs, const
 void launch_stored(hipStream_t st, Job *jobs, int njobs, uint8_t *out) {
   hipLaunchKernelGGL(uncompressed_kernel, dim3((unsigned)njobs), dim3(256), 0, st, jobs, njobs, out);
 }
-void launch_pack(hipStream_t st, const Job *jobs, int njobs, const uint64_t *dst_off, const uint8_t *src, uint8_t *dst) {
-  hipLaunchKernelGGL(pack_kernel, dim3(64, (unsigned)njobs), dim3(256), 0, st, jobs, dst_off, src, dst);
+void launch_pack(hipStream_t st, const Job *jobs, int njobs, uint64_t out_pos, uint64_t out_cap, uint64_t *dst_off,
+                 const uint8_t *src, uint8_t *dst) {
+  hipLaunchKernelGGL(dst_off_kernel, dim3(1), dim3(1024), 0, st, jobs, njobs, out_pos, out_cap, dst_off);
+  hipLaunchKernelGGL(pack_kernel, dim3(64, (unsigned)njobs), dim3(256), 0, st, jobs, dst_off, njobs, src, dst);
 }
 
 }  // namespace enc

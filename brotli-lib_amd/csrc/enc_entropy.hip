@@ -285,21 +285,20 @@ __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *s
 
 // ---------------------------------------------------------------- histograms by block type
 // Block per segment, after the split: literal histograms per (block type, context), command
-// histograms per block type, distance-code histograms per (block type, distance context):
+// histograms per block type, distance-code histograms per (block type, distance context),
 // accumulated in LDS (literals one block type at a time) and added to the metablock's with
 // one global atomic per non-zero bin (the histogram pass of storeMetaBlock, metablock.ts:580-640).
 template <int NT>
 __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const Cmd *cmds,
                                                        const uint32_t *cmd_pos, const Unit *units, uint32_t *hl,
                                                        uint32_t *hc, uint32_t *hd) {
+  typedef hipcub::BlockScan<uint32_t, NT> Scan;
+  __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t sh_l[kLitCtx * 256];   // command + distance histograms first, then literals per type
   __shared__ uint8_t ut[kSubPerSeg][3];
-  __shared__ uint32_t sh_present;
+  __shared__ ItemMap<NT> map;
+  __shared__ uint32_t sh_pos[NT], sh_ins[NT];
   uint32_t *sh_c = sh_l, *sh_d = sh_l + kMaxBT * 704;
-  struct LitRows {
-    uint32_t off[64], pos[64];
-  };
-  __shared__ LitRows lit_rows[NT / 64];
   const Seg &sg = segs[blockIdx.x];
   const Job &jb = jobs[sg.job];
   if (jb.uncompressed) return;
@@ -309,12 +308,6 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
   for (int i = t; i < 512; i += NT) lut[i] = kRfcContextLut[(mb.ctx_mode << 9) + i];
   const Unit *un = units + (size_t)blockIdx.x * kSubPerSeg;
   if (t < kSubPerSeg * 3) ut[t / 3][t % 3] = un[t / 3].type[t % 3];
-  if (t == 64) {   // the literal block types this segment's literals fall in
-    uint32_t present = 0;
-#pragma unroll
-    for (int u = 0; u < kSubPerSeg; u++) present |= un[u].nsym[0] ? 1u << un[u].type[0] : 0u;
-    sh_present = present;
-  }
   for (int i = t; i < (int)mb.nbt[1] * 704; i += NT) sh_c[i] = 0;
   for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT) sh_d[i] = 0;
   __syncthreads();
@@ -333,56 +326,58 @@ __global__ __launch_bounds__(NT) void histo_kernel(const Job *jobs, const Seg *s
     if (sh_c[i]) atomicAdd(&hc[(size_t)m * kMaxBT * 704 + i], sh_c[i]);
   for (int i = t; i < (int)mb.nbt[2] * kDistCtx * 128; i += NT)
     if (sh_d[i]) atomicAdd(&hd[(size_t)m * kMaxBT * kDistCtx * 128 + i], sh_d[i]);
-  // The literals, a pass per block type present (its histogram in LDS, flushed with one global
-  // atomic per non-zero bin): a wave per 64 commands (no block barrier), the inserts' offsets by
-  // a wave prefix sum in the wave's LDS rows, each lane's literal found by a six-step search
-  // over them and counted when its unit is of the pass's type.  (The passes used block scans
-  // before, a barrier per 1,024 commands.  Every literal by a global atomic instead slowed the
-  // other encode lane's kernels, C4 encode -2.3 %, and serialised on 16 MiB metablocks' hot
-  // bins, C2 type_histo 0.24 -> 0.70 ms.)
-  uint32_t *hm = hl + (size_t)m * kLitSlots * 256;
-  const int w = t >> 6, ln = t & 63;
-  LitRows &rw = lit_rows[w];
-  const uint32_t present = sh_present;
+  __syncthreads();
+  uint32_t present = 0;   // literal block types used by this segment
+  for (int u = 0; u < kSubPerSeg; u++) present |= 1u << ut[u][0];
   for (int ty = 0; ty < kMaxBT; ty++) {
     if (!(present >> ty & 1)) continue;
-    __syncthreads();
     for (int i = t; i < kLitCtx * 256; i += NT) sh_l[i] = 0;
     __syncthreads();
-    for (uint32_t base = (uint32_t)w * 64; base < n; base += NT) {
-      const uint32_t q = base + ln;
-      uint32_t ins = 0, pos = 0;
-      if (q < n) {
-        ins = c[q].ins;
-        pos = cp[q];
+    for (uint32_t base = 0; base < n; base += NT) {   // the literals of this type, spread over the lanes
+      const uint32_t q = base + t, nb = min((uint32_t)NT, n - base);
+      uint32_t cnt = 0;
+      if (q < n && c[q].ins) {   // the command's literals that lie in units of this type
+        const uint32_t pos = cp[q], ins = c[q].ins;
+        sh_pos[t] = pos;
+        sh_ins[t] = ins;
+        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
+        for (uint32_t v = ulo; v <= uhi; v++)
+          if (ut[v][0] == ty) {
+            const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
+            const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
+            cnt += s1 - s0;
+          }
       }
-      uint32_t x = ins;   // inclusive prefix sum over the wave
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (ln >= o) x += y;
-      }
-      const uint32_t nl = __shfl(x, 63, 64);
-      rw.off[ln] = x - ins;
-      rw.pos[ln] = pos;
-      wave_sync();
-      for (uint32_t i = ln; i < nl; i += 64) {
-        uint32_t j = 0;   // the last command whose offset is <= i (the one owning literal i)
-#pragma unroll
-        for (int s = 32; s; s >>= 1)
-          if (rw.off[j + s] <= i) j += s;
-        const uint32_t lp = rw.pos[j] + i - rw.off[j];
-        if (ut[unit_of(sg, lp)][0] == ty) {
-          const uint32_t p12 = prev2(jb, lp);
-          atomicAdd(&sh_l[(lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp]], 1u);
+      uint32_t off, nlits;
+      Scan(scan_tmp).ExclusiveSum(cnt, off, nlits);
+      map.off[t] = off;
+      if (t == 0) map.off[nb] = nlits;
+      __syncthreads();
+      for (uint32_t i = t; i < nlits; i += NT) {
+        const uint32_t j = map.find(i, nb);
+        // the (i - off)-th of command j's literals in type-ty units (an insert spans few units)
+        const uint32_t pos = sh_pos[j], ins = sh_ins[j];
+        const uint32_t ulo = unit_of(sg, pos), uhi = unit_of(sg, pos + ins - 1);
+        uint32_t k = i - map.off[j], lp = pos;
+        for (uint32_t v = ulo; v <= uhi; v++) {
+          if (ut[v][0] != ty) continue;
+          const uint32_t s0 = v == ulo ? pos : sg.start + (v << kSubBits);
+          const uint32_t s1 = v == uhi ? pos + ins : sg.start + ((v + 1) << kSubBits);
+          if (k < s1 - s0) {
+            lp = s0 + k;
+            break;
+          }
+          k -= s1 - s0;
         }
+        const uint32_t p12 = prev2(jb, lp);
+        atomicAdd(&sh_l[(lut[p12 & 0xFF] | lut[256 + (p12 >> 8)]) * 256 + jb.data[lp]], 1u);
       }
-      wave_sync();   // (the rows are rewritten by the next batch)
+      __syncthreads();
     }
-    __syncthreads();
-    uint32_t *dst = hm + ty * kLitCtx * 256;
+    uint32_t *dst = hl + ((size_t)m * kLitSlots + ty * kLitCtx) * 256;
     for (int i = t; i < kLitCtx * 256; i += NT)
       if (sh_l[i]) atomicAdd(&dst[i], sh_l[i]);
+    __syncthreads();
   }
 }
 
@@ -1554,30 +1549,29 @@ __device__ void split_path(int t, int nu, const uint32_t *ns, const float *ucost
   uint32_t *Xm = reinterpret_cast<uint32_t *>(Sd + kCh * S);   // exit maps
   uint8_t *Pc = reinterpret_cast<uint8_t *>(Xm + kCh), *Qp = Pc + kCh, *Ln = Qp + kCh;
   constexpr float kBig = 1e30f;
-  if (t < nch) {   // chunk transfer matrix
-    float T[S * S];
+  {   // the chunks' transfer matrices: a lane per entry (q, p) = lane S q + p of a chunk's S x S
+      // lanes (64 / S^2 chunks a wave); a column's minimum over q by xor shuffles (a minimum is
+      // exact in any order, so the entries are the serial walk's bit for bit).  (A thread per
+      // chunk took S^2 steps a unit: the cadence's 1 MiB metablocks have 8 chunks of 16 units.)
+    constexpr int kE = S * S, kPer = 64 / kE;   // lanes a chunk, chunks a wave
+    const int lane = t & 63, e = lane % kE, q = e / S;
+    const int nwv = (int)(blockDim.x >> 6);
+    for (int c0 = (t >> 6) * kPer; c0 < nch; c0 += nwv * kPer) {
+      const int c = c0 + lane / kE;   // this lane's chunk (past nch: idle lanes, same steps)
+      float T = (e / S) == (e % S) ? 0.f : kBig;
+      const int ib = c * CL, i1 = min(nu, ib + CL);
+      for (int k = 0; k < CL; k++) {
+        const int i = ib + k;
+        const bool live = c < nch && i < i1 && ns[i] != 0u;
+        float col = T;
 #pragma unroll
-    for (int e = 0; e < S * S; e++) T[e] = (e / S) == (e % S) ? 0.f : kBig;
-    const int i1 = min(nu, (t + 1) * CL);
-    for (int i = t * CL; i < i1; i++) {
-      if (!ns[i]) continue;
-      float col[S];
-#pragma unroll
-      for (int p = 0; p < S; p++) {
-        float v = T[p];
-#pragma unroll
-        for (int q = 1; q < S; q++) v = fminf(v, T[S * q + p]);
-        col[p] = v + sw_cost;
+        for (int o = S; o < kE; o <<= 1) col = fminf(col, __shfl_xor(col, o, 64));
+        col += sw_cost;
+        const float u = live ? ucost[i * S + q] : 0.f;
+        T = live ? fminf(T, col) + u : T;
       }
-#pragma unroll
-      for (int q = 0; q < S; q++) {
-        const float u = ucost[i * S + q];
-#pragma unroll
-        for (int p = 0; p < S; p++) T[S * q + p] = fminf(T[S * q + p], col[p]) + u;
-      }
+      if (c < nch) Tm[c * kE + e] = T;
     }
-#pragma unroll
-    for (int e = 0; e < S * S; e++) Tm[t * S * S + e] = T[e];
   }
   __syncthreads();
   if (t == 0) {   // the costs at every chunk start

@@ -1253,7 +1253,9 @@ extern "C" int mib_debug_read_dp_prof(unsigned long long *out) {
 }
 #endif
 // dp_kernel<4> when there are enough segments for three such waves per SIMD (1024 SIMDs:
-// 256 CUs x 4; 143 VGPRs), dp_kernel<2> when there are enough for one, else dp_kernel<1>.
+// 256 CUs x 4; 143 VGPRs), dp_kernel<2> when there are more than enough for one, else
+// dp_kernel<1> (a cadence update()'s 2,048 pieces of 512 B: 390 -> 343 us a chunk with one
+// piece a wave, two waves a SIMD, r06 kn_ks).
 // Four segments a wave: a step's node fetch, staging and table reads serve four segments and
 // text's short staircases still fit 16 lanes' chunks (C4 dp 91.7 -> 75.3 ms, one encode lane,
 // r04an; in round 3, before the LDS trim, it was slower: 106.6 -> 119.5 ms)
@@ -1263,7 +1265,7 @@ constexpr int kKs4Segs = 3 * 4 * 1024;
 static int dp_ks(int nsegs, bool font) {
   static const int v = knob("MIB_DP_KS") ? atoi(knob("MIB_DP_KS")) : 0;   // experiments
   if (v == 1 || v == 2 || v == 4) return v;
-  return !font && nsegs >= kKs4Segs ? 4 : nsegs < 2048 ? 1 : 2;
+  return !font && nsegs >= kKs4Segs ? 4 : nsegs <= 2048 ? 1 : 2;
 }
 template <bool KD, bool KC>
 static void launch_dp_t(hipStream_t st, const Job *jobs, const Seg *segs, int nsegs, const uint32_t *lit_h,

@@ -523,7 +523,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   Codes *codes = ar.take<Codes>(nm1);
   uint8_t *hdr = ar.take<uint8_t>(nm1 * kHdrBytes);
   uint8_t *trees = ar.take<uint8_t>(nm1 * kTreeSlots * kTreeBytes);
-  uint64_t *d_dst_off = ar.take<uint64_t>(k + 1);
+  uint64_t *d_dst_off = ar.take<uint64_t>(k + 2);   // (+ the pack's status)
   uint8_t *oscr = ar.take<uint8_t>(out_scratch + 64);
   PushSum *push = reinterpret_cast<PushSum *>(ar.take<uint8_t>(ns1 * part_push_bytes()));
   CostModel *model = two_pass ? ar.take<CostModel>(k) : nullptr;
@@ -676,25 +676,23 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   launch_stored(st, d_jobs, (int)k, oscr);
   tm.stop();
   CK(hipGetLastError());
+  // the streams' places in the packed output are summed on the device (dst_off_kernel), and
+  // the jobs come back once, after the pack
+  tm.start("pack");
+  launch_pack(st, d_jobs, (int)k, out_pos, out_cap, d_dst_off, oscr, d_out);
+  tm.stop();
+  CK(hipGetLastError());
+  uint64_t status = 0;
   CK(hipMemcpyAsync(jobs.data(), d_jobs, sizeof(Job) * k, hipMemcpyDeviceToHost, st));
+  CK(hipMemcpyAsync(&status, d_dst_off + k + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   CK(hipStreamSynchronize(st));
-  std::vector<uint64_t> dst(k + 1);
-  dst[0] = out_pos;
+  if (status == 1) return MIB_E_NO_PROGRESS;   // cannot happen: offsets falls back first
+  if (status) return MIB_E_NEED_SPACE;
   for (size_t j = 0; j < k; j++) {
-    const uint64_t nb = (jobs[j].total_bits + 7) >> 3;
-    if (nb > jobs[j].out_cap) return MIB_E_NO_PROGRESS;   // cannot happen: offsets falls back first
-    sizes[j] = nb;
-    dst[j + 1] = dst[j] + nb;
+    sizes[j] = (jobs[j].total_bits + 7) >> 3;
     if (dc_out)
       for (int q = 0; q < 4; q++) dc_out[j][q] = jobs[j].dc_out[q];
   }
-  if (dst[k] > out_cap) return MIB_E_NEED_SPACE;
-  CK(hipMemcpyAsync(d_dst_off, dst.data(), sizeof(uint64_t) * (k + 1), hipMemcpyHostToDevice, st));
-  tm.start("pack");
-  launch_pack(st, d_jobs, (int)k, d_dst_off, oscr, d_out);
-  tm.stop();
-  CK(hipGetLastError());
-  CK(hipStreamSynchronize(st));
   tm.collect();
   return 0;
 }
@@ -1150,7 +1148,8 @@ static int encoder_run(mib_ctx *c, mib_encoder *const *es, const uint64_t *ns, c
     // 1 GiB stream takes 7 encodes instead of 32)
     if (!e->chunk_fixed) e->chunk = std::max(e->chunk, std::min<uint64_t>(kMaxChunk, e->abs / e->block * e->block));
   }
-  CK(hipStreamSynchronize(st));
+  // (no wait for the history moves: the next call's copies and launches are behind them on the
+  // same stream, and a buffer is freed only by hipFree, which waits for the device)
   return 0;
 }
 
