@@ -75,6 +75,11 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=10.0, help='target wall time of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-gather', action='store_true')
+    ap.add_argument('--kernel-events', default=None, choices=['all', 'decode'],
+                    help='c4/c3/c2: HIP events around every kernel of the timed steps (all), or the decoder\'s '
+                         'only, the encoder\'s table then from one untimed step after them (decode). Default: '
+                         'decode, except c3, whose dominant kernel is the encoder\'s DP (events on every kernel '
+                         'cost C4 ~1.3 %% of its MB/s, 2.3 %% of its encode)')
     ap.add_argument('--stream-chunk', type=int, default=32, help='c5: BrotliEncoder streamChunk in MiB (0: the reference\'s cadence)')
     ap.add_argument('--gpus-in-lib', type=int, default=0,
                     help='host-API leg: the batch through mib_*_batch_n with N shards against the one-context batch')
@@ -247,15 +252,23 @@ def run_stream(args, rank, world, local):
         raise SystemExit('c5 round trip FAILED')
     if world > 1:
         dist.barrier()
-    brotli_amd.default_profiling(True)
+    # The encode loop runs without kernel events (a reference-cadence update() is one launch
+    # sequence of ~2.8 ms, with ~25 event pairs in it); the decode loop times the
+    # decoder (its kernel is the leg's dominant one: the roofline's launch time comes from the
+    # timed region); one more, untimed, encode fills the encoder's kernel table.
+    brotli_amd.default_profiling(False)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         stream = enc()
     t1 = time.perf_counter()
+    brotli_amd.default_profiling('decode')
     for _ in range(args.steps):
         out = brotli_amd.brotliDecode(stream, {'customDictionary': cdict})
     t2 = time.perf_counter()
-    times = brotli_amd.default_kernel_times()
+    times = brotli_amd.default_kernel_times()   # (the decoder's: the timed region)
+    brotli_amd.default_profiling(True)
+    enc()   # (untimed: the encoder's kernel table, one step)
+    enc_times = brotli_amd.default_kernel_times()
     brotli_amd.default_profiling(False)
     assert out == data
     del out
@@ -267,11 +280,10 @@ def run_stream(args, rank, world, local):
         dt, te, td = (float(x) for x in t.tolist())
     if rank == 0:
         mb = world * size / 1e6
-        # the dominant kernel: the longest launch (the encode lanes' kernels run concurrently,
-        # so their summed time is not time on the chip's clock)
+        # the dominant kernel: the longest launch of the timed region's (the decoder's: every
+        # encoder launch covers one device chunk of the stream and is far shorter); decode
+        # launches cover the whole stream
         dom_name, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0] / max(1, kv[1][1]))
-        # the dominant kernel: decode launches cover the whole stream, encoder launches one
-        # device chunk each (update() hands the device whole chunks of the stream)
         launches_per_step = max(1, dom_n // args.steps)
         launch_bytes = (size + len(stream)) // launches_per_step
         avg_ms = dom_ms / max(1, dom_n)
@@ -323,7 +335,10 @@ def run_stream(args, rank, world, local):
                        'custom_dictionary_bytes': len(cdict), 'parallelism': 'replicas%d' % world},
             'encode_MBps': round(mb / te, 3), 'decode_MBps': round(mb / td, 3),
             'compressed_ratio': round(len(stream) / size, 5),
-            'kernel_ms_per_step': {n: round(v[0] / args.steps, 3) for n, v in sorted(times.items())},
+            'kernel_ms_per_step': dict(sorted(list({n: round(v[0] / args.steps, 3) for n, v in times.items()}.items()) +
+                                              list({n: round(v[0], 3) for n, v in enc_times.items()}.items()))),
+            'kernel_times_from': 'decoder: the timed decode loop; encoder: one untimed encode step after it (the '
+                                 'timed encode loop runs without kernel events)',
             'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 3), 'peak': PEAK_HBM_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 6),
                          'traffic': load_traffic(dom_name, 'c5' if args.stream_chunk else 'c5cad'),
@@ -628,6 +643,10 @@ def main():
     gpu_sizes = [out_off[i + 1] - out_off[i] for i in range(k)]
 
     times = {}
+    if args.kernel_events is None:
+        args.kernel_events = 'all' if wl == 'c3' else 'decode'
+    if args.kernel_events == 'decode':
+        ctx.set_profiling('decode')
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -638,6 +657,15 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    timed = set(times)   # (the kernels the timed steps' events measured: the roofline's candidates)
+    if args.kernel_events == 'decode':   # the encoder's kernel table: one untimed step, scaled
+        ctx.set_profiling(True)
+        extra = {}
+        step(extra)
+        torch.cuda.synchronize()
+        for n, (ms, c) in extra.items():
+            if n not in times:
+                times[n] = [ms * args.steps, c * args.steps]
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -676,7 +704,8 @@ def main():
         dec_ms = walls[' decode_wall'][0] / args.steps
         # the dominant kernel: the longest launch (the encode lanes' kernels run concurrently,
         # so their summed time is not time on the chip's clock)
-        dom_name, (dom_ms, dom_n) = max(times.items(), key=lambda kv: kv[1][0] / max(1, kv[1][1]))
+        dom_name, (dom_ms, dom_n) = max(((n, v) for n, v in times.items() if n in timed),
+                                        key=lambda kv: kv[1][0] / max(1, kv[1][1]))
         # a kernel launched L times per step covers 1/L of the batch per launch
         launches_per_step = max(1, dom_n // args.steps)
         launch_bytes = (total + comp_bytes) // launches_per_step
@@ -709,6 +738,7 @@ def main():
             'compressed_ratio': round(comp_all / (world * total), 5),
             'ratio_same_sample': ratios,
             'kernel_ms_per_step': {n: round(v[0] / args.steps, 3) for n, v in sorted(times.items())},
+            'kernel_events': args.kernel_events,
             'roofline': {'bound': 'hbm', 'kernel': dom_name, 'achieved': round(achieved, 3), 'peak': PEAK_HBM_GBS,
                          'unit': 'GB/s', 'frac': round(achieved / PEAK_HBM_GBS, 6),
                          'traffic': load_traffic(dom_name, wl),

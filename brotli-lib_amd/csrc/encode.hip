@@ -543,7 +543,7 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   uint32_t *d_any_binary = cache ? ar.take<uint32_t>(1) : nullptr;
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
-  Timer tm{ctx, st, mib_ctx_profiling(ctx) != 0, {}};
+  Timer tm{ctx, st, mib_ctx_profiling(ctx) == 1, {}};   // (2: the decoder's kernels only)
   CK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(Job) * k, hipMemcpyHostToDevice, st));
   if (nsegs) CK(hipMemcpyAsync(d_segs, segs.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
   if (nmbs) CK(hipMemcpyAsync(d_mbs, mbs.data(), sizeof(Mb) * nmbs, hipMemcpyHostToDevice, st));

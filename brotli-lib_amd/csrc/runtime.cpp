@@ -342,7 +342,7 @@ struct mib_ctx {
   // part decoding counters (streams decoded part-parallel / sent back to the serial decoder)
   uint64_t parts_used = 0, parts_fallback = 0;
   // profiling
-  bool profiling = false;
+  int profiling = 0;   // 0 off, 1 every kernel, 2 the decoder's only (mib_ctx_set_profiling)
   std::vector<mib_kernel_time> times;
   std::mutex times_mu;   // (two encode lanes collect at once)
   void add_time(const char *name, double ms) {
@@ -363,7 +363,7 @@ struct mib_ctx {
 };
 
 extern "C" void mib_ctx_add_time(mib_ctx *c, const char *name, double ms) { c->add_time(name, ms); }
-extern "C" int mib_ctx_profiling(mib_ctx *c) { return c->profiling ? 1 : 0; }
+extern "C" int mib_ctx_profiling(mib_ctx *c) { return c->profiling; }
 extern "C" void **mib_ctx_enc_ws(mib_ctx *c) { return &c->enc_ws; }
 // encode lane l (1 .. kEncLanes - 1): its workspace slot, its stream (created on first use, on
 // the context's device)
@@ -797,7 +797,7 @@ void mib_ctx_free(mib_ctx *c) {
   delete c;
 }
 
-void mib_ctx_set_profiling(mib_ctx *c, int on) { c->profiling = on != 0; }
+void mib_ctx_set_profiling(mib_ctx *c, int on) { c->profiling = on == 2 ? 2 : on != 0 ? 1 : 0; }
 
 void mib_part_stats(mib_ctx *c, uint64_t *parallel, uint64_t *fallback) {
   if (!c) c = default_ctx();

@@ -377,14 +377,20 @@ def part_stats(ctx=None):
     return a.value, b.value
 
 
-def default_profiling(on=True):
+def _prof_mode(on):
+    return 2 if on == 'decode' else (1 if on else 0)
+
+
+def default_profiling(on=True, clear=True):
     """Per-kernel timing (HIP events) of the host-buffer calls (brotliEncode, brotliDecode,
-    BrotliEncoder, the batches): on / off, and the accumulated times cleared."""
+    BrotliEncoder, the batches): on / off / 'decode' (the decoder's kernels only), and the
+    accumulated times cleared unless clear=False."""
     c = _L().mib_default_ctx()
     if not c:
         raise BrotliError('brotli_amd: no usable device')
-    _L().mib_ctx_set_profiling(c, 1 if on else 0)
-    _L().mib_ctx_clear_times(c)
+    _L().mib_ctx_set_profiling(c, _prof_mode(on))
+    if clear:
+        _L().mib_ctx_clear_times(c)
 
 
 def default_kernel_times():
@@ -403,7 +409,11 @@ class DeviceContext:
         self._c = _L().mib_ctx_new(device)
         if not self._c:
             raise BrotliError('brotli_amd: no usable device %d' % device)
-        _L().mib_ctx_set_profiling(self._c, 1 if profiling else 0)
+        _L().mib_ctx_set_profiling(self._c, _prof_mode(profiling))
+
+    def set_profiling(self, on):
+        """True / False / 'decode' (the decoder's kernels only)."""
+        _L().mib_ctx_set_profiling(self._c, _prof_mode(on))
 
     def close(self):
         if getattr(self, '_c', None) and _lib is not None:

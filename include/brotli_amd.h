@@ -160,6 +160,8 @@ int mib_ctx_decode(mib_ctx *c, const uint8_t *d_in, const uint64_t *in_offsets, 
 /* Per-kernel device time of the last mib_ctx_* call (ms, HIP events on the launch stream). */
 typedef struct { char name[32]; double ms; uint32_t launches; } mib_kernel_time;
 int mib_ctx_kernel_times(mib_ctx *c, mib_kernel_time *out, int max);
+/* on: 0 off, 1 every kernel, 2 the decoder's kernels only (one event pair a decode call; the
+ * encoder's ~25 event pairs a call are overhead a small call notices). */
 void mib_ctx_set_profiling(mib_ctx *c, int on);
 /* The context behind the host-buffer entry points (mib_encode, mib_decode, the batches,
  * BrotliEncoder), created on first use (NULL without a device): for profiling them.  Its
