@@ -544,23 +544,32 @@ int encode_group(mib_ctx *ctx, const Params &prm, const StreamDesc *sd, size_t k
   if (ar.off > ws->cap) return MIB_E_OUT_OF_MEMORY;
 
   Timer tm{ctx, st, mib_ctx_profiling(ctx) == 1, {}};   // (2: the decoder's kernels only)
-  CK(hipMemcpyAsync(d_jobs, jobs.data(), sizeof(Job) * k, hipMemcpyHostToDevice, st));
-  if (nsegs) CK(hipMemcpyAsync(d_segs, segs.data(), sizeof(Seg) * nsegs, hipMemcpyHostToDevice, st));
-  if (nmbs) CK(hipMemcpyAsync(d_mbs, mbs.data(), sizeof(Mb) * nmbs, hipMemcpyHostToDevice, st));
+  {   // the descriptors (jobs, segments, metablocks, position -> job / segment) lie back to back
+      // in the arena (taken in that order): one upload of their image
+    uint8_t *const d0 = reinterpret_cast<uint8_t *>(d_jobs);
+    const size_t end = (size_t)(reinterpret_cast<uint8_t *>(d_seg_ref + seg_ref.size()) - d0);
+    std::vector<uint8_t> img(end);
+    auto put = [&](const void *dst, const void *src, size_t n) {
+      if (n) memcpy(img.data() + (reinterpret_cast<const uint8_t *>(dst) - d0), src, n);
+    };
+    put(d_jobs, jobs.data(), sizeof(Job) * k);
+    put(d_segs, segs.data(), sizeof(Seg) * nsegs);
+    put(d_mbs, mbs.data(), sizeof(Mb) * nmbs);
+    put(d_seg_job, seg_job.data(), seg_job.size() * 4);
+    put(d_seg_ref, seg_ref.data(), seg_ref.size() * sizeof(SegRef));
+    CK(hipMemcpyAsync(d0, img.data(), end, hipMemcpyHostToDevice, st));
+  }
   // the sampled first iteration's and the parse pieces' segment tables, derived on the device
   // (the pieces' table of a C4 call is 12.6 MB: built on the host it was a host loop and a
   // pageable copy every call)
   if (nsegs) launch_derive_segs(st, d_segs, nsegs, sampled ? zopfli_sample() : 0u, d_sample, d_pieces);
   Seg *const d_fin = ps ? d_pieces : d_segs;   // the final parse's segment table
   const int nfin = ps ? (int)npieces : nsegs;
-  CK(hipMemcpyAsync(d_seg_job, seg_job.data(), seg_job.size() * 4, hipMemcpyHostToDevice, st));
-  CK(hipMemcpyAsync(d_seg_ref, seg_ref.data(), seg_ref.size() * sizeof(SegRef), hipMemcpyHostToDevice, st));
   CK(hipMemsetAsync(oscr, 0, out_scratch + 64, st));
   if (nsegs) {
-    CK(hipMemsetAsync(lit_h, 0, k * 256 * 4, st));
-    CK(hipMemsetAsync(hl, 0, nm1 * kLitSlots * 256 * 4, st));
-    CK(hipMemsetAsync(hc, 0, nm1 * kMaxBT * 704 * 4, st));
-    CK(hipMemsetAsync(hd, 0, nm1 * kMaxBT * kDistCtx * 128 * 4, st));
+    // lit_h, hl, hc, hd lie back to back in the arena (taken in that order): one memset
+    CK(hipMemsetAsync(lit_h, 0, reinterpret_cast<uint8_t *>(hd + nm1 * kMaxBT * kDistCtx * 128) -
+                                    reinterpret_cast<uint8_t *>(lit_h), st));
     CK(hipMemsetAsync(choice, 0, ((size_t)total + 1) * 8, st));
     const int depth = (int)env_u32("MIB_DEPTH", (uint32_t)depth_for_quality(prm.quality), 1, 64);   // override: experiments
     // (a batch of many metablocks fills the chip with each launch: there the independent
