@@ -153,7 +153,7 @@ __global__ __launch_bounds__(64) void context_mode_kernel(const Job *jobs, Mb *m
 template <int NT>
 __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *segs, const Mb *mbs, const RawCmd *raw,
                                                        Cmd *cmds, uint32_t *cmd_pos, Unit *units, uint32_t *unit_h) {
-  typedef hipcub::BlockScan<uint32_t, NT> Scan;
+  typedef hipcub::BlockScan<uint64_t, NT> Scan;
   __shared__ typename Scan::TempStorage scan_tmp;
   __shared__ uint32_t sh_h[kSubPerSeg * kSubHist];
   __shared__ uint32_t sh_n[kSubPerSeg][3], sh_first[kSubPerSeg][3];
@@ -192,15 +192,20 @@ __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *s
     } else if (q < n) {
       ins = sg.extra_ins;
     }
-    uint32_t off, total;
-    Scan(scan_tmp).ExclusiveSum(ins + len, off, total);
-    const uint32_t pos = sh_run + off;
     // the decoder's distance ring before this command: pushes of the batch before it (by
     // rank), then the ring the batch started with
     const uint32_t push = (q < nraw && !is_word(jb, d) && d != prevd) ? 1u : 0u;   // dictionary words never push
-    uint32_t rank, npush;
-    __syncthreads();
-    Scan(scan_tmp).ExclusiveSum(push, rank, npush);
+    // one block scan of three packed counts, each field wide enough for its batch total (no
+    // carries between fields): bytes, insert + copy, bits 35-63 (< 2^24 carried literals of
+    // a <= 16 MiB metablock + the segment); literals, bits 10-34 (< 2^25); ring pushes, bits
+    // 0-9 (<= NT)
+    static_assert(NT < 1024, "the pushes' field");
+    uint64_t ex, tot;
+    Scan(scan_tmp).ExclusiveSum(((uint64_t)(ins + len) << 35) | ((uint64_t)ins << 10) | push, ex, tot);
+    const uint32_t off = (uint32_t)(ex >> 35), total = (uint32_t)(tot >> 35);
+    const uint32_t loff = (uint32_t)(ex >> 10) & 0x1FFFFFFu, nlits = (uint32_t)(tot >> 10) & 0x1FFFFFFu;
+    const uint32_t rank = (uint32_t)ex & 0x3FFu, npush = (uint32_t)tot & 0x3FFu;
+    const uint32_t pos = sh_run + off;
     if (push) sh_push[rank] = d;
     __syncthreads();
     uint32_t ring[4];
@@ -253,8 +258,6 @@ __global__ __launch_bounds__(NT) void codes_kernel(const Job *jobs, const Seg *s
     }
     // the literals of the batch, spread over the lanes (items = inserts, see ItemMap)
     sh_pos[t] = pos;
-    uint32_t loff, nlits;
-    Scan(scan_tmp).ExclusiveSum(q < n ? ins : 0u, loff, nlits);
     const uint32_t nb = min((uint32_t)NT, n - base);
     map.off[t] = loff;
     if (t == 0) map.off[nb] = nlits;
