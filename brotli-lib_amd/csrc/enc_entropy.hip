@@ -1540,7 +1540,7 @@ __device__ void block_scan2(int t, int n, FA fa, FB fb, uint32_t *ea, uint32_t *
 // the same sums as ever; else kMaxBT).  Scratch (in th): the
 // chunks' S x S matrices, their start costs, exit maps (3 bits per state) and handed states.
 // ucost rows are S wide.
-template <int S>
+template <int S, bool kLanes>
 __device__ void split_path(int t, int nu, const uint32_t *ns, const float *ucost, uint8_t *asg, uint16_t *bp,
                            uint32_t *scratch, float sw_cost) {
   constexpr int kCh = S <= 4 ? kPathChunks : kPathChunks / 2;   // (the scratch fits th either way)
@@ -1600,7 +1600,44 @@ __device__ void split_path(int t, int nu, const uint32_t *ns, const float *ucost
     Pc[kCh - 1] = (uint8_t)cur;   // (handed to the last chunk below)
   }
   __syncthreads();
-  if (t < nch) {   // replay: the serial walk's switch bits, then the chunk's exit map
+  if constexpr (kLanes) {   // replay: the serial walk's switch bits, then the chunk's exit map -- a lane per state q
+      // of a chunk's S lanes (64 / S chunks a wave).  The unit's best state is the group's
+      // minimum (exact in any order) and, as the serial scan's strict '<' picks, the lowest q
+      // holding it below 1e30; the exit map walks back a lane per entry state.
+    constexpr int kPer = 64 / S;
+    const int lane = t & 63, q = lane % S, g = lane / S;
+    const uint64_t gmask = (S == 64 ? ~0ull : ((1ull << S) - 1)) << (g * S);
+    const int nwv = (int)(blockDim.x >> 6);
+    for (int c0 = (t >> 6) * kPer; c0 < nch; c0 += nwv * kPer) {
+      const int c = c0 + g;   // (past nch: idle lanes, same steps)
+      const int i0 = c * CL, i1 = min(nu, i0 + CL);
+      float dq = c < nch ? Sd[c * S + q] : 0.f;
+      for (int k = 0; k < CL; k++) {
+        const int i = i0 + k;
+        const bool live = c < nch && i < i1 && ns[i] != 0u;
+        float m = dq;
+#pragma unroll
+        for (int o = 1; o < S; o <<= 1) m = fminf(m, __shfl_xor(m, o, 64));
+        const float best = fminf(m, 1e30f);
+        const uint64_t eq = __ballot(dq == best && dq < 1e30f) & gmask;
+        const int bq = eq ? (__ffsll((unsigned long long)(eq >> (g * S))) - 1) : 0;
+        const float sw = best + sw_cost;
+        const bool sv = sw < dq;   // (never at the first unit: every cost is 0 there)
+        const uint32_t bb = (uint32_t)((__ballot(sv) & gmask) >> (g * S));
+        const float nd = (sv ? sw : dq) + (live ? ucost[i * S + q] : 0.f);
+        if (live && q == 0) bp[i] = (uint16_t)(bb | (uint32_t)(bq << 8));
+        dq = live ? nd : dq;
+      }
+      wave_sync();   // (bp of this wave's chunks, written by their lanes q = 0)
+      int cur = q;
+      for (int i = i1 - 1; i >= i0; i--)
+        if (c < nch && ns[i] && (bp[i] >> cur & 1)) cur = bp[i] >> 8;
+      uint32_t xm = (uint32_t)cur << (3 * q);
+#pragma unroll
+      for (int o = 1; o < S; o <<= 1) xm |= (uint32_t)__shfl_xor((int)xm, o, 64);
+      if (c < nch && q == 0) Xm[c] = xm;
+    }
+  } else if (t < nch) {   // (a thread per chunk: the batch build, whose registers the lane form raised past three waves a SIMD, C4 -0.8 %)
     float dp[S];
 #pragma unroll
     for (int q = 0; q < S; q++) dp[q] = Sd[t * S + q];
@@ -1904,7 +1941,7 @@ __global__ __launch_bounds__(NT) void split_kernel(const Job *jobs, Mb *mbs, int
       // (the switch bits), and the backtrack runs per chunk from the state handed in from
       // the right (one thread chains the chunks' exit maps).  Scratch: th, which the next
       // iteration recomputes.
-      split_path<S>(t, nu, ns, ucost, asg, bp, &th[0][0], sw_cost);
+      split_path<S, NT == 1024>(t, nu, ns, ucost, asg, bp, &th[0][0], sw_cost);
       __syncthreads();
       SPMARK(5);
     }
